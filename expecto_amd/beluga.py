@@ -1,0 +1,185 @@
+"""Drop-in ``Beluga`` module backed by the gfx950 HIP kernels.
+
+Mirrors the reference operator API (``Beluga.py:18-51``): the same ``nn.Module`` tree,
+so ``state_dict()`` keys are exactly ``model.0.{0,2,6,8,12,14}.{weight,bias}``,
+``model.1.2.1.{weight,bias}``, ``model.1.4.1.{weight,bias}`` and a strict
+``load_state_dict(torch.load(pth))`` of the reference checkpoint works unchanged
+(``chromatin.py:102-106``).  Constructing the layers in the reference order also
+reproduces the reference's default initialisation bit for bit under the same seed.
+
+``forward(x)`` takes ``x`` = ``[B,4,1,2000]`` (or ``[B,4,2000]``) fp32 on the GPU and
+returns ``[B,2002]`` sigmoid outputs, computed by ``libexpecto_hip.so``.  There is no
+CPU path: a CPU tensor, or a missing library, raises ``RuntimeError``.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+from torch import nn
+
+from . import _lib
+
+PARAM_KEYS = (
+    "model.0.0.weight", "model.0.0.bias", "model.0.2.weight", "model.0.2.bias",
+    "model.0.6.weight", "model.0.6.bias", "model.0.8.weight", "model.0.8.bias",
+    "model.0.12.weight", "model.0.12.bias", "model.0.14.weight", "model.0.14.bias",
+    "model.1.2.1.weight", "model.1.2.1.bias", "model.1.4.1.weight", "model.1.4.1.bias",
+)
+INPUT_LEN = 2000
+N_FEATURES = 2002
+
+
+class _Flatten(nn.Module):
+    """Stands where the reference has ``Lambda(lambda x: x.view(...))`` (no parameters)."""
+
+    def forward(self, x):
+        return x.reshape(x.size(0), -1)
+
+
+class BelugaEngine:
+    """Owns one ``expecto_beluga_t`` handle (weights repacked on the device + workspace)."""
+
+    def __init__(self, params: list, device: int, max_batch: int = 1024, stream=None):
+        self.lib = _lib.load()
+        if len(params) != len(PARAM_KEYS):
+            raise RuntimeError("Beluga needs 16 parameter tensors")
+        ptrs = (ctypes.c_void_p * len(params))()
+        for i, p in enumerate(params):
+            if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()):
+                raise RuntimeError(f"parameter {PARAM_KEYS[i]} must be a contiguous fp32 device tensor")
+            ptrs[i] = p.data_ptr()
+        h = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            _lib.check(self.lib.expecto_beluga_create(device, ptrs, int(max_batch), _lib.stream_ptr(stream),
+                                                      ctypes.byref(h)), "expecto_beluga_create")
+        self.handle = h
+        self.device = device
+        self.max_batch = max_batch
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            self.lib.expecto_beluga_destroy(h)
+            self.handle = None
+
+    def forward_onehot(self, x: torch.Tensor, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+        if x.dim() == 4:
+            if x.shape[2] != 1:
+                raise RuntimeError("expected input [B,4,1,2000]")
+            x3 = x
+        elif x.dim() == 3:
+            x3 = x
+        else:
+            raise RuntimeError("expected input [B,4,1,2000] or [B,4,2000]")
+        if x3.shape[1] != 4 or x3.shape[-1] != INPUT_LEN:
+            raise RuntimeError(f"expected 4 channels x {INPUT_LEN} positions, got {tuple(x.shape)}")
+        if x3.dtype != torch.float32:
+            raise RuntimeError("input must be float32")
+        if not x3.is_contiguous():
+            # the reference fails on non-contiguous input at x.view (Beluga.py:42)
+            raise RuntimeError("view size is not compatible with input tensor's size and stride "
+                               "(input must be contiguous)")
+        n = x3.shape[0]
+        if out is None:
+            out = torch.empty((n, N_FEATURES), device=x3.device, dtype=torch.float32)
+        _lib.check(self.lib.expecto_beluga_forward_onehot(self.handle, _lib.dptr(x3), n, _lib.dptr(out),
+                                                          _lib.stream_ptr(stream)), "forward_onehot")
+        return out
+
+    def forward_codes(self, codes: torch.Tensor, strand_mode: int = _lib.STRAND_BOTH,
+                      out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+        if codes.dtype != torch.uint8 or codes.dim() != 2 or codes.shape[1] < INPUT_LEN:
+            raise RuntimeError("codes must be uint8 [n, >=2000]")
+        if codes.stride(1) != 1:
+            raise RuntimeError("codes rows must be contiguous")
+        n = codes.shape[0]
+        rows = 2 * n if strand_mode == _lib.STRAND_BOTH else n
+        if out is None:
+            out = torch.empty((rows, N_FEATURES), device=codes.device, dtype=torch.float32)
+        _lib.check(self.lib.expecto_beluga_forward_codes(self.handle, _lib.dptr(codes), n, codes.stride(0),
+                                                         int(strand_mode), _lib.dptr(out),
+                                                         _lib.stream_ptr(stream)), "forward_codes")
+        return out
+
+    def set_profiling(self, on: bool):
+        _lib.check(self.lib.expecto_beluga_set_profiling(self.handle, int(on)), "set_profiling")
+
+    def layer_times(self):
+        ms = (ctypes.c_double * _lib.N_LAYERS)()
+        calls = (ctypes.c_longlong * _lib.N_LAYERS)()
+        n = self.lib.expecto_beluga_layer_times(self.handle, ms, calls, _lib.N_LAYERS)
+        if n < 0:
+            _lib.check(n, "layer_times")
+        return {_lib.LAYER_NAMES[i]: (ms[i], calls[i]) for i in range(_lib.N_LAYERS)}
+
+    def device_bytes(self) -> int:
+        return int(self.lib.expecto_beluga_device_bytes(self.handle))
+
+
+class Beluga(nn.Module):
+    """Reference-compatible Beluga (Beluga.py:18-48) whose forward runs on gfx950 HIP kernels."""
+
+    def __init__(self, max_batch: int = 1024):
+        super().__init__()
+        self.model = nn.Sequential(
+            nn.Sequential(
+                nn.Conv2d(4, 320, (1, 8)), nn.ReLU(),
+                nn.Conv2d(320, 320, (1, 8)), nn.ReLU(), nn.Dropout(0.2), nn.MaxPool2d((1, 4), (1, 4)),
+                nn.Conv2d(320, 480, (1, 8)), nn.ReLU(),
+                nn.Conv2d(480, 480, (1, 8)), nn.ReLU(), nn.Dropout(0.2), nn.MaxPool2d((1, 4), (1, 4)),
+                nn.Conv2d(480, 640, (1, 8)), nn.ReLU(),
+                nn.Conv2d(640, 640, (1, 8)), nn.ReLU(),
+            ),
+            nn.Sequential(
+                nn.Dropout(0.5), _Flatten(),
+                nn.Sequential(nn.Identity(), nn.Linear(67840, 2003)), nn.ReLU(),
+                nn.Sequential(nn.Identity(), nn.Linear(2003, 2002)),
+            ),
+            nn.Sigmoid(),
+        )
+        self.max_batch = max_batch
+        self._engine = None
+        self._engine_key = None
+
+    # -- engine management: rebuilt whenever the parameters change (load_state_dict, .cuda())
+    def _params(self):
+        sd = dict(self.named_parameters())
+        return [sd[k] for k in PARAM_KEYS]
+
+    def _key(self, params):
+        return tuple((p.data_ptr(), p._version) for p in params)
+
+    def engine(self) -> BelugaEngine:
+        params = self._params()
+        key = self._key(params)
+        if self._engine is None or self._engine_key != key:
+            dev = params[0].device
+            if dev.type != "cuda":
+                raise RuntimeError("Beluga parameters are on the CPU: call .cuda() first "
+                                   "(the MI355X engine has no CPU path)")
+            self._engine = None
+            self._engine = BelugaEngine([p.detach().contiguous() for p in params], dev.index or 0, self.max_batch)
+            self._engine_key = key
+        return self._engine
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not x.is_cuda:
+            raise RuntimeError("Beluga.forward needs a device tensor (input.cuda()); there is no CPU path")
+        return self.engine().forward_onehot(x)
+
+    def forward_codes(self, codes: torch.Tensor, strand_mode: int = _lib.STRAND_BOTH) -> torch.Tensor:
+        return self.engine().forward_codes(codes, strand_mode)
+
+
+def seeded(seed: int = 0, gain: float | None = None, max_batch: int = 1024) -> Beluga:
+    """``torch.manual_seed(seed); Beluga()`` -- same RNG stream as the reference -- with every
+    weight optionally scaled by ``gain`` (the golden vectors use sqrt(6))."""
+    torch.manual_seed(seed)
+    m = Beluga(max_batch=max_batch)
+    if gain is not None:
+        with torch.no_grad():
+            for k, p in m.named_parameters():
+                if k.endswith(".weight"):
+                    p.mul_(gain)
+    return m.eval()

@@ -1,0 +1,657 @@
+// Beluga forward for MI355X (gfx950 / CDNA4): conv1 one-hot kernel + fp32-MFMA
+// implicit-GEMM kernels with fused bias/ReLU/MaxPool/Sigmoid epilogues.
+//
+// Replaces the ATen ops launched by Beluga.forward (reference Beluga.py:18-51,
+// SURVEY.md 2.2).  Layout in HBM (per window, channel-last, fp32):
+//   act0 [2000][320]  conv1 out (1993 valid)          -> buffer P
+//   act1 [ 500][320]  conv2+pool (496 valid)          -> buffer Q
+//   act2 [ 500][480]  conv3 (489 valid)               -> buffer P
+//   act3 [ 125][480]  conv4+pool (120 valid)          -> buffer Q
+//   act4 [ 125][640]  conv5 (113 valid)               -> buffer P
+//   act5 [ 125][640]  conv6 (106 valid)               -> buffer Q
+// With channel-last rows the im2col row of output position t of a k=8 conv is the
+// CONTIGUOUS slice X[t*Cin : (t+8)*Cin], so every conv is a GEMM with an overlapping
+// (Toeplitz) A operand: A[m][k] = X[m*Cin + k], K = 8*Cin, B = W repacked [Cout][tap*Cin+ci].
+// FC1 reads the first 106 rows of act5 as one 67840-long row (weights permuted from the
+// reference flatten order c*106+t to t*640+c).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+namespace expecto {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int kLen = 2000;         // input window (chromatin.py:35-36, fixed by FC1)
+constexpr int kNFeat = 2002;
+constexpr int kFc1In = 67840;      // 640 * 106
+constexpr int kFc1Out = 2003;
+constexpr int kHidLd = 2016;       // FC1 output row stride = FC2 K (2003 padded to 32)
+
+// GEMM tile: 128 rows x 160 cols x 32 k, 4 waves stacked along M (each 32 x 160 =
+// five 32x32 accumulators of v_mfma_f32_32x32x2_f32).
+constexpr int GBM = 128;
+constexpr int GBN = 160;
+constexpr int GBK = 32;
+constexpr int LDS_STRIDE = GBK + 4;  // 144-B rows: ds_read_b128 lane groups conflict-free
+constexpr int GTN = GBN / 32;
+
+enum { EPI_RELU = 0, EPI_RELU_POOL4 = 1, EPI_SIGMOID = 2, EPI_PARTIAL = 3 };
+
+struct GemmArgs {
+  const float* A;
+  long long lda;
+  long long M;
+  const float* B;  // [Npad][ldb], K-contiguous
+  long long ldb;
+  int kper;        // K range per split, multiple of GBK
+  int n_tiles;
+  long long m_tiles;
+  int m_fastest;
+  const float* bias;
+  float* C;
+  long long ldc;
+  int n_store;
+  int s_in;     // rows per window in the A/M index space
+  int t_valid;  // valid output positions (pooled count for EPI_RELU_POOL4)
+  int s_out;    // rows per window in C
+  long long split_stride;
+};
+
+// LAYER only makes the symbol distinct per layer (rocprof attributes time per layer).
+template <int LAYER, int EPI>
+__global__ __launch_bounds__(256, 2) void beluga_gemm(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) float smem[(GBM + GBN) * LDS_STRIDE];
+  float* As = smem;
+  float* Bs = smem + GBM * LDS_STRIDE;
+
+  // XCD-aware remap: blocks b, b+8, b+16.. share an XCD; give them consecutive tiles.
+  const unsigned nblk = gridDim.x, bid = blockIdx.x;
+  const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
+  const unsigned lin = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  long long mt;
+  int nt, ks;
+  if (p.m_fastest) {
+    mt = lin % p.m_tiles;
+    const long long rest = lin / p.m_tiles;
+    nt = (int)(rest % p.n_tiles);
+    ks = (int)(rest / p.n_tiles);
+  } else {
+    nt = (int)(lin % (unsigned)p.n_tiles);
+    const long long rest = lin / (unsigned)p.n_tiles;
+    mt = rest % p.m_tiles;
+    ks = (int)(rest / p.m_tiles);
+  }
+
+  const int tid = threadIdx.x;
+  const int lr = tid >> 3, lc = (tid & 7) << 2;
+  const long long m0 = mt * GBM;
+  const int n0 = nt * GBN;
+  const long long kb = (long long)ks * p.kper;
+
+  const float* ag[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    long long m = m0 + lr + 32 * i;
+    if (m > p.M - 1) m = p.M - 1;  // clamp: tail rows read valid memory, never stored
+    ag[i] = p.A + m * p.lda + kb + lc;
+  }
+  const float* bg[GTN];
+#pragma unroll
+  for (int i = 0; i < GTN; ++i) bg[i] = p.B + (long long)(n0 + lr + 32 * i) * p.ldb + kb + lc;
+
+  floatx4 ra[4], rb[GTN];
+  const int wave = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
+  floatx16 acc[GTN];
+#pragma unroll
+  for (int t = 0; t < GTN; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  // k order inside a 32-deep stage: MFMA step s = 4g+qq, lane half h takes k = 8g+4h+qq,
+  // so each lane feeds 4 consecutive MFMAs from one ds_read_b128 (same order for A and B).
+  const float* aw = As + (wave * 32 + li) * LDS_STRIDE + 4 * lh;
+  const float* bw = Bs + li * LDS_STRIDE + 4 * lh;
+  const int nk = p.kper / GBK;
+
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ra[i] = *(const floatx4*)(ag[i]);
+#pragma unroll
+  for (int i = 0; i < GTN; ++i) rb[i] = *(const floatx4*)(bg[i]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) *(floatx4*)(As + (lr + 32 * i) * LDS_STRIDE + lc) = ra[i];
+#pragma unroll
+  for (int i = 0; i < GTN; ++i) *(floatx4*)(Bs + (lr + 32 * i) * LDS_STRIDE + lc) = rb[i];
+  __syncthreads();
+
+  for (int s = 0; s < nk; ++s) {
+    const bool more = (s + 1) < nk;
+    if (more) {
+      const int k0 = (s + 1) * GBK;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ra[i] = *(const floatx4*)(ag[i] + k0);
+#pragma unroll
+      for (int i = 0; i < GTN; ++i) rb[i] = *(const floatx4*)(bg[i] + k0);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const floatx4 a = *(const floatx4*)(aw + 8 * g);
+      floatx4 b[GTN];
+#pragma unroll
+      for (int t = 0; t < GTN; ++t) b[t] = *(const floatx4*)(bw + t * 32 * LDS_STRIDE + 8 * g);
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+        for (int t = 0; t < GTN; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[qq], b[t][qq], acc[t], 0, 0, 0);
+    }
+    __syncthreads();
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) *(floatx4*)(As + (lr + 32 * i) * LDS_STRIDE + lc) = ra[i];
+#pragma unroll
+      for (int i = 0; i < GTN; ++i) *(floatx4*)(Bs + (lr + 32 * i) * LDS_STRIDE + lc) = rb[i];
+      __syncthreads();
+    }
+  }
+
+  // Epilogue. C/D layout of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5),
+  // so rows 4g..4g+3 of a pool window sit in registers 4q..4q+3 of ONE lane.
+  const long long mw = m0 + wave * 32;
+#pragma unroll
+  for (int t = 0; t < GTN; ++t) {
+    const int n = n0 + t * 32 + li;
+    if (n >= p.n_store) continue;
+    if (EPI == EPI_PARTIAL) {
+      float* cp = p.C + (long long)ks * p.split_stride + n;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long long m = mw + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < p.M) cp[m * p.ldc] = acc[t][r];
+      }
+    } else if (EPI == EPI_RELU_POOL4) {
+      const float bn = p.bias[n];
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        const long long m = mw + 8 * qd + 4 * lh;  // first of 4 pooled rows (multiple of 4)
+        if (m >= p.M) continue;
+        const long long w = m / p.s_in;
+        const int tp = (int)(m - w * p.s_in) >> 2;
+        if (tp >= p.t_valid) continue;
+        float mx = fmaxf(fmaxf(acc[t][4 * qd], acc[t][4 * qd + 1]), fmaxf(acc[t][4 * qd + 2], acc[t][4 * qd + 3]));
+        // maxpool(relu(x+b)) == relu(max(x)+b): x -> fl(x+b) and relu are monotone.
+        p.C[(w * p.s_out + tp) * p.ldc + n] = fmaxf(mx + bn, 0.f);
+      }
+    } else {
+      const float bn = p.bias[n];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long long m = mw + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m >= p.M) continue;
+        const long long w = m / p.s_in;
+        const int tpos = (int)(m - w * p.s_in);
+        if (tpos >= p.t_valid) continue;
+        const float v = acc[t][r] + bn;
+        float o;
+        if (EPI == EPI_SIGMOID)
+          o = 1.0f / (1.0f + expf(-v));
+        else
+          o = fmaxf(v, 0.f);
+        p.C[(w * p.s_out + tpos) * p.ldc + n] = o;
+      }
+    }
+  }
+}
+
+// conv1 (4 -> 320, k=8): 32 FMAs per output; one window x 128 positions per block,
+// one output channel per thread (coalesced channel-last stores).  The input tile is built
+// in LDS either from one-hot floats ([B][4][1][2000], Beluga.py:23) or from base codes
+// with the encodeSeqs mapping A,G,C,T -> channel 0..3 (chromatin.py:155-160) and the
+// reverse complement [:, ::-1, ::-1] (chromatin.py:170) generated on the fly.
+constexpr int C1_T = 128;
+__global__ __launch_bounds__(320) void beluga_conv1(const float* __restrict__ x, const uint8_t* __restrict__ codes,
+                                                    long long code_stride, int n_src, int mode, long long row0,
+                                                    const float* __restrict__ w1, const float* __restrict__ b1,
+                                                    float* __restrict__ out) {
+  __shared__ floatx4 xs[C1_T + 8];
+  const int t0 = blockIdx.x * C1_T;
+  const long long win = blockIdx.y;
+  const long long r = row0 + win;
+  const int tid = threadIdx.x;
+  for (int j = tid; j < C1_T + 7; j += 320) {
+    const int pos = t0 + j;
+    floatx4 v = {0.f, 0.f, 0.f, 0.f};
+    if (pos < kLen) {
+      if (x) {
+        const float* xr = x + r * (4 * kLen);
+        v[0] = xr[pos];
+        v[1] = xr[kLen + pos];
+        v[2] = xr[2 * kLen + pos];
+        v[3] = xr[3 * kLen + pos];
+      } else {
+        long long src = r;
+        bool rc = (mode == EXPECTO_STRAND_RC);
+        if (mode == EXPECTO_STRAND_BOTH && r >= n_src) {
+          src = r - n_src;
+          rc = true;
+        }
+        const int pp = rc ? (kLen - 1 - pos) : pos;
+        const unsigned c = codes[src * code_stride + pp];
+        if (c < 4) {
+          const unsigned ch = rc ? 3 - c : c;
+          v[0] = ch == 0 ? 1.f : 0.f;
+          v[1] = ch == 1 ? 1.f : 0.f;
+          v[2] = ch == 2 ? 1.f : 0.f;
+          v[3] = ch == 3 ? 1.f : 0.f;
+        }
+      }
+    }
+    xs[j] = v;
+  }
+  __syncthreads();
+  const int co = tid;
+  float w[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) w[i] = w1[co * 32 + i];  // [ci*8 + k] as in the reference
+  const float bco = b1[co];
+  const int tmax = min(C1_T, kLen - 7 - t0);
+  float* o = out + (win * kLen + t0) * 320 + co;
+  for (int t = 0; t < tmax; ++t) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const floatx4 v = xs[t + k];
+      s = fmaf(w[k], v[0], s);
+      s = fmaf(w[8 + k], v[1], s);
+      s = fmaf(w[16 + k], v[2], s);
+      s = fmaf(w[24 + k], v[3], s);
+    }
+    o[(long long)t * 320] = fmaxf(s + bco, 0.f);
+  }
+}
+
+__global__ void fc1_reduce(const float* __restrict__ part, int splits, long long split_stride, long long count,
+                           const float* __restrict__ bias, float* __restrict__ h1) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const int n = (int)(i % kHidLd);
+  float s = 0.f;
+  for (int k = 0; k < splits; ++k) s += part[k * split_stride + i];
+  h1[i] = n < kFc1Out ? fmaxf(s + bias[n], 0.f) : 0.f;
+}
+
+// ---- weight repacking (reference layouts -> kernel layouts) --------------------------
+__global__ void repack_conv(const float* __restrict__ W, int cout, int cin, int npad, float* __restrict__ Wt) {
+  const long long K = 8LL * cin;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npad * K) return;
+  const int n = (int)(i / K);
+  const int k = (int)(i % K);
+  const int tap = k / cin, ci = k % cin;
+  Wt[i] = n < cout ? W[((long long)n * cin + ci) * 8 + tap] : 0.f;
+}
+
+__global__ void repack_fc1(const float* __restrict__ W, int npad, float* __restrict__ Wp) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)npad * kFc1In) return;
+  const int o = (int)(i / kFc1In);
+  const int k = (int)(i % kFc1In);
+  const int t = k / 640, c = k % 640;  // kernel order t*640+c <- reference flatten c*106+t
+  Wp[i] = o < kFc1Out ? W[(long long)o * kFc1In + c * 106 + t] : 0.f;
+}
+
+__global__ void repack_fc2(const float* __restrict__ W, int npad, float* __restrict__ Wp) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)npad * kHidLd) return;
+  const int o = (int)(i / kHidLd);
+  const int k = (int)(i % kHidLd);
+  Wp[i] = (o < kNFeat && k < kFc1Out) ? W[(long long)o * kFc1Out + k] : 0.f;
+}
+
+__global__ void pad_copy(const float* __restrict__ src, int n, int npad, float* __restrict__ dst) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < npad) dst[i] = i < n ? src[i] : 0.f;
+}
+
+}  // namespace expecto
+
+using namespace expecto;
+
+// ---- handle -----------------------------------------------------------------------------
+namespace {
+constexpr int kNumLayers = 9;
+struct ConvGeo {
+  int cin, cout, s_in, t_valid, s_out, pool;
+};
+// conv2..conv6 (index 0..4) -- positions from SURVEY.md section 0 item 3.
+constexpr ConvGeo kConv[5] = {
+    {320, 320, 2000, 496, 500, 1},  // conv2: 1986 valid -> pool 496
+    {320, 480, 500, 489, 500, 0},   // conv3
+    {480, 480, 500, 120, 125, 1},   // conv4: 482 valid -> pool 120
+    {480, 640, 125, 113, 125, 0},   // conv5
+    {640, 640, 125, 106, 125, 0},   // conv6
+};
+constexpr int kFcSplits[] = {1, 2, 4, 5, 8, 10};  // divisors of 67840/32 = 2120
+}  // namespace
+
+struct expecto_beluga {
+  int device = 0;
+  int max_batch = 0;
+  float* w1 = nullptr;
+  float* b1 = nullptr;
+  float* wt[5] = {};
+  float* bt[5] = {};
+  float* fc1w = nullptr;
+  float* fc1b = nullptr;
+  float* fc2w = nullptr;
+  float* fc2b = nullptr;
+  float* P = nullptr;
+  float* Q = nullptr;
+  float* part = nullptr;
+  float* h1 = nullptr;
+  size_t bytes = 0;
+  std::vector<void*> allocs;
+  bool profiling = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<int, int>> pending;  // (layer, event index of start)
+  size_t ev_next = 0;
+  double ms[kNumLayers] = {};
+  long long calls[kNumLayers] = {};
+};
+
+namespace {
+int dalloc(expecto_beluga* h, float** p, size_t nfloat) {
+  void* ptr = nullptr;
+  hipError_t e = hipMalloc(&ptr, nfloat * sizeof(float));
+  if (e != hipSuccess) {
+    set_error(std::string("hipMalloc: ") + hipGetErrorString(e));
+    return EXPECTO_ENOMEM;
+  }
+  h->allocs.push_back(ptr);
+  h->bytes += nfloat * sizeof(float);
+  *p = static_cast<float*>(ptr);
+  return EXPECTO_OK;
+}
+
+int npad_of(int n) { return (n + GBN - 1) / GBN * GBN; }
+
+size_t p_floats(int nb) { return (size_t)nb * 2000 * 320 + 16 * 640; }
+size_t q_floats(int nb) { return (size_t)nb * 500 * 320 + 16 * 640; }
+
+int resolve_events(expecto_beluga* h) {
+  for (auto& pr : h->pending) {
+    EXPECTO_HIP_CHECK(hipEventSynchronize(h->ev_pool[pr.second + 1]));
+    float ms = 0.f;
+    EXPECTO_HIP_CHECK(hipEventElapsedTime(&ms, h->ev_pool[pr.second], h->ev_pool[pr.second + 1]));
+    h->ms[pr.first] += ms;
+    h->calls[pr.first] += 1;
+  }
+  h->pending.clear();
+  h->ev_next = 0;
+  return EXPECTO_OK;
+}
+
+struct LayerTimer {
+  expecto_beluga* h;
+  int layer;
+  int idx = -1;
+  hipStream_t st;
+  LayerTimer(expecto_beluga* hh, int l, hipStream_t s) : h(hh), layer(l), st(s) {
+    if (!h->profiling) return;
+    if (h->ev_next + 2 > h->ev_pool.size()) resolve_events(h);
+    idx = (int)h->ev_next;
+    h->ev_next += 2;
+    hipEventRecord(h->ev_pool[idx], st);
+  }
+  ~LayerTimer() {
+    if (idx < 0) return;
+    hipEventRecord(h->ev_pool[idx + 1], st);
+    h->pending.push_back({layer, idx});
+  }
+};
+
+template <int LAYER, int EPI>
+int launch_gemm(const GemmArgs& a, int splits, hipStream_t st) {
+  const long long nblk = a.m_tiles * a.n_tiles * splits;
+  EXPECTO_REQUIRE(nblk > 0 && nblk < (1LL << 31), "gemm grid out of range");
+  EXPECTO_REQUIRE(a.kper % GBK == 0 && a.kper > 0, "gemm K not a multiple of 32");
+  EXPECTO_REQUIRE(a.lda % 4 == 0 && a.ldb % 4 == 0, "gemm leading dims must be multiples of 4");
+  beluga_gemm<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
+  return check_launch("beluga_gemm");
+}
+
+// One chunk of nb windows; conv1 input from x (one-hot) or codes.
+int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long long code_stride, int n_src,
+                  int mode, long long row0, int nb, float* y, hipStream_t st) {
+  int rc;
+  {
+    LayerTimer lt(h, 0, st);
+    dim3 grid((kLen - 7 + C1_T - 1) / C1_T, nb);
+    beluga_conv1<<<grid, dim3(320), 0, st>>>(x, codes, code_stride, n_src, mode, row0, h->w1, h->b1, h->P);
+    if ((rc = check_launch("beluga_conv1"))) return rc;
+  }
+  float* src = h->P;
+  float* dst = h->Q;
+  for (int l = 0; l < 5; ++l) {
+    const ConvGeo& g = kConv[l];
+    GemmArgs a{};
+    a.A = src;
+    a.lda = g.cin;
+    a.M = (long long)nb * g.s_in;
+    a.B = h->wt[l];
+    a.ldb = 8LL * g.cin;
+    a.kper = 8 * g.cin;
+    a.n_tiles = npad_of(g.cout) / GBN;
+    a.m_tiles = (a.M + GBM - 1) / GBM;
+    a.m_fastest = 0;
+    a.bias = h->bt[l];
+    a.C = dst;
+    a.ldc = g.cout;
+    a.n_store = g.cout;
+    a.s_in = g.s_in;
+    a.t_valid = g.t_valid;
+    a.s_out = g.s_out;
+    LayerTimer lt(h, l + 1, st);
+    switch (l) {
+      case 0: rc = launch_gemm<2, EPI_RELU_POOL4>(a, 1, st); break;
+      case 1: rc = launch_gemm<3, EPI_RELU>(a, 1, st); break;
+      case 2: rc = launch_gemm<4, EPI_RELU_POOL4>(a, 1, st); break;
+      case 3: rc = launch_gemm<5, EPI_RELU>(a, 1, st); break;
+      default: rc = launch_gemm<6, EPI_RELU>(a, 1, st); break;
+    }
+    if (rc) return rc;
+    std::swap(src, dst);
+  }
+  // src now holds act5 (buffer Q): FC1 reads rows 0..105 of each window as one row.
+  const long long m_tiles = (nb + GBM - 1) / GBM;
+  const int n_tiles1 = npad_of(kFc1Out) / GBN;
+  int splits = kFcSplits[0];
+  for (int s : kFcSplits) {
+    splits = s;
+    if (m_tiles * n_tiles1 * s >= 1000) break;
+  }
+  {
+    GemmArgs a{};
+    a.A = src;
+    a.lda = 125LL * 640;
+    a.M = nb;
+    a.B = h->fc1w;
+    a.ldb = kFc1In;
+    a.kper = kFc1In / splits;
+    a.n_tiles = n_tiles1;
+    a.m_tiles = m_tiles;
+    a.m_fastest = 1;
+    a.C = h->part;
+    a.ldc = kHidLd;
+    a.n_store = kHidLd;
+    a.split_stride = (long long)nb * kHidLd;
+    LayerTimer lt(h, 6, st);
+    if ((rc = launch_gemm<7, EPI_PARTIAL>(a, splits, st))) return rc;
+  }
+  {
+    LayerTimer lt(h, 7, st);
+    const long long count = (long long)nb * kHidLd;
+    fc1_reduce<<<dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st>>>(h->part, splits, count, count, h->fc1b,
+                                                                            h->h1);
+    if ((rc = check_launch("fc1_reduce"))) return rc;
+  }
+  {
+    GemmArgs a{};
+    a.A = h->h1;
+    a.lda = kHidLd;
+    a.M = nb;
+    a.B = h->fc2w;
+    a.ldb = kHidLd;
+    a.kper = kHidLd;
+    a.n_tiles = npad_of(kNFeat) / GBN;
+    a.m_tiles = m_tiles;
+    a.m_fastest = 1;
+    a.bias = h->fc2b;
+    a.C = y;
+    a.ldc = kNFeat;
+    a.n_store = kNFeat;
+    a.s_in = 1;
+    a.t_valid = 1;
+    a.s_out = 1;
+    LayerTimer lt(h, 8, st);
+    if ((rc = launch_gemm<8, EPI_SIGMOID>(a, 1, st))) return rc;
+  }
+  return EXPECTO_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int expecto_beluga_create(int device, const float* const* params, int max_batch, void* stream,
+                          expecto_beluga_t* out) {
+  EXPECTO_REQUIRE(out != nullptr && params != nullptr, "null argument");
+  EXPECTO_REQUIRE(max_batch > 0 && max_batch <= (1 << 16), "max_batch out of range");
+  for (int i = 0; i < EXPECTO_BELUGA_NPARAMS; ++i) EXPECTO_REQUIRE(params[i] != nullptr, "null parameter pointer");
+  EXPECTO_HIP_CHECK(hipSetDevice(device));
+  hipStream_t st = as_stream(stream);
+  auto* h = new expecto_beluga();
+  h->device = device;
+  h->max_batch = max_batch;
+  int rc = 0;
+  auto fail = [&](int code) {
+    expecto_beluga_destroy(h);
+    return code;
+  };
+  if ((rc = dalloc(h, &h->w1, 320 * 32)) || (rc = dalloc(h, &h->b1, 320))) return fail(rc);
+  EXPECTO_HIP_CHECK(hipMemcpyAsync(h->w1, params[0], 320 * 32 * sizeof(float), hipMemcpyDeviceToDevice, st));
+  EXPECTO_HIP_CHECK(hipMemcpyAsync(h->b1, params[1], 320 * sizeof(float), hipMemcpyDeviceToDevice, st));
+  for (int l = 0; l < 5; ++l) {
+    const ConvGeo& g = kConv[l];
+    const int np = npad_of(g.cout);
+    const long long K = 8LL * g.cin;
+    if ((rc = dalloc(h, &h->wt[l], (size_t)np * K)) || (rc = dalloc(h, &h->bt[l], np))) return fail(rc);
+    const long long tot = np * K;
+    repack_conv<<<dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st>>>(params[2 + 2 * l], g.cout, g.cin, np,
+                                                                          h->wt[l]);
+    pad_copy<<<dim3((np + 255) / 256), dim3(256), 0, st>>>(params[3 + 2 * l], g.cout, np, h->bt[l]);
+  }
+  const int np1 = npad_of(kFc1Out), np2 = npad_of(kNFeat);
+  if ((rc = dalloc(h, &h->fc1w, (size_t)np1 * kFc1In)) || (rc = dalloc(h, &h->fc1b, np1)) ||
+      (rc = dalloc(h, &h->fc2w, (size_t)np2 * kHidLd)) || (rc = dalloc(h, &h->fc2b, np2)))
+    return fail(rc);
+  {
+    const long long tot = (long long)np1 * kFc1In;
+    repack_fc1<<<dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st>>>(params[12], np1, h->fc1w);
+    pad_copy<<<dim3((np1 + 255) / 256), dim3(256), 0, st>>>(params[13], kFc1Out, np1, h->fc1b);
+    const long long tot2 = (long long)np2 * kHidLd;
+    repack_fc2<<<dim3((unsigned)((tot2 + 255) / 256)), dim3(256), 0, st>>>(params[14], np2, h->fc2w);
+    pad_copy<<<dim3((np2 + 255) / 256), dim3(256), 0, st>>>(params[15], kNFeat, np2, h->fc2b);
+  }
+  if ((rc = check_launch("repack"))) return fail(rc);
+  const size_t pf = p_floats(max_batch), qf = q_floats(max_batch);
+  const size_t partf = (size_t)kFcSplits[5] * max_batch * kHidLd;
+  if ((rc = dalloc(h, &h->P, pf)) || (rc = dalloc(h, &h->Q, qf)) || (rc = dalloc(h, &h->part, partf)) ||
+      (rc = dalloc(h, &h->h1, (size_t)max_batch * kHidLd)))
+    return fail(rc);
+  EXPECTO_HIP_CHECK(hipMemsetAsync(h->P, 0, pf * sizeof(float), st));
+  EXPECTO_HIP_CHECK(hipMemsetAsync(h->Q, 0, qf * sizeof(float), st));
+  EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
+  *out = h;
+  return EXPECTO_OK;
+}
+
+void expecto_beluga_destroy(expecto_beluga_t h) {
+  if (!h) return;
+  for (void* p : h->allocs) hipFree(p);
+  for (hipEvent_t e : h->ev_pool) hipEventDestroy(e);
+  delete h;
+}
+
+size_t expecto_beluga_device_bytes(expecto_beluga_t h) { return h ? h->bytes : 0; }
+
+int expecto_beluga_forward_onehot(expecto_beluga_t h, const float* x, int n, float* y, void* stream) {
+  EXPECTO_REQUIRE(h != nullptr, "null handle");
+  EXPECTO_REQUIRE(n >= 0, "negative batch");
+  if (n == 0) return EXPECTO_OK;
+  EXPECTO_REQUIRE(x != nullptr && y != nullptr, "null input/output");
+  EXPECTO_HIP_CHECK(hipSetDevice(h->device));
+  hipStream_t st = as_stream(stream);
+  for (long long r0 = 0; r0 < n; r0 += h->max_batch) {
+    const int nb = (int)std::min<long long>(h->max_batch, n - r0);
+    int rc = forward_chunk(h, x, nullptr, 0, 0, 0, r0, nb, y + r0 * kNFeat, st);
+    if (rc) return rc;
+  }
+  return EXPECTO_OK;
+}
+
+int expecto_beluga_forward_codes(expecto_beluga_t h, const uint8_t* codes, int n, long long code_stride,
+                                 int strand_mode, float* y, void* stream) {
+  EXPECTO_REQUIRE(h != nullptr, "null handle");
+  EXPECTO_REQUIRE(n >= 0, "negative batch");
+  EXPECTO_REQUIRE(strand_mode >= 0 && strand_mode <= 2, "bad strand mode");
+  if (n == 0) return EXPECTO_OK;
+  EXPECTO_REQUIRE(codes != nullptr && y != nullptr, "null input/output");
+  EXPECTO_REQUIRE(code_stride >= kLen, "code_stride < 2000");
+  EXPECTO_HIP_CHECK(hipSetDevice(h->device));
+  hipStream_t st = as_stream(stream);
+  const long long rows = strand_mode == EXPECTO_STRAND_BOTH ? 2LL * n : n;
+  for (long long r0 = 0; r0 < rows; r0 += h->max_batch) {
+    const int nb = (int)std::min<long long>(h->max_batch, rows - r0);
+    int rc = forward_chunk(h, nullptr, codes, code_stride, n, strand_mode, r0, nb, y + r0 * kNFeat, st);
+    if (rc) return rc;
+  }
+  return EXPECTO_OK;
+}
+
+int expecto_beluga_set_profiling(expecto_beluga_t h, int on) {
+  EXPECTO_REQUIRE(h != nullptr, "null handle");
+  if (on && h->ev_pool.empty()) {
+    h->ev_pool.resize(1024);
+    for (auto& e : h->ev_pool) EXPECTO_HIP_CHECK(hipEventCreate(&e));
+  }
+  if (!on) {
+    int rc = resolve_events(h);
+    if (rc) return rc;
+  }
+  h->profiling = on != 0;
+  if (on) {
+    std::fill(h->ms, h->ms + kNumLayers, 0.0);
+    std::fill(h->calls, h->calls + kNumLayers, 0LL);
+  }
+  return EXPECTO_OK;
+}
+
+int expecto_beluga_layer_times(expecto_beluga_t h, double* ms, long long* calls, int max_layers) {
+  EXPECTO_REQUIRE(h != nullptr, "null handle");
+  int rc = resolve_events(h);
+  if (rc) return rc;
+  const int n = std::min(max_layers, kNumLayers);
+  for (int i = 0; i < n; ++i) {
+    if (ms) ms[i] = h->ms[i];
+    if (calls) calls[i] = h->calls[i];
+  }
+  return kNumLayers;
+}
+
+}  // extern "C"

@@ -1,0 +1,199 @@
+// HBM-bound kernels around the Beluga forward (gfx950):
+//  * variant window generation from a device-resident genome (chromatin.py:175-209),
+//  * diff = alt - ref (chromatin.py:281), fwd/rc averaging (predict.py:186-190),
+//  * TSS spatial-transform reduction (compute_expecto_features.py:88-124),
+//  * variant spatial reduction (predict.py:87-136).
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "common.h"
+
+namespace expecto {
+
+thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+constexpr int kLen = 2000;
+
+// One window per blockIdx.y (variant) x blockIdx.z (allele*n_shift + shift); 2000 codes
+// per window; 4 codes per thread (uint32 stores).
+__global__ void variant_windows_kernel(const uint8_t* __restrict__ genome, long long genome_len,
+                                       const long long* __restrict__ var_off, const uint8_t* __restrict__ ref_code,
+                                       const uint8_t* __restrict__ alt_code, int n, const int* __restrict__ shifts,
+                                       int n_shift, uint8_t* __restrict__ codes) {
+  const int v = blockIdx.y;
+  const int j = blockIdx.z % n_shift;
+  const int allele = blockIdx.z / n_shift;
+  const int i4 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i4 >= kLen) return;
+  const int shift = shifts[j];
+  // crop index i <-> genome offset off_v + shift - 999 + i; variant at i = 999 - shift.
+  const long long base = var_off[v] + shift - 999;
+  const int mut = 999 - shift;
+  const uint8_t allele_code = allele ? alt_code[v] : ref_code[v];
+  unsigned packed = 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int i = i4 + e;
+    const long long g = base + i;
+    unsigned c = (g >= 0 && g < genome_len) ? genome[g] : 4u;
+    if (i == mut) c = allele_code;
+    packed |= c << (8 * e);
+  }
+  *reinterpret_cast<unsigned*>(codes + ((long long)(allele * n_shift + j) * n + v) * kLen + i4) = packed;
+}
+
+__global__ void diff_kernel(const float4* __restrict__ a, const float4* __restrict__ b, long long n4,
+                            float4* __restrict__ out) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const float4 x = a[i], y = b[i];
+    out[i] = make_float4(x.x - y.x, x.y - y.y, x.z - y.z, x.w - y.w);
+  }
+}
+
+__global__ void diff_tail(const float* a, const float* b, long long start, long long n, float* out) {
+  const long long i = start + threadIdx.x;
+  if (i < n) out[i] = a[i] - b[i];
+}
+
+__global__ void fwd_rc_avg_kernel(const float* __restrict__ x, int rows, int cols, float* __restrict__ out) {
+  const long long total = (long long)rows * cols;
+  const long long half = total;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x)
+    out[i] = (x[i] + x[i + half]) / 2.0f;
+}
+
+// grid: (ceil(nfeat/256), n_genes); thread = feature f; loops over the shifts in order.
+__global__ void tss_reduce_kernel(const float* __restrict__ fwd, const float* __restrict__ rc,
+                                  const double* __restrict__ weights, int n_shift, int nfeat,
+                                  double* __restrict__ out) {
+  extern __shared__ double wsh[];  // [10][n_shift]
+  for (int i = threadIdx.x; i < 10 * n_shift; i += blockDim.x) wsh[i] = weights[i];
+  __syncthreads();
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  const long long g = blockIdx.y;
+  if (f >= nfeat) return;
+  double acc[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) acc[k] = 0.0;
+  const float* pf = fwd + g * n_shift * nfeat + f;
+  const float* pr = rc + g * n_shift * nfeat + f;
+  for (int s = 0; s < n_shift; ++s) {
+    const float p = 0.5f * (pf[(long long)s * nfeat] + pr[(long long)s * nfeat]);  // f32 like numpy
+    const double pd = (double)p;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) acc[k] += wsh[k * n_shift + s] * pd;
+  }
+  double* o = out + g * 10LL * nfeat + f;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) o[(long long)k * nfeat] = acc[k];
+}
+
+// grid: (ceil(nfeat/256), n); weights W_j[k] computed per variant in f64.
+__global__ void variant_reduce_kernel(const float* __restrict__ eff, const long long* __restrict__ dist,
+                                      const uint8_t* __restrict__ strand_plus, const int* __restrict__ shifts,
+                                      int n_shift, int n, int nfeat, double* __restrict__ out) {
+  __shared__ double wsh[32 * 10];
+  const long long v = blockIdx.y;
+  const double decay[5] = {0.01, 0.02, 0.05, 0.1, 0.2};
+  if ((int)threadIdx.x < n_shift) {
+    const int j = threadIdx.x;
+    const long long sgn = strand_plus[v] ? 1 : -1;
+    const long long d = dist[v] * sgn + (long long)shifts[j] * sgn;
+    const double fl = floor(fabs((double)d) / 200.0);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const double e = exp(-decay[k] * fl);
+      wsh[j * 10 + k] = d <= 0 ? e : 0.0;
+      wsh[j * 10 + 5 + k] = d >= 0 ? e : 0.0;
+    }
+  }
+  __syncthreads();
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= nfeat) return;
+  double acc[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) acc[k] = 0.0;
+  for (int j = 0; j < n_shift; ++j) {
+    const double e = (double)eff[((long long)j * n + v) * nfeat + f];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) acc[k] += e * wsh[j * 10 + k];
+  }
+  double* o = out + v * 10LL * nfeat + f;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) o[(long long)k * nfeat] = acc[k];
+}
+
+}  // namespace expecto
+
+using namespace expecto;
+
+extern "C" {
+
+const char* expecto_last_error(void) { return g_last_error.c_str(); }
+const char* expecto_version(void) { return "expecto_hip 0.1.0 gfx950"; }
+
+int expecto_variant_windows(const uint8_t* genome, long long genome_len, const long long* var_off,
+                            const uint8_t* ref_code, const uint8_t* alt_code, int n, const int* shifts, int n_shift,
+                            uint8_t* codes, void* stream) {
+  EXPECTO_REQUIRE(n >= 0 && n_shift > 0 && n_shift <= 65535 / 2, "bad variant/shift count");
+  if (n == 0) return EXPECTO_OK;
+  EXPECTO_REQUIRE(n <= 65535, "at most 65535 variants per call");
+  EXPECTO_REQUIRE(genome && var_off && ref_code && alt_code && shifts && codes, "null argument");
+  dim3 grid((kLen / 4 + 255) / 256, n, 2 * n_shift);
+  variant_windows_kernel<<<grid, dim3(256), 0, as_stream(stream)>>>(genome, genome_len, var_off, ref_code, alt_code, n,
+                                                                    shifts, n_shift, codes);
+  return check_launch("variant_windows");
+}
+
+int expecto_diff(const float* alt, const float* ref, long long count, float* out, void* stream) {
+  EXPECTO_REQUIRE(count >= 0, "negative count");
+  if (count == 0) return EXPECTO_OK;
+  EXPECTO_REQUIRE(alt && ref && out, "null argument");
+  EXPECTO_REQUIRE(((uintptr_t)alt | (uintptr_t)ref | (uintptr_t)out) % 16 == 0, "diff buffers must be 16-B aligned");
+  const long long n4 = count / 4;
+  if (n4 > 0) {
+    const long long blocks = std::min<long long>((n4 + 255) / 256, 8192);
+    diff_kernel<<<dim3((unsigned)blocks), dim3(256), 0, as_stream(stream)>>>(
+        reinterpret_cast<const float4*>(alt), reinterpret_cast<const float4*>(ref), n4, reinterpret_cast<float4*>(out));
+  }
+  if (count % 4) diff_tail<<<1, 4, 0, as_stream(stream)>>>(alt, ref, n4 * 4, count, out);
+  return check_launch("diff");
+}
+
+int expecto_fwd_rc_average(const float* x, int rows, int cols, float* out, void* stream) {
+  EXPECTO_REQUIRE(rows >= 0 && cols >= 0, "negative shape");
+  if (rows == 0 || cols == 0) return EXPECTO_OK;
+  EXPECTO_REQUIRE(x && out, "null argument");
+  const long long total = (long long)rows * cols;
+  const long long blocks = std::min<long long>((total + 255) / 256, 8192);
+  fwd_rc_avg_kernel<<<dim3((unsigned)blocks), dim3(256), 0, as_stream(stream)>>>(x, rows, cols, out);
+  return check_launch("fwd_rc_average");
+}
+
+int expecto_tss_reduce(const float* fwd, const float* rc, const double* weights, int n_genes, int n_shift, int nfeat,
+                       double* out, void* stream) {
+  EXPECTO_REQUIRE(n_genes >= 0 && n_shift > 0 && n_shift <= 4096 && nfeat > 0, "bad shape");
+  if (n_genes == 0) return EXPECTO_OK;
+  EXPECTO_REQUIRE(n_genes <= 65535, "at most 65535 genes per call");
+  EXPECTO_REQUIRE(fwd && rc && weights && out, "null argument");
+  dim3 grid((nfeat + 255) / 256, n_genes);
+  tss_reduce_kernel<<<grid, dim3(256), 10 * n_shift * sizeof(double), as_stream(stream)>>>(fwd, rc, weights, n_shift,
+                                                                                          nfeat, out);
+  return check_launch("tss_reduce");
+}
+
+int expecto_variant_reduce(const float* effects, const long long* dist, const uint8_t* strand_plus, const int* shifts,
+                           int n_shift, int n, int nfeat, double* out, void* stream) {
+  EXPECTO_REQUIRE(n >= 0 && n_shift > 0 && n_shift <= 32 && nfeat > 0, "bad shape (n_shift <= 32)");
+  if (n == 0) return EXPECTO_OK;
+  EXPECTO_REQUIRE(n <= 65535, "at most 65535 variants per call");
+  EXPECTO_REQUIRE(effects && dist && strand_plus && shifts && out, "null argument");
+  dim3 grid((nfeat + 255) / 256, n);
+  variant_reduce_kernel<<<grid, dim3(256), 0, as_stream(stream)>>>(effects, dist, strand_plus, shifts, n_shift, n,
+                                                                   nfeat, out);
+  return check_launch("variant_reduce");
+}
+
+}  // extern "C"

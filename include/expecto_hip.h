@@ -1,0 +1,121 @@
+/*
+ * expecto_hip.h -- C-ABI of the MI355X-native ExPecto Beluga hot path (gfx950).
+ *
+ * Every entry point takes plain pointers and sizes; device pointers are HIP device
+ * memory, `stream` is a hipStream_t passed as void* (NULL = the null stream).  All
+ * functions return 0 on success and a negative status on failure; the message of the
+ * last failure on the calling thread is returned by expecto_last_error().
+ *
+ * Reference interfaces each entry point replaces (paths relative to the reference repo):
+ *   expecto_beluga_create          Beluga() + load_state_dict(torch.load(pth)) + .cuda()
+ *                                  (Beluga.py:18-48; chromatin.py:102-106;
+ *                                   compute_expecto_features.py:36-40)
+ *   expecto_beluga_forward_onehot  Beluga.forward(x[B,4,1,2000]) -> [B,2002]
+ *                                  (Beluga.py:50-51; called at chromatin.py:270,278,
+ *                                   compute_expecto_features.py:121-122)
+ *   expecto_beluga_forward_codes   encodeSeqs(...) one-hot + Beluga.forward, fused: the
+ *                                  one-hot / reverse-complement of chromatin.py:153-171
+ *                                  is generated inside the conv1 kernel from base codes
+ *   expecto_variant_windows        fetchSeqs window splice for SNVs (chromatin.py:175-209)
+ *                                  from a device-resident genome
+ *   expecto_diff                   diff = alt - ref (chromatin.py:281)
+ *   expecto_fwd_rc_average         (x[:N] + x[N:]) / 2 (predict.py:186-190;
+ *                                   0.5*(fwd+rc) of compute_expecto_features.py:123)
+ *   expecto_tss_reduce             pos_weights x pred_fwd_rc (compute_expecto_features.py:91-124)
+ *   expecto_variant_reduce         exp-decay shift weights x effects (predict.py:87-136)
+ *   expecto_beluga_destroy         (model teardown)
+ */
+#ifndef EXPECTO_HIP_H
+#define EXPECTO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct expecto_beluga* expecto_beluga_t;
+
+enum {
+  EXPECTO_OK = 0,
+  EXPECTO_EINVAL = -1,   /* bad argument (shape, pointer, mode)            */
+  EXPECTO_EHIP = -2,     /* HIP runtime error                              */
+  EXPECTO_ENOMEM = -3,   /* device allocation failed                       */
+};
+
+/* Strand modes of expecto_beluga_forward_codes. */
+enum {
+  EXPECTO_STRAND_FWD = 0,   /* n output rows: the windows as given                       */
+  EXPECTO_STRAND_RC = 1,    /* n output rows: reverse complement of each window          */
+  EXPECTO_STRAND_BOTH = 2,  /* 2n output rows: [fwd rows 0..n-1 ; rc rows n..2n-1]
+                               (encodeSeqs row order, chromatin.py:170-171)             */
+};
+
+/* Number of parameter tensors and their order (the reference state-dict keys,
+ * SURVEY.md 2.2): model.0.{0,2,6,8,12,14}.{weight,bias}, model.1.2.1.{weight,bias},
+ * model.1.4.1.{weight,bias}. */
+#define EXPECTO_BELUGA_NPARAMS 16
+#define EXPECTO_BELUGA_INPUT_LEN 2000
+#define EXPECTO_BELUGA_NFEAT 2002
+
+/* Build a model handle on `device`.  `params` are 16 DEVICE pointers to fp32 tensors in
+ * the reference layouts (conv weight [Cout,Cin,1,8], fc weight [out,in]); they are
+ * repacked into the kernels' layouts, so the caller may free them afterwards.
+ * `max_batch` bounds the windows processed per internal chunk (workspace size). */
+int expecto_beluga_create(int device, const float* const* params, int max_batch, void* stream,
+                          expecto_beluga_t* out);
+void expecto_beluga_destroy(expecto_beluga_t h);
+
+/* Bytes of device memory the handle owns (weights + workspace). */
+size_t expecto_beluga_device_bytes(expecto_beluga_t h);
+
+/* y[n,2002] = Beluga.forward(x[n,4,1,2000]) (x contiguous fp32, any values). */
+int expecto_beluga_forward_onehot(expecto_beluga_t h, const float* x, int n, float* y, void* stream);
+
+/* Windows given as base codes (uint8, 0=A 1=G 2=C 3=T 4=zero column for N/n/H/-),
+ * window i at codes + i*code_stride, 2000 codes each.  y has n rows (FWD, RC) or 2n rows
+ * (BOTH). */
+int expecto_beluga_forward_codes(expecto_beluga_t h, const uint8_t* codes, int n, long long code_stride,
+                                 int strand_mode, float* y, void* stream);
+
+/* Per-layer device time accumulated over forward calls while profiling is on (ms).
+ * Layers: 0 conv1, 1 conv2, 2 conv3, 3 conv4, 4 conv5, 5 conv6, 6 fc1, 7 fc1-reduce, 8 fc2.
+ * `calls` receives the number of launches per layer.  Returns the number of layers. */
+int expecto_beluga_set_profiling(expecto_beluga_t h, int on);
+int expecto_beluga_layer_times(expecto_beluga_t h, double* ms, long long* calls, int max_layers);
+
+/* SNV windows from a device-resident genome (uint8 codes as above).  For variant v and
+ * shift s the 2000-code window is genome[off_v + shift - 999 + i], i = 0..1999, with the
+ * code at index 999 - shift replaced by ref_code[v] (allele 0) or alt_code[v] (allele 1)
+ * (chromatin.py:202-209 then the centre crop of :164).  off_v = 0-based genome offset of
+ * the variant base.  Output codes[((a*n_shift + j)*n + v)*2000 + i] for allele a in {0,1}. */
+int expecto_variant_windows(const uint8_t* genome, long long genome_len, const long long* var_off,
+                            const uint8_t* ref_code, const uint8_t* alt_code, int n,
+                            const int* shifts, int n_shift, uint8_t* codes, void* stream);
+
+/* out[i] = a[i] - b[i], i < count (fp32). */
+int expecto_diff(const float* alt, const float* ref, long long count, float* out, void* stream);
+
+/* out[r, f] = (x[r, f] + x[r + rows, f]) / 2 for r < rows, f < cols (fp32). */
+int expecto_fwd_rc_average(const float* x, int rows, int cols, float* out, void* stream);
+
+/* TSS reduction for n_genes genes: fwd and rc are [n_genes, n_shift, nfeat] fp32;
+ * weights [10, n_shift] fp64; out [n_genes, 10*nfeat] fp64 with
+ * out[g, k*nfeat + f] = sum_s weights[k,s] * (0.5f*(fwd[g,s,f] + rc[g,s,f])). */
+int expecto_tss_reduce(const float* fwd, const float* rc, const double* weights, int n_genes, int n_shift,
+                       int nfeat, double* out, void* stream);
+
+/* Variant reduction: effects [n_shift, n, nfeat] fp32 (fwd/rc-averaged, shift order of
+ * chromatin.py:243), dist[n] (pos - TSS, int64), strand_plus[n] (1 '+', 0 '-'),
+ * shifts[n_shift]; out [n, 10*nfeat] fp64 (predict.py:87-124 feature layout). */
+int expecto_variant_reduce(const float* effects, const long long* dist, const uint8_t* strand_plus,
+                           const int* shifts, int n_shift, int n, int nfeat, double* out, void* stream);
+
+const char* expecto_last_error(void);
+const char* expecto_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EXPECTO_HIP_H */
