@@ -1,0 +1,173 @@
+"""Benchmark of the ExPecto hot path on MI355X (contract: see task / DESIGN.md "Measurement").
+
+Workload (BASELINE.json configs[1], per GPU): 1k synthetic biallelic SNVs, shift 0, ref+alt
+alleles x fwd+rc strands = 4000 Beluga windows per step.  One step = device window
+generation from the HBM-resident genome (expecto_variant_windows) + the Beluga forward over
+all 4000 windows (conv1 .. fc2+sigmoid, fp32) + diff = alt - ref: exactly the device work of
+one chromatin.py shift for 1k variants, inputs already resident in HBM.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+N>1: weak scaling, each rank its own 1k SNVs, no collective in the step (variants are
+independent; the RCCL gather belongs to file output).  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from expecto_amd import beluga, dist as edist, synthetic  # noqa: E402
+from expecto_amd.genome import DeviceGenome, Fasta  # noqa: E402
+from expecto_amd.pipeline import VariantPipeline, VariantSet  # noqa: E402
+
+METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
+FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+
+# per-window dense MACs of each layer, for the roofline of each kernel
+LAYER_MACS = {
+    "conv1": 1993 * 320 * 32, "conv2": 1986 * 320 * 2560, "conv3": 489 * 480 * 2560,
+    "conv4": 482 * 480 * 3840, "conv5": 113 * 640 * 3840, "conv6": 106 * 640 * 5120,
+    "fc1": 67840 * 2003, "fc1_reduce": 0, "fc2": 2003 * 2002,
+}
+KERNEL_NAMES = {"conv2": "beluga_gemm<2, 1>", "conv3": "beluga_gemm<3, 0>", "conv4": "beluga_gemm<4, 1>",
+                "conv5": "beluga_gemm<5, 0>", "conv6": "beluga_gemm<6, 0>", "fc1": "beluga_gemm<7, 3>",
+                "fc2": "beluga_gemm<8, 2>", "conv1": "beluga_conv1", "fc1_reduce": "fc1_reduce"}
+WINDOW_MACS = sum(LAYER_MACS.values())
+
+
+def cpu_baseline(sd_cpu, codes: np.ndarray, seconds: float, threads: int, windows_per_variant: int):
+    """Oracle torch-CPU forward (the reference's CPU arithmetic) on a bounded sample."""
+    from oracle.beluga_np import forward_torch_cpu
+    from expecto_amd.encode import codes_to_onehot
+
+    torch.set_num_threads(threads)
+    x = torch.from_numpy(codes_to_onehot(codes[:32], with_rc=False).astype(np.float32)).unsqueeze(2)
+    forward_torch_cpu(sd_cpu, x[:4])                     # warm-up
+    done, t0 = 0, time.perf_counter()
+    while True:
+        forward_torch_cpu(sd_cpu, x)
+        done += x.shape[0]
+        el = time.perf_counter() - t0
+        if el >= seconds or el >= 30.0:
+            break
+    wps = done / el
+    return {"value": wps / windows_per_variant, "unit": "variants/s", "cores": threads, "kind": "port",
+            "windows_per_s": wps,
+            "sample": f"{done} windows of the same workload (seeded SNV ref windows), batch 32, "
+                      f"oracle/beluga_np.forward_torch_cpu (torch CPU fp32, oneDNN), {el:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--variants", type=int, default=1000, help="SNVs per GPU per step")
+    ap.add_argument("--maxshift", type=int, default=0, help="0 = configs[1] (shift 0 only)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank, world, local = edist.init("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    from expecto_amd.pipeline import shift_order
+    shifts = shift_order(args.maxshift)
+    S, n = len(shifts), args.variants
+    rows = 4 * S * n
+
+    genome = synthetic.genome_bytes(n_contigs=24, contig_len=2_000_000, seed=0)
+    fasta = Fasta.from_dict(genome)
+    snvs = synthetic.snvs(genome, n, seed=1 + rank)
+    vs = VariantSet([s[0] for s in snvs], np.array([s[1] for s in snvs]), [s[2] for s in snvs],
+                    [s[3] for s in snvs])
+    model = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=rows)
+    sd_cpu = {k: v.detach().clone() for k, v in model.state_dict().items()} if (rank == 0 and world == 1) else None
+    model = model.cuda()
+    eng = model.engine()
+    pipe = VariantPipeline(eng, fasta, DeviceGenome(fasta, device=dev))
+    prep = pipe.prepare(vs, shifts)                          # variant table resident in HBM
+    y = torch.empty((2, 2, S, n, 2002), dtype=torch.float32, device=dev)
+    codes = torch.empty((2, S, n, 2000), dtype=torch.uint8, device=dev)
+
+    def step():
+        pipe.predict(prep, out=y, codes=codes)
+        return pipe.diff(y)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    eng.set_profiling(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    el = time.perf_counter() - t0
+    layers = eng.layer_times()
+    eng.set_profiling(False)
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = float(t.item())
+
+    total_rows = rows * args.steps
+    value = world * n * args.steps / el
+    fwd_ms = sum(ms for ms, _ in layers.values())
+    dom = max((k for k in layers if LAYER_MACS[k]), key=lambda k: layers[k][0])
+    dom_ms, dom_calls = layers[dom]
+    dom_flops_launch = 2.0 * LAYER_MACS[dom] * total_rows / dom_calls
+    achieved = dom_flops_launch / (dom_ms / dom_calls / 1e3) / 1e12
+    rec = {
+        "metric": METRIC, "value": value, "unit": "variants/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic: seeded genome (24 x 2 Mbp), seeded SNVs, seeded Beluga weights x sqrt(6)",
+        "config": {"workload": f"configs[1]: {n} SNVs/GPU, shifts {shifts}, ref+alt x fwd+rc = "
+                               f"{rows} Beluga windows/step/GPU (window gen + forward + diff)",
+                   "variants_per_gpu": n, "windows_per_variant": 4 * S, "parallelism": f"dp{world} (variant shards)"},
+        "windows_per_s": world * total_rows / el,
+        "variants_200shift_per_s": world * total_rows / el / 800.0,
+        "forward_tflops": 2.0 * WINDOW_MACS * world * total_rows / el / 1e12,
+        "roofline": {"bound": "mfma", "kernel": KERNEL_NAMES[dom], "layer": dom, "achieved": achieved,
+                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
+                     "traffic": None, "avg_launch_ms": dom_ms / dom_calls,
+                     "algorithmic_flops_per_launch": dom_flops_launch},
+        "layer_ms_per_step": {k: ms / args.steps for k, (ms, c) in layers.items()},
+        "device_forward_ms_per_step": fwd_ms / args.steps,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from expecto_amd.encode import seqs_to_codes
+        g1 = genome["chr1"]
+        rng = np.random.default_rng(5)
+        sample = [g1[p - 1000:p + 1000] for p in rng.integers(5000, len(g1) - 5000, 32)]
+        rec["cpu_baseline"] = cpu_baseline(sd_cpu, seqs_to_codes(sample), args.cpu_seconds,
+                                           min(args.cpu_threads, os.cpu_count() or 1), 4 * S)
+        rec["speedup_vs_cpu_baseline"] = value / rec["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(rec))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -44,6 +44,27 @@ __global__ void variant_windows_kernel(const uint8_t* __restrict__ genome, long 
   *reinterpret_cast<unsigned*>(codes + ((long long)(allele * n_shift + j) * n + v) * kLen + i4) = packed;
 }
 
+// TSS tiling (compute_expecto_features.py:107-111): window of gene g at shift s covers the
+// 1-based positions tss + s*strand - 999 .. tss + s*strand + 1000 -> 0-based offset
+// tss_off[g] + s*strand - 999 + i.  Output codes[(g*n_shift + j)*2000 + i].
+__global__ void tss_windows_kernel(const uint8_t* __restrict__ genome, long long genome_len,
+                                   const long long* __restrict__ tss_off, const int8_t* __restrict__ strand,
+                                   const int* __restrict__ shifts, int n_shift, uint8_t* __restrict__ codes) {
+  const long long g = blockIdx.y;
+  const int j = blockIdx.z;
+  const int i4 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i4 >= kLen) return;
+  const long long base = tss_off[g] + (long long)shifts[j] * strand[g] - 999;
+  unsigned packed = 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const long long q = base + i4 + e;
+    const unsigned c = (q >= 0 && q < genome_len) ? genome[q] : 4u;
+    packed |= c << (8 * e);
+  }
+  *reinterpret_cast<unsigned*>(codes + (g * n_shift + j) * kLen + i4) = packed;
+}
+
 __global__ void diff_kernel(const float4* __restrict__ a, const float4* __restrict__ b, long long n4,
                             float4* __restrict__ out) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
@@ -52,9 +73,11 @@ __global__ void diff_kernel(const float4* __restrict__ a, const float4* __restri
   }
 }
 
-__global__ void diff_tail(const float* a, const float* b, long long start, long long n, float* out) {
-  const long long i = start + threadIdx.x;
-  if (i < n) out[i] = a[i] - b[i];
+__global__ void diff_scalar(const float* __restrict__ a, const float* __restrict__ b, long long start, long long n,
+                            float* __restrict__ out) {
+  for (long long i = start + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    out[i] = a[i] - b[i];
 }
 
 __global__ void fwd_rc_avg_kernel(const float* __restrict__ x, int rows, int cols, float* __restrict__ out) {
@@ -147,18 +170,35 @@ int expecto_variant_windows(const uint8_t* genome, long long genome_len, const l
   return check_launch("variant_windows");
 }
 
+int expecto_tss_windows(const uint8_t* genome, long long genome_len, const long long* tss_off, const int8_t* strand,
+                        int n_genes, const int* shifts, int n_shift, uint8_t* codes, void* stream) {
+  EXPECTO_REQUIRE(n_genes >= 0 && n_shift > 0 && n_shift <= 65535, "bad gene/shift count");
+  if (n_genes == 0) return EXPECTO_OK;
+  EXPECTO_REQUIRE(n_genes <= 65535, "at most 65535 genes per call");
+  EXPECTO_REQUIRE(genome && tss_off && strand && shifts && codes, "null argument");
+  dim3 grid((kLen / 4 + 255) / 256, n_genes, n_shift);
+  tss_windows_kernel<<<grid, dim3(256), 0, as_stream(stream)>>>(genome, genome_len, tss_off, strand, shifts, n_shift,
+                                                                codes);
+  return check_launch("tss_windows");
+}
+
 int expecto_diff(const float* alt, const float* ref, long long count, float* out, void* stream) {
   EXPECTO_REQUIRE(count >= 0, "negative count");
   if (count == 0) return EXPECTO_OK;
   EXPECTO_REQUIRE(alt && ref && out, "null argument");
-  EXPECTO_REQUIRE(((uintptr_t)alt | (uintptr_t)ref | (uintptr_t)out) % 16 == 0, "diff buffers must be 16-B aligned");
+  hipStream_t st = as_stream(stream);
+  if (((uintptr_t)alt | (uintptr_t)ref | (uintptr_t)out) % 16 != 0) {
+    const long long blocks = std::min<long long>((count + 255) / 256, 8192);
+    diff_scalar<<<dim3((unsigned)blocks), dim3(256), 0, st>>>(alt, ref, 0, count, out);
+    return check_launch("diff");
+  }
   const long long n4 = count / 4;
   if (n4 > 0) {
     const long long blocks = std::min<long long>((n4 + 255) / 256, 8192);
-    diff_kernel<<<dim3((unsigned)blocks), dim3(256), 0, as_stream(stream)>>>(
+    diff_kernel<<<dim3((unsigned)blocks), dim3(256), 0, st>>>(
         reinterpret_cast<const float4*>(alt), reinterpret_cast<const float4*>(ref), n4, reinterpret_cast<float4*>(out));
   }
-  if (count % 4) diff_tail<<<1, 4, 0, as_stream(stream)>>>(alt, ref, n4 * 4, count, out);
+  if (count % 4) diff_scalar<<<1, 64, 0, st>>>(alt, ref, n4 * 4, count, out);
   return check_launch("diff");
 }
 

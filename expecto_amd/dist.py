@@ -1,0 +1,60 @@
+"""One process per GPU: variant/gene sharding and the final gather to rank 0.
+
+Variants (and genes) are independent, so each rank takes a contiguous range and computes
+it with no data-path collective; the only exchange is the final gather of the per-shift
+outputs to rank 0 (``torch.distributed`` backend "nccl" = RCCL over xGMI on MI355X;
+"gloo" on CPU for tests), after which rank 0 writes the reference-layout files.
+Launch with ``python -m torch.distributed.run --nproc-per-node N ...``.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+
+def env_rank():
+    return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
+
+
+def init(backend: str | None = None):
+    """Initialise the process group when launched with WORLD_SIZE > 1; returns (rank, world, local)."""
+    import torch.distributed as dist
+
+    rank, world, local = env_rank()
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    return rank, world, local
+
+
+def shard_range(n: int, rank: int, world: int):
+    """Contiguous [lo, hi) range of n items for `rank` (first n % world ranks get one more)."""
+    q, r = divmod(n, world)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (1 if rank < r else 0)
+
+
+def gather_rows(t: torch.Tensor, dim: int, n_total: int, world: int):
+    """Gather the shards of `t` along `dim` (contiguous rank ranges of shard_range) to every rank.
+
+    Returns the full tensor (rank order = global order).  Uses one all_gather of
+    equally padded shards (RCCL ring over xGMI on the GPU)."""
+    import torch.distributed as dist
+
+    if world == 1:
+        return t
+    x = t.movedim(dim, 0).contiguous()
+    max_n = max(shard_range(n_total, r, world)[1] - shard_range(n_total, r, world)[0] for r in range(world))
+    pad = torch.zeros((max_n,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    pad[: x.shape[0]] = x
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad)
+    pieces = []
+    for r in range(world):
+        lo, hi = shard_range(n_total, r, world)
+        pieces.append(parts[r][: hi - lo])
+    return torch.cat(pieces, 0).movedim(0, dim)

@@ -76,15 +76,22 @@ class CodeGenome:
         self.offsets: dict[str, int] = {}
         self.lengths: dict[str, int] = {}
         pos = GUARD
+        bad_off, bad_chr = [], []
         for n in names:
             raw = np.frombuffer(fasta.raw(n), np.uint8)
             c = _LUT[raw]
-            c[c == 255] = CODE_ZERO  # non-ACGTN characters never reach a window on the device path
+            bad = np.nonzero(c == 255)[0]
+            if bad.size:  # characters encodeSeqs rejects: windows touching them raise KeyError
+                bad_off.append(bad + pos)
+                bad_chr.append(raw[bad])
+                c[bad] = CODE_ZERO
             codes[pos:pos + raw.size] = c
             self.offsets[n] = pos
             self.lengths[n] = raw.size
             pos += raw.size + GUARD
         self.codes = codes
+        self.invalid_offsets = np.concatenate(bad_off).astype(np.int64) if bad_off else np.zeros(0, np.int64)
+        self.invalid_chars = np.concatenate(bad_chr) if bad_chr else np.zeros(0, np.uint8)
 
     def offset(self, chrom: str, pos1: int) -> int:
         """Flat offset of the 1-based position ``pos1`` of ``chrom``."""

@@ -1,0 +1,197 @@
+"""TSS-tiling feature precompute on the device: drop-ins for the reference
+``compute_expecto_features.py`` and ``replicate_expecto_features.py`` CLIs.
+
+Per gene: 200 windows at ``tss + s*strand`` for ``s in range(-20000, 20000, 200)``
+(``compute_expecto_features.py:88,107-111``), the Beluga forward on each window and on
+its reverse complement (``:115-122``), ``pred = 0.5*(fwd+rc)`` (``:123``), and either the
+10x200 exp-decay reduction to 20020 float64 features (``:124-128``) or the raw
+``(200,2002)`` float32 ``pred`` per gene (``replicate_expecto_features.py:86``).
+
+All of it runs on the GPU for batches of genes: ``expecto_tss_windows`` cuts the windows
+from the HBM-resident genome, one ``forward_codes(BOTH)`` covers fwd and rc, and
+``expecto_tss_reduce`` / ``expecto_fwd_rc_average`` finish it.
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import os
+import sys
+
+import numpy as np
+import pandas as pd
+import torch
+
+from . import _lib
+from . import dist as edist
+from .beluga import Beluga, seeded
+from .features import TSS_SHIFTS, fwd_rc_average, tss_pos_weights, tss_reduce
+from .genome import DeviceGenome, Fasta
+
+
+class TSSPipeline:
+    def __init__(self, engine, dgenome, shifts=TSS_SHIFTS):
+        self.engine = engine
+        self.dg = dgenome
+        self.dev = dgenome.codes.device
+        self.shifts = list(shifts)
+        self.lib = _lib.load()
+        self.sh_d = torch.tensor(self.shifts, dtype=torch.int32, device=self.dev)
+        self.w_d = torch.from_numpy(tss_pos_weights(self.shifts)).to(self.dev)
+
+    def window_codes(self, chroms, tss, strands) -> torch.Tensor:
+        G, S = len(chroms), len(self.shifts)
+        off = np.array([self.dg.offset(c, int(t)) for c, t in zip(chroms, tss)], np.int64)
+        codes = torch.empty((G, S, 2000), dtype=torch.uint8, device=self.dev)
+        if G:
+            # keep the argument tensors referenced until the launch is queued (a temporary's
+            # block would go back to the caching allocator and be reused by the next one)
+            off_d = torch.from_numpy(off).to(self.dev)
+            strand_d = torch.tensor(np.asarray(strands, np.int8), device=self.dev)
+            _lib.check(self.lib.expecto_tss_windows(
+                _lib.dptr(self.dg.codes), self.dg.codes.numel(), _lib.dptr(off_d), _lib.dptr(strand_d), G,
+                _lib.dptr(self.sh_d), S, _lib.dptr(codes), _lib.stream_ptr()), "tss_windows")
+        return codes
+
+    def predict(self, chroms, tss, strands) -> torch.Tensor:
+        """[2 (fwd, rc), G, S, 2002] fp32."""
+        G, S = len(chroms), len(self.shifts)
+        codes = self.window_codes(chroms, tss, strands)
+        y = torch.empty((2, G, S, 2002), dtype=torch.float32, device=self.dev)
+        self.engine.forward_codes(codes.view(G * S, 2000), _lib.STRAND_BOTH, out=y.view(2 * G * S, 2002))
+        return y
+
+    def features(self, chroms, tss, strands) -> torch.Tensor:
+        """[G, 20020] float64 (compute_expecto_features.py:123-124)."""
+        y = self.predict(chroms, tss, strands)
+        return tss_reduce(y[0], y[1], self.w_d)
+
+    def pred_fwd_rc(self, chroms, tss, strands) -> torch.Tensor:
+        """[G, S, 2002] float32 0.5*(fwd+rc) (replicate_expecto_features.py:83)."""
+        y = self.predict(chroms, tss, strands)
+        G, S = y.shape[1], y.shape[2]
+        return fwd_rc_average(y.view(2 * G * S, 2002)).view(G, S, 2002)
+
+
+def _load_model(args) -> Beluga:
+    if getattr(args, "synthetic_weights", None) is not None:
+        m = seeded(args.synthetic_weights, gain=math.sqrt(6.0), max_batch=args.max_batch)
+    else:
+        m = Beluga(max_batch=args.max_batch)
+        m.load_state_dict(torch.load(args.weights, map_location="cpu", weights_only=True))
+        m.eval()
+    return m.cuda()
+
+
+def _common_args(p):
+    p.add_argument('--windowsize', action="store", dest="windowsize", type=int, default=2000)
+    p.add_argument('--cuda', action='store_true')
+    p.add_argument('--genome', default='./resources/hg19.fa')
+    p.add_argument('--weights', default='./resources/deepsea.beluga.pth')
+    p.add_argument('--synthetic-weights', type=int, default=None, dest='synthetic_weights')
+    p.add_argument('--max-batch', type=int, default=2048, dest='max_batch')
+    p.add_argument('--gene-batch', type=int, default=16, dest='gene_batch')
+
+
+def _anno_genes(path):
+    """(gene_id, chrom, CAGE_TSS, strand) per annotation row (replicate_expecto_features.py:40-43)."""
+    out = []
+    for i, line in enumerate(open(path)):
+        if i == 0:
+            continue
+        gene_id, _, chrom, strand, _, tss, _ = line.rstrip().split(",")
+        out.append((gene_id, chrom, int(tss), 1 if strand == "+" else -1))
+    return out
+
+
+def _batches(items, size):
+    for i in range(0, len(items), size):
+        yield items[i:i + size]
+
+
+def compute_main(argv=None):
+    """compute_expecto_features.py main() (:17-128)."""
+    p = argparse.ArgumentParser(description='Compute ExPecto chromatin features for TSS list')
+    p.add_argument('annoFile')
+    p.add_argument('tss_file')
+    p.add_argument('-o', dest="out_dir", type=str, default='temp_compute_expecto_features')
+    p.add_argument('--no-liftover', action='store_true', dest='no_liftover',
+                   help='treat every hg38 TSS as unmapped (the reference needs the liftover package)')
+    _common_args(p)
+    args = p.parse_args(argv)
+    if args.windowsize != 2000:
+        raise ValueError("--windowsize must be 2000 (Beluga.py:43)")
+    os.makedirs(args.out_dir, exist_ok=True)
+    fasta = Fasta(args.genome)
+    model = _load_model(args)
+    tss_df = pd.read_csv(args.tss_file, sep='\t', index_col=0).set_index('ens_id')
+    if args.no_liftover:
+        converter = None
+    else:
+        try:
+            from liftover import get_lifter
+        except ImportError as e:
+            raise RuntimeError("the hg38->hg19 TSS override needs the `liftover` package; "
+                               "pass --no-liftover to keep the annotated TSSs") from e
+        converter = get_lifter('hg38', 'hg19')
+    genes = []
+    found = no_map = 0
+    for i, line in enumerate(open(args.annoFile)):
+        if i == 0:
+            continue
+        gene_id, _, chrom, strand, _, tss, _ = line.rstrip().split(",")
+        if gene_id in tss_df.index:
+            found += 1
+            chrom38, tss38, strand, _, is_default = tss_df.loc[gene_id]
+            coords = converter.convert_coordinate(chrom38, tss38) if converter is not None else []
+            if len(coords) == 0:
+                no_map += 1
+            elif not is_default:
+                assert len(coords) == 1, f"hg38 to hg19 conversion returned multiple entries for {chrom38}," \
+                                         f"position {tss38}"
+                chrom, tss, _ = coords[0]
+        genes.append((gene_id, chrom, int(tss), 1 if strand == "+" else -1))
+    print(f"Found {found} genes in geneAnno file that match a TSS in provided TSS file...")
+    print(f"Failed to convert {no_map} hg38 positions to hg19 with liftover tool...")
+    anno = pd.read_csv(args.annoFile, index_col=0)
+    changed = sum(1 for g, c, t, s in genes if anno.loc[g, 'CAGE_representative_TSS'] != t)
+    print(f"Found {changed} altered TSSs out of {anno.shape[0]} total TSSs...")
+    dg = DeviceGenome(fasta)
+    pipe = TSSPipeline(model.engine(), dg)
+    feats = []
+    for b in _batches(genes, args.gene_batch):
+        f = pipe.features([g[1] for g in b], [g[2] for g in b], [g[3] for g in b])
+        feats.append(f.cpu().numpy())
+    arr = np.concatenate(feats, 0) if feats else np.zeros((0, 20020))
+    np.save(f'{args.out_dir}/Xreducedall.2002.representative_tss_top', arr)
+    return arr
+
+
+def replicate_main(argv=None):
+    """replicate_expecto_features.py main() (:16-86): one (200,2002) float32 .npy per gene."""
+    p = argparse.ArgumentParser(description='Replicate ExPecto chromatin features')
+    p.add_argument('annoFile')
+    p.add_argument('-o', dest="out_dir", type=str, default='temp_replicate_expecto_features')
+    _common_args(p)
+    args = p.parse_args(argv)
+    if args.windowsize != 2000:
+        raise ValueError("--windowsize must be 2000 (Beluga.py:43)")
+    rank, world, local = edist.init()
+    os.makedirs(args.out_dir, exist_ok=True)
+    fasta = Fasta(args.genome)
+    model = _load_model(args)
+    genes = _anno_genes(args.annoFile)
+    lo, hi = edist.shard_range(len(genes), rank, world)   # per-gene files: no collective
+    dg = DeviceGenome(fasta)
+    pipe = TSSPipeline(model.engine(), dg)
+    for b in _batches(genes[lo:hi], args.gene_batch):
+        pred = pipe.pred_fwd_rc([g[1] for g in b], [g[2] for g in b], [g[3] for g in b]).cpu().numpy()
+        for g, pr in zip(b, pred):
+            np.save(f'{args.out_dir}/{g[0]}', pr)
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "replicate":
+        replicate_main(sys.argv[2:])
+    else:
+        compute_main(sys.argv[1:] if len(sys.argv) > 1 and sys.argv[1] != "compute" else sys.argv[2:])

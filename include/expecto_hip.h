@@ -18,6 +18,8 @@
  *                                  is generated inside the conv1 kernel from base codes
  *   expecto_variant_windows        fetchSeqs window splice for SNVs (chromatin.py:175-209)
  *                                  from a device-resident genome
+ *   expecto_tss_windows            TSS tiling genome.sequence(...) + encodeSeqs
+ *                                  (compute_expecto_features.py:107-113)
  *   expecto_diff                   diff = alt - ref (chromatin.py:281)
  *   expecto_fwd_rc_average         (x[:N] + x[N:]) / 2 (predict.py:186-190;
  *                                   0.5*(fwd+rc) of compute_expecto_features.py:123)
@@ -93,6 +95,12 @@ int expecto_beluga_layer_times(expecto_beluga_t h, double* ms, long long* calls,
 int expecto_variant_windows(const uint8_t* genome, long long genome_len, const long long* var_off,
                             const uint8_t* ref_code, const uint8_t* alt_code, int n,
                             const int* shifts, int n_shift, uint8_t* codes, void* stream);
+
+/* TSS tiling windows (compute_expecto_features.py:107-111): gene g, shift j covers the
+ * 0-based genome offsets tss_off[g] + shifts[j]*strand[g] - 999 + i, i = 0..1999
+ * (strand = +1/-1).  Output codes[(g*n_shift + j)*2000 + i]. */
+int expecto_tss_windows(const uint8_t* genome, long long genome_len, const long long* tss_off, const int8_t* strand,
+                        int n_genes, const int* shifts, int n_shift, uint8_t* codes, void* stream);
 
 /* out[i] = a[i] - b[i], i < count (fp32). */
 int expecto_diff(const float* alt, const float* ref, long long count, float* out, void* stream);

@@ -1,0 +1,94 @@
+"""End-to-end CLI parity on the GPU: chromatin.py shift sweep -> .diff.h5, TSS features,
+replicate per-gene predictions, and predict.py's variant feature reduction -- each against
+the golden vectors produced by running the reference (tests/golden/make_golden.py)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, assert_close
+
+pytestmark = pytest.mark.gpu
+
+GENOME_ARGS = dict(n_contigs=3, contig_len=60000, seed=7)   # = make_golden.GENOME_ARGS
+
+
+@pytest.fixture(scope="module")
+def workdir(tmp_path_factory):
+    from expecto_amd import synthetic
+    d = tmp_path_factory.mktemp("pipe")
+    synthetic.write_fasta(str(d / "hg19.fa"), synthetic.genome_bytes(**GENOME_ARGS))
+    return d
+
+
+def test_chromatin_cli_matches_reference(workdir, capsys):
+    from expecto_amd import chromatin, h5
+    vcf = workdir / "in.vcf"
+    with open(vcf, "w") as f:
+        f.write("##fileformat=VCFv4.1\n")
+        f.write(open(os.path.join(GOLDEN, "chromatin_vcf.txt")).read())
+    out = workdir / "chrom_out"
+    chromatin.main([str(vcf), "--maxshift", "200", "--output_dir", str(out), "--genome", str(workdir / "hg19.fa"),
+                    "--synthetic-weights", "0", "--max-batch", "40"])
+    printed = [l for l in capsys.readouterr().out.splitlines() if l.startswith("Number of")]
+    assert printed == open(os.path.join(GOLDEN, "chromatin_stdout.txt")).read().splitlines()
+    assert open(out / "snps_hg19.vcf").read() == open(os.path.join(GOLDEN, "chromatin_snps_hg19.vcf")).read()
+    gold = np.load(os.path.join(GOLDEN, "chromatin.npz"))
+    for s in (0, -200, 200):
+        got = h5.read(str(out / f"snps.shift_{s}.diff.h5"))
+        assert sorted(got) == ["alt", "diff", "ref"]
+        for k in ("ref", "alt", "diff"):
+            assert got[k].dtype == np.float32 and got[k].shape == gold[f"{k}_{s}"].shape
+            assert_close(got[k], gold[f"{k}_{s}"], what=f"shift {s} {k}")
+
+
+def test_tss_compute_and_replicate_match_reference(workdir):
+    from expecto_amd import tss
+    anno = workdir / "anno.csv"
+    anno.write_text("id,symbol,seqnames,strand,TSS,CAGE_representative_TSS,type\n"
+                    "ENSGT0001,G1,chr1,+,30000,30000,protein_coding\n"
+                    "ENSGT0002,G2,chr2,-,29000,29123,protein_coding\n")
+    tssf = workdir / "tss.tsv"
+    tssf.write_text("idx\tens_id\tchrom\ttss\tstrand\tcount\tis_default\n0\tENSGT0002\tchr2\t29123\t-\t5\tTrue\n")
+    out = workdir / "tss_out"
+    feats = tss.compute_main([str(anno), str(tssf), "-o", str(out), "--no-liftover", "--genome",
+                              str(workdir / "hg19.fa"), "--synthetic-weights", "0", "--gene-batch", "1"])
+    gold = np.load(os.path.join(GOLDEN, "tss.npz"))
+    saved = np.load(out / "Xreducedall.2002.representative_tss_top.npy")
+    assert saved.dtype == np.float64 and saved.shape == (2, 20020)
+    assert_close(saved, gold["features"], what="TSS features")
+    assert_close(feats, gold["features"], what="TSS features (returned)")
+    anno1 = workdir / "anno1.csv"
+    anno1.write_text("id,symbol,seqnames,strand,TSS,CAGE_representative_TSS,type\n"
+                     "ENSGT0002,G2,chr2,-,29000,29123,protein_coding\n")
+    rep = workdir / "rep_out"
+    tss.replicate_main([str(anno1), "-o", str(rep), "--genome", str(workdir / "hg19.fa"), "--synthetic-weights",
+                        "0"])
+    pr = np.load(rep / "ENSGT0002.npy")
+    assert pr.dtype == np.float32 and tuple(pr.shape) == tuple(gold["rep_shape"])
+    assert_close(pr[::8], gold["rep_rows"], what="replicate rows")
+    assert abs(pr.astype(np.float64).sum() - gold["rep_sum"][0]) <= 1e-4 * abs(gold["rep_sum"][0])
+
+
+def test_variant_feature_reduction_matches_predict_py():
+    """predict.py:87-136 on the reference's own chromatin outputs (captured golden)."""
+    import torch
+    from expecto_amd.features import fwd_rc_average, variant_features
+    gold = np.load(os.path.join(GOLDEN, "chromatin.npz"))
+    feats = np.load(os.path.join(GOLDEN, "predict_features.npz"))
+    rows = [r.split("\t") for r in feats["gene_rows"]]
+    coor = [r.split("\t") for r in feats["coor_rows"]]
+    key = lambda r: (r[0].replace("chr", ""), r[2] if len(r) > 5 else r[1])
+    vidx = [next(i for i, c in enumerate(coor) if c[0].replace("chr", "") == r[0] and c[1] == r[2]) for r in rows]
+    shifts = [0, -200, 200]
+    out = {}
+    for name in ("diff", "ref", "alt"):
+        eff = []
+        for s in shifts:
+            x = torch.from_numpy(gold[f"{name}_{s}"]).cuda()
+            eff.append(fwd_rc_average(x)[torch.tensor(vidx, device="cuda")])
+        eff = torch.stack(eff, 0)
+        dist = -np.array([int(r[-1]) for r in rows])
+        strand = np.array([r[-3] == "+" for r in rows])
+        out[name] = variant_features(eff, dist, strand, shifts).cpu().numpy()
+        assert_close(out[name], feats[name], rtol=1e-9, atol=1e-12, what=f"variant features {name}")

@@ -1,0 +1,63 @@
+"""CPU: the self-contained HDF5 writer/reader (the .diff.h5 output layout)."""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+H5PY_PY = "/opt/conda/bin/python3.9"   # h5py 3.3.0 lives only in this container's conda python
+
+
+def test_reader_parses_reference_example_file():
+    from expecto_amd import h5
+    d = h5.read(os.path.join(GOLDEN, "example.vcf.shift_0.diff.h5"))
+    assert list(d) == ["pred"]
+    assert d["pred"].shape == (20, 2002) and d["pred"].dtype == np.float32
+    assert 0.18 < float(np.abs(d["pred"]).max()) < 0.2          # |pred| max 0.19
+
+
+def test_roundtrip(tmp_path):
+    from expecto_amd import h5
+    rng = np.random.default_rng(0)
+    data = {"diff": rng.standard_normal((6, 2002)).astype(np.float32),
+            "ref": rng.random((6, 2002), dtype=np.float32), "alt": rng.random((6, 2002), dtype=np.float32),
+            "f64": rng.standard_normal((3, 5)), "vec": np.arange(7, dtype=np.float64), "empty": np.zeros((0, 2002),
+                                                                                                   np.float32)}
+    p = str(tmp_path / "x.h5")
+    h5.write(p, data)
+    back = h5.read(p)
+    assert sorted(back) == sorted(data)
+    for k in data:
+        assert back[k].dtype == data[k].dtype and np.array_equal(back[k], data[k]), k
+
+
+def test_header_bytes_match_h5py_layout(tmp_path):
+    """Superblock and root group bytes equal the reference file's (h5py-written) up to the
+    EOF address, for a single 'pred' dataset of the same shape."""
+    from expecto_amd import h5
+    ref = open(os.path.join(GOLDEN, "example.vcf.shift_0.diff.h5"), "rb").read()
+    p = str(tmp_path / "p.h5")
+    h5.write(p, {"pred": np.zeros((20, 2002), np.float32)})
+    mine = open(p, "rb").read()
+    assert len(mine) == len(ref)
+    assert mine[:40] == ref[:40] and mine[48:136] == ref[48:136]   # skip nothing but the B-tree/heap body
+
+
+@pytest.mark.skipif(not os.path.exists(H5PY_PY), reason="no h5py interpreter in this environment")
+def test_h5py_reads_our_files(tmp_path):
+    from expecto_amd import h5
+    rng = np.random.default_rng(1)
+    a = rng.random((12, 2002), dtype=np.float32)
+    p = str(tmp_path / "snps.shift_0.diff.h5")
+    h5.write(p, {"diff": a - 0.5, "ref": a, "alt": a * 2})
+    np.save(str(tmp_path / "a.npy"), a)
+    code = ("import h5py, numpy as np, sys; f = h5py.File(sys.argv[1], 'r'); a = np.load(sys.argv[2]);"
+            "assert sorted(f.keys()) == ['alt','diff','ref'];"
+            "assert f['ref'].dtype == np.float32 and f['ref'].shape == (12, 2002);"
+            "assert np.array_equal(f['ref'][:], a) and np.array_equal(f['alt'][:], a*2);"
+            "assert np.array_equal(f['diff'][6:12, :], (a-0.5)[6:12]); print('ok')")
+    r = subprocess.run([H5PY_PY, "-c", code, p, str(tmp_path / "a.npy")], capture_output=True, text=True)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr
