@@ -11,7 +11,8 @@
 //   act5 [ 125][640]  conv6 (106 valid)               -> buffer Q
 // With channel-last rows the im2col row of output position t of a k=8 conv is the
 // CONTIGUOUS slice X[t*Cin : (t+8)*Cin], so every conv is a GEMM with an overlapping
-// (Toeplitz) A operand: A[m][k] = X[m*Cin + k], K = 8*Cin, B = W repacked [Cout][tap*Cin+ci].
+// (Toeplitz) A operand: A[m][tap,ci] = X[(m+tap)*Cin + ci], K = 8*Cin, taken in the order
+// [ci/32][tap][ci%32] (B = W repacked [Cout][ci/32][tap][ci%32]).
 // FC1 reads the first 106 rows of act5 as one 67840-long row (weights permuted from the
 // reference flatten order c*106+t to t*640+c).
 #include <hip/hip_runtime.h>
@@ -51,6 +52,7 @@ struct GemmArgs {
   const float* B;  // [Npad][ldb], K-contiguous
   long long ldb;
   int kper;        // K range per split, multiple of GBK
+  int taps;        // conv: 8 (K order = [ci/32][tap][ci%32]); fc: 1
   int n_tiles;
   long long m_tiles;
   int m_fastest;
@@ -93,18 +95,26 @@ __global__ __launch_bounds__(256, 2) void beluga_gemm(GemmArgs p) {
   const int lr = tid >> 3, lc = (tid & 7) << 2;
   const long long m0 = mt * GBM;
   const int n0 = nt * GBN;
-  const long long kb = (long long)ks * p.kper;
+  // K stages: global stage gs -> (chunk = gs / taps, tap = gs % taps).  A stage = rows
+  // m+tap of channels chunk*32..+31 (taps innermost keeps the 32-channel slice L1/L2-hot
+  // across the 8 taps); B is repacked in the same [chunk][tap][32] order, so its stage
+  // offset is simply gs*32.
+  const int gs0 = ks * (p.kper / GBK);
 
   const float* ag[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     long long m = m0 + lr + 32 * i;
     if (m > p.M - 1) m = p.M - 1;  // clamp: tail rows read valid memory, never stored
-    ag[i] = p.A + m * p.lda + kb + lc;
+    ag[i] = p.A + m * p.lda + lc;
   }
   const float* bg[GTN];
 #pragma unroll
-  for (int i = 0; i < GTN; ++i) bg[i] = p.B + (long long)(n0 + lr + 32 * i) * p.ldb + kb + lc;
+  for (int i = 0; i < GTN; ++i) bg[i] = p.B + (long long)(n0 + lr + 32 * i) * p.ldb + (long long)gs0 * GBK + lc;
+  auto a_off = [&](int gs) -> long long {
+    const int chunk = gs / p.taps, tap = gs - chunk * p.taps;
+    return (long long)tap * p.lda + chunk * GBK;
+  };
 
   floatx4 ra[4], rb[GTN];
   const int wave = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
@@ -120,8 +130,11 @@ __global__ __launch_bounds__(256, 2) void beluga_gemm(GemmArgs p) {
   const float* bw = Bs + li * LDS_STRIDE + 4 * lh;
   const int nk = p.kper / GBK;
 
+  {
+    const long long ao = a_off(gs0);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) ra[i] = *(const floatx4*)(ag[i]);
+    for (int i = 0; i < 4; ++i) ra[i] = *(const floatx4*)(ag[i] + ao);
+  }
 #pragma unroll
   for (int i = 0; i < GTN; ++i) rb[i] = *(const floatx4*)(bg[i]);
 #pragma unroll
@@ -134,8 +147,9 @@ __global__ __launch_bounds__(256, 2) void beluga_gemm(GemmArgs p) {
     const bool more = (s + 1) < nk;
     if (more) {
       const int k0 = (s + 1) * GBK;
+      const long long ao = a_off(gs0 + s + 1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ra[i] = *(const floatx4*)(ag[i] + k0);
+      for (int i = 0; i < 4; ++i) ra[i] = *(const floatx4*)(ag[i] + ao);
 #pragma unroll
       for (int i = 0; i < GTN; ++i) rb[i] = *(const floatx4*)(bg[i] + k0);
     }
@@ -292,8 +306,8 @@ __global__ void repack_conv(const float* __restrict__ W, int cout, int cin, int 
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= npad * K) return;
   const int n = (int)(i / K);
-  const int k = (int)(i % K);
-  const int tap = k / cin, ci = k % cin;
+  const int k = (int)(i % K);  // kernel K order [ci/32][tap][ci%32] (cin is a multiple of 32)
+  const int chunk = k / (8 * GBK), tap = (k / GBK) % 8, ci = chunk * GBK + k % GBK;
   Wt[i] = n < cout ? W[((long long)n * cin + ci) * 8 + tap] : 0.f;
 }
 
@@ -422,6 +436,7 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st) {
   EXPECTO_REQUIRE(nblk > 0 && nblk < (1LL << 31), "gemm grid out of range");
   EXPECTO_REQUIRE(a.kper % GBK == 0 && a.kper > 0, "gemm K not a multiple of 32");
   EXPECTO_REQUIRE(a.lda % 4 == 0 && a.ldb % 4 == 0, "gemm leading dims must be multiples of 4");
+  EXPECTO_REQUIRE(a.taps == 1 || (a.taps == 8 && a.lda % GBK == 0), "conv GEMM needs Cin % 32 == 0");
   beluga_gemm<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
   return check_launch("beluga_gemm");
 }
@@ -447,6 +462,7 @@ int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long 
     a.B = h->wt[l];
     a.ldb = 8LL * g.cin;
     a.kper = 8 * g.cin;
+    a.taps = 8;
     a.n_tiles = npad_of(g.cout) / GBN;
     a.m_tiles = (a.M + GBM - 1) / GBM;
     a.m_fastest = 0;
@@ -484,6 +500,7 @@ int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long 
     a.B = h->fc1w;
     a.ldb = kFc1In;
     a.kper = kFc1In / splits;
+    a.taps = 1;
     a.n_tiles = n_tiles1;
     a.m_tiles = m_tiles;
     a.m_fastest = 1;
@@ -509,6 +526,7 @@ int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long 
     a.B = h->fc2w;
     a.ldb = kHidLd;
     a.kper = kHidLd;
+    a.taps = 1;
     a.n_tiles = npad_of(kNFeat) / GBN;
     a.m_tiles = m_tiles;
     a.m_fastest = 1;
