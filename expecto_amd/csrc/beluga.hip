@@ -3,17 +3,17 @@
 //
 // Replaces the ATen ops launched by Beluga.forward (reference Beluga.py:18-51,
 // SURVEY.md 2.2).  Layout in HBM (per window, channel-last, fp32):
-//   act0 [2000][320]  conv1 out (1993 valid)          -> buffer P
-//   act1 [ 500][320]  conv2+pool (496 valid)          -> buffer Q
-//   act2 [ 500][480]  conv3 (489 valid)               -> buffer P
-//   act3 [ 125][480]  conv4+pool (120 valid)          -> buffer Q
-//   act4 [ 125][640]  conv5 (113 valid)               -> buffer P
-//   act5 [ 125][640]  conv6 (106 valid)               -> buffer Q
+//   act0 [1996][320]  conv1 out (1993 valid)          -> buffer P
+//   act1 [ 496][320]  conv2+pool (496 valid)          -> buffer Q
+//   act2 [ 492][480]  conv3 (489 valid)               -> buffer P
+//   act3 [ 120][480]  conv4+pool (120 valid)          -> buffer Q
+//   act4 [ 113][640]  conv5 (113 valid)               -> buffer P
+//   act5 [ 106][640]  conv6 (106 valid)               -> buffer Q
 // With channel-last rows the im2col row of output position t of a k=8 conv is the
 // CONTIGUOUS slice X[t*Cin : (t+8)*Cin], so every conv is a GEMM with an overlapping
 // (Toeplitz) A operand: A[m][tap,ci] = X[(m+tap)*Cin + ci], K = 8*Cin, taken in the order
 // [ci/32][tap][ci%32] (B = W repacked [Cout][ci/32][tap][ci%32]).
-// FC1 reads the first 106 rows of act5 as one 67840-long row (weights permuted from the
+// FC1 reads the 106 rows of act5 as one 67840-long row (weights permuted from the
 // reference flatten order c*106+t to t*640+c).
 #include <hip/hip_runtime.h>
 
@@ -23,205 +23,19 @@
 #include <vector>
 
 #include "common.h"
+#include "gemm_kernel.h"
 
 namespace expecto {
-
-typedef float floatx4 __attribute__((ext_vector_type(4)));
-typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kLen = 2000;         // input window (chromatin.py:35-36, fixed by FC1)
 constexpr int kNFeat = 2002;
 constexpr int kFc1In = 67840;      // 640 * 106
 constexpr int kFc1Out = 2003;
 constexpr int kHidLd = 2016;       // FC1 output row stride = FC2 K (2003 padded to 32)
-
-// GEMM tile: 128 rows x 160 cols x 32 k, 4 waves stacked along M (each 32 x 160 =
-// five 32x32 accumulators of v_mfma_f32_32x32x2_f32).
-constexpr int GBM = 128;
-constexpr int GBN = 160;
-constexpr int GBK = 32;
-constexpr int LDS_STRIDE = GBK + 4;  // 144-B rows: ds_read_b128 lane groups conflict-free
-constexpr int GTN = GBN / 32;
-
-enum { EPI_RELU = 0, EPI_RELU_POOL4 = 1, EPI_SIGMOID = 2, EPI_PARTIAL = 3 };
-
-struct GemmArgs {
-  const float* A;
-  long long lda;
-  long long M;
-  const float* B;  // [Npad][ldb], K-contiguous
-  long long ldb;
-  int kper;        // K range per split, multiple of GBK
-  int taps;        // conv: 8 (K order = [ci/32][tap][ci%32]); fc: 1
-  int n_tiles;
-  long long m_tiles;
-  int m_fastest;
-  const float* bias;
-  float* C;
-  long long ldc;
-  int n_store;
-  int s_in;     // rows per window in the A/M index space
-  int t_valid;  // valid output positions (pooled count for EPI_RELU_POOL4)
-  int s_out;    // rows per window in C
-  long long split_stride;
-};
-
-// LAYER only makes the symbol distinct per layer (rocprof attributes time per layer).
-template <int LAYER, int EPI>
-__global__ __launch_bounds__(256, 2) void beluga_gemm(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) float smem[(GBM + GBN) * LDS_STRIDE];
-  float* As = smem;
-  float* Bs = smem + GBM * LDS_STRIDE;
-
-  // XCD-aware remap: blocks b, b+8, b+16.. share an XCD; give them consecutive tiles.
-  const unsigned nblk = gridDim.x, bid = blockIdx.x;
-  const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
-  const unsigned lin = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
-  long long mt;
-  int nt, ks;
-  if (p.m_fastest) {
-    mt = lin % p.m_tiles;
-    const long long rest = lin / p.m_tiles;
-    nt = (int)(rest % p.n_tiles);
-    ks = (int)(rest / p.n_tiles);
-  } else {
-    nt = (int)(lin % (unsigned)p.n_tiles);
-    const long long rest = lin / (unsigned)p.n_tiles;
-    mt = rest % p.m_tiles;
-    ks = (int)(rest / p.m_tiles);
-  }
-
-  const int tid = threadIdx.x;
-  const int lr = tid >> 3, lc = (tid & 7) << 2;
-  const long long m0 = mt * GBM;
-  const int n0 = nt * GBN;
-  // K stages: global stage gs -> (chunk = gs / taps, tap = gs % taps).  A stage = rows
-  // m+tap of channels chunk*32..+31 (taps innermost keeps the 32-channel slice L1/L2-hot
-  // across the 8 taps); B is repacked in the same [chunk][tap][32] order, so its stage
-  // offset is simply gs*32.
-  const int gs0 = ks * (p.kper / GBK);
-
-  const float* ag[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    long long m = m0 + lr + 32 * i;
-    if (m > p.M - 1) m = p.M - 1;  // clamp: tail rows read valid memory, never stored
-    ag[i] = p.A + m * p.lda + lc;
-  }
-  const float* bg[GTN];
-#pragma unroll
-  for (int i = 0; i < GTN; ++i) bg[i] = p.B + (long long)(n0 + lr + 32 * i) * p.ldb + (long long)gs0 * GBK + lc;
-  auto a_off = [&](int gs) -> long long {
-    const int chunk = gs / p.taps, tap = gs - chunk * p.taps;
-    return (long long)tap * p.lda + chunk * GBK;
-  };
-
-  floatx4 ra[4], rb[GTN];
-  const int wave = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
-  floatx16 acc[GTN];
-#pragma unroll
-  for (int t = 0; t < GTN; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-
-  // k order inside a 32-deep stage: MFMA step s = 4g+qq, lane half h takes k = 8g+4h+qq,
-  // so each lane feeds 4 consecutive MFMAs from one ds_read_b128 (same order for A and B).
-  const float* aw = As + (wave * 32 + li) * LDS_STRIDE + 4 * lh;
-  const float* bw = Bs + li * LDS_STRIDE + 4 * lh;
-  const int nk = p.kper / GBK;
-
-  {
-    const long long ao = a_off(gs0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ra[i] = *(const floatx4*)(ag[i] + ao);
-  }
-#pragma unroll
-  for (int i = 0; i < GTN; ++i) rb[i] = *(const floatx4*)(bg[i]);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) *(floatx4*)(As + (lr + 32 * i) * LDS_STRIDE + lc) = ra[i];
-#pragma unroll
-  for (int i = 0; i < GTN; ++i) *(floatx4*)(Bs + (lr + 32 * i) * LDS_STRIDE + lc) = rb[i];
-  __syncthreads();
-
-  for (int s = 0; s < nk; ++s) {
-    const bool more = (s + 1) < nk;
-    if (more) {
-      const int k0 = (s + 1) * GBK;
-      const long long ao = a_off(gs0 + s + 1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ra[i] = *(const floatx4*)(ag[i] + ao);
-#pragma unroll
-      for (int i = 0; i < GTN; ++i) rb[i] = *(const floatx4*)(bg[i] + k0);
-    }
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const floatx4 a = *(const floatx4*)(aw + 8 * g);
-      floatx4 b[GTN];
-#pragma unroll
-      for (int t = 0; t < GTN; ++t) b[t] = *(const floatx4*)(bw + t * 32 * LDS_STRIDE + 8 * g);
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq)
-#pragma unroll
-        for (int t = 0; t < GTN; ++t)
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[qq], b[t][qq], acc[t], 0, 0, 0);
-    }
-    __syncthreads();
-    if (more) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) *(floatx4*)(As + (lr + 32 * i) * LDS_STRIDE + lc) = ra[i];
-#pragma unroll
-      for (int i = 0; i < GTN; ++i) *(floatx4*)(Bs + (lr + 32 * i) * LDS_STRIDE + lc) = rb[i];
-      __syncthreads();
-    }
-  }
-
-  // Epilogue. C/D layout of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5),
-  // so rows 4g..4g+3 of a pool window sit in registers 4q..4q+3 of ONE lane.
-  const long long mw = m0 + wave * 32;
-#pragma unroll
-  for (int t = 0; t < GTN; ++t) {
-    const int n = n0 + t * 32 + li;
-    if (n >= p.n_store) continue;
-    if (EPI == EPI_PARTIAL) {
-      float* cp = p.C + (long long)ks * p.split_stride + n;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const long long m = mw + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (m < p.M) cp[m * p.ldc] = acc[t][r];
-      }
-    } else if (EPI == EPI_RELU_POOL4) {
-      const float bn = p.bias[n];
-#pragma unroll
-      for (int qd = 0; qd < 4; ++qd) {
-        const long long m = mw + 8 * qd + 4 * lh;  // first of 4 pooled rows (multiple of 4)
-        if (m >= p.M) continue;
-        const long long w = m / p.s_in;
-        const int tp = (int)(m - w * p.s_in) >> 2;
-        if (tp >= p.t_valid) continue;
-        float mx = fmaxf(fmaxf(acc[t][4 * qd], acc[t][4 * qd + 1]), fmaxf(acc[t][4 * qd + 2], acc[t][4 * qd + 3]));
-        // maxpool(relu(x+b)) == relu(max(x)+b): x -> fl(x+b) and relu are monotone.
-        p.C[(w * p.s_out + tp) * p.ldc + n] = fmaxf(mx + bn, 0.f);
-      }
-    } else {
-      const float bn = p.bias[n];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const long long m = mw + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (m >= p.M) continue;
-        const long long w = m / p.s_in;
-        const int tpos = (int)(m - w * p.s_in);
-        if (tpos >= p.t_valid) continue;
-        const float v = acc[t][r] + bn;
-        float o;
-        if (EPI == EPI_SIGMOID)
-          o = 1.0f / (1.0f + expf(-v));
-        else
-          o = fmaxf(v, 0.f);
-        p.C[(w * p.s_out + tpos) * p.ldc + n] = o;
-      }
-    }
-  }
-}
+constexpr int kWM = 4;             // GEMM waves per block (stacked along M)
+constexpr int kMinBlocks = 2;      // resident blocks per CU the register budget targets
+constexpr int kPipe = 1;           // MFMA / ds_read interleave pinned (tools/gemm_bench A/B: +6-8 %)
+constexpr int GBM = 32 * kWM;      // GEMM tile rows
 
 // conv1 (4 -> 320, k=8): 32 FMAs per output; one window x 128 positions per block,
 // one output channel per thread (coalesced channel-last stores).  The input tile is built
@@ -232,7 +46,7 @@ constexpr int C1_T = 128;
 __global__ __launch_bounds__(320) void beluga_conv1(const float* __restrict__ x, const uint8_t* __restrict__ codes,
                                                     long long code_stride, int n_src, int mode, long long row0,
                                                     const float* __restrict__ w1, const float* __restrict__ b1,
-                                                    float* __restrict__ out) {
+                                                    float* __restrict__ out, int out_rows) {
   __shared__ floatx4 xs[C1_T + 8];
   const int t0 = blockIdx.x * C1_T;
   const long long win = blockIdx.y;
@@ -275,7 +89,7 @@ __global__ __launch_bounds__(320) void beluga_conv1(const float* __restrict__ x,
   for (int i = 0; i < 32; ++i) w[i] = w1[co * 32 + i];  // [ci*8 + k] as in the reference
   const float bco = b1[co];
   const int tmax = min(C1_T, kLen - 7 - t0);
-  float* o = out + (win * kLen + t0) * 320 + co;
+  float* o = out + (win * out_rows + t0) * 320 + co;
   for (int t = 0; t < tmax; ++t) {
     float s = 0.f;
 #pragma unroll
@@ -343,13 +157,16 @@ constexpr int kNumLayers = 9;
 struct ConvGeo {
   int cin, cout, s_in, t_valid, s_out, pool;
 };
-// conv2..conv6 (index 0..4) -- positions from SURVEY.md section 0 item 3.
+// conv2..conv6 (index 0..4) -- positions from SURVEY.md section 0 item 3.  Row strides per
+// window are the valid rows, rounded up to a multiple of 4 where a pool epilogue follows
+// (so a pool group never straddles two windows): 1993->1996, 489->492.
+constexpr int kS1 = 1996;  // conv1 output rows per window (1993 valid)
 constexpr ConvGeo kConv[5] = {
-    {320, 320, 2000, 496, 500, 1},  // conv2: 1986 valid -> pool 496
-    {320, 480, 500, 489, 500, 0},   // conv3
-    {480, 480, 500, 120, 125, 1},   // conv4: 482 valid -> pool 120
-    {480, 640, 125, 113, 125, 0},   // conv5
-    {640, 640, 125, 106, 125, 0},   // conv6
+    {320, 320, kS1, 496, 496, 1},  // conv2: 1986 valid -> pool 496
+    {320, 480, 496, 489, 492, 0},  // conv3
+    {480, 480, 492, 120, 120, 1},  // conv4: 482 valid -> pool 120
+    {480, 640, 120, 113, 113, 0},  // conv5
+    {640, 640, 113, 106, 106, 0},  // conv6 -> FC1 reads 106*640 = 67840 contiguous floats
 };
 constexpr int kFcSplits[] = {1, 2, 4, 5, 8, 10};  // divisors of 67840/32 = 2120
 }  // namespace
@@ -395,8 +212,8 @@ int dalloc(expecto_beluga* h, float** p, size_t nfloat) {
 
 int npad_of(int n) { return (n + GBN - 1) / GBN * GBN; }
 
-size_t p_floats(int nb) { return (size_t)nb * 2000 * 320 + 16 * 640; }
-size_t q_floats(int nb) { return (size_t)nb * 500 * 320 + 16 * 640; }
+size_t p_floats(int nb) { return (size_t)nb * kS1 * 320 + 16 * 640; }
+size_t q_floats(int nb) { return (size_t)nb * 496 * 320 + 16 * 640; }
 
 int resolve_events(expecto_beluga* h) {
   for (auto& pr : h->pending) {
@@ -437,7 +254,7 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st) {
   EXPECTO_REQUIRE(a.kper % GBK == 0 && a.kper > 0, "gemm K not a multiple of 32");
   EXPECTO_REQUIRE(a.lda % 4 == 0 && a.ldb % 4 == 0, "gemm leading dims must be multiples of 4");
   EXPECTO_REQUIRE(a.taps == 1 || (a.taps == 8 && a.lda % GBK == 0), "conv GEMM needs Cin % 32 == 0");
-  beluga_gemm<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
+  beluga_gemm<LAYER, EPI, kWM, kMinBlocks, GBK, kPipe><<<dim3((unsigned)nblk), dim3(64 * kWM), 0, st>>>(a);
   return check_launch("beluga_gemm");
 }
 
@@ -448,7 +265,7 @@ int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long 
   {
     LayerTimer lt(h, 0, st);
     dim3 grid((kLen - 7 + C1_T - 1) / C1_T, nb);
-    beluga_conv1<<<grid, dim3(320), 0, st>>>(x, codes, code_stride, n_src, mode, row0, h->w1, h->b1, h->P);
+    beluga_conv1<<<grid, dim3(320), 0, st>>>(x, codes, code_stride, n_src, mode, row0, h->w1, h->b1, h->P, kS1);
     if ((rc = check_launch("beluga_conv1"))) return rc;
   }
   float* src = h->P;
@@ -495,7 +312,7 @@ int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long 
   {
     GemmArgs a{};
     a.A = src;
-    a.lda = 125LL * 640;
+    a.lda = (long long)kFc1In;
     a.M = nb;
     a.B = h->fc1w;
     a.ldb = kFc1In;

@@ -1,0 +1,227 @@
+// fp32-MFMA implicit-GEMM kernel template (gfx950) shared by the library and tools/gemm_bench.
+//
+// C[m][n] = epilogue( sum_k A[m][k] * B[n][k] ), A rows may overlap (conv Toeplitz rows).
+// Tile: (32*WM) rows x 160 cols x BK k; WM waves stacked along M, each 32 x 160 =
+// five 32x32 accumulators of v_mfma_f32_32x32x2_f32 (exact fp32, fmaf-chain numerics).
+// K is consumed in 32-wide "blocks" (one (chunk, tap) pair of a conv); a BK=64 stage holds
+// two consecutive blocks.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace expecto {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int GBN = 160;
+constexpr int GBK = 32;               // K block (one conv (chunk, tap) pair)
+constexpr int GTN = GBN / 32;
+
+enum { EPI_RELU = 0, EPI_RELU_POOL4 = 1, EPI_SIGMOID = 2, EPI_PARTIAL = 3 };
+
+struct GemmArgs {
+  const float* A;
+  long long lda;
+  long long M;
+  const float* B;  // [Npad][ldb], K-contiguous
+  long long ldb;
+  int kper;        // K range per split, multiple of the stage depth BK
+  int taps;        // conv: 8 (K order = [ci/32][tap][ci%32]); fc: 1
+  int n_tiles;
+  long long m_tiles;
+  int m_fastest;
+  const float* bias;
+  float* C;
+  long long ldc;
+  int n_store;
+  int s_in;     // rows per window in the A/M index space
+  int t_valid;  // valid output positions (pooled count for EPI_RELU_POOL4)
+  int s_out;    // rows per window in C
+  long long split_stride;
+};
+
+// LAYER only makes the symbol distinct per layer (rocprof attributes time per layer).
+template <int LAYER, int EPI, int WM = 4, int MINB = 2, int BK = 32, int PIPE = 0>
+__global__ __launch_bounds__(64 * WM, MINB * WM / 4) void beluga_gemm(GemmArgs p) {
+  constexpr int BM = 32 * WM;
+  constexpr int NT = 64 * WM;
+  constexpr int LDS_STRIDE = BK + 4;             // rows of 36/68 floats: b128 reads conflict-free
+  constexpr int F4 = BK / 4;                     // float4 per tile row
+  constexpr int RSTEP = NT / F4;                 // rows covered by one load pass
+  constexpr int ALD = BM / RSTEP;                // float4 A loads per thread
+  constexpr int BLD = (GBN + RSTEP - 1) / RSTEP; // float4 B loads per thread
+  constexpr int KB = BK / GBK;                   // K blocks per stage
+  static_assert(BM % RSTEP == 0, "tile rows must be a multiple of the load pass");
+  __shared__ __attribute__((aligned(16))) float smem[(BM + GBN) * LDS_STRIDE];
+  float* As = smem;
+  float* Bs = smem + BM * LDS_STRIDE;
+
+  // XCD-aware remap: blocks b, b+8, b+16.. share an XCD; give them consecutive tiles.
+  const unsigned nblk = gridDim.x, bid = blockIdx.x;
+  const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
+  const unsigned lin = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  long long mt;
+  int nt, ks;
+  if (p.m_fastest) {
+    mt = lin % p.m_tiles;
+    const long long rest = lin / p.m_tiles;
+    nt = (int)(rest % p.n_tiles);
+    ks = (int)(rest / p.n_tiles);
+  } else {
+    nt = (int)(lin % (unsigned)p.n_tiles);
+    const long long rest = lin / (unsigned)p.n_tiles;
+    mt = rest % p.m_tiles;
+    ks = (int)(rest / p.m_tiles);
+  }
+
+  const int tid = threadIdx.x;
+  const int lr = tid / F4, lc = (tid % F4) * 4;
+  const int lkb = lc / GBK, lcc = lc % GBK;        // K block of this thread's A column
+  const long long m0 = mt * BM;
+  const int n0 = nt * GBN;
+  // K stages: global stage gs -> (chunk = gs / taps, tap = gs % taps).  A stage = rows
+  // m+tap of channels chunk*32..+31 (taps innermost keeps the 32-channel slice L1/L2-hot
+  // across the 8 taps); B is repacked in the same [chunk][tap][32] order, so its stage
+  // offset is simply gs*32.
+  const int gs0 = ks * (p.kper / GBK);             // first K block of this split
+
+  const float* ag[ALD];
+#pragma unroll
+  for (int i = 0; i < ALD; ++i) {
+    long long m = m0 + lr + RSTEP * i;
+    if (m > p.M - 1) m = p.M - 1;  // clamp: tail rows read valid memory, never stored
+    ag[i] = p.A + m * p.lda + lcc;
+  }
+  const float* bg[BLD];
+#pragma unroll
+  for (int i = 0; i < BLD; ++i) {
+    const int r = min(lr + RSTEP * i, GBN - 1);
+    bg[i] = p.B + (long long)(n0 + r) * p.ldb + (long long)gs0 * GBK + lc;
+  }
+  auto a_off = [&](int gs) -> long long {
+    const int chunk = gs / p.taps, tap = gs - chunk * p.taps;
+    return (long long)tap * p.lda + chunk * GBK;
+  };
+  auto b_ok = [&](int i) { return (GBN % RSTEP == 0) || (lr + RSTEP * i < GBN); };
+
+  floatx4 ra[ALD], rb[BLD];
+  const int wave = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
+  floatx16 acc[GTN];
+#pragma unroll
+  for (int t = 0; t < GTN; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  // k order inside a 32-deep stage: MFMA step s = 4g+qq, lane half h takes k = 8g+4h+qq,
+  // so each lane feeds 4 consecutive MFMAs from one ds_read_b128 (same order for A and B).
+  const float* aw = As + (wave * 32 + li) * LDS_STRIDE + 4 * lh;
+  const float* bw = Bs + li * LDS_STRIDE + 4 * lh;
+  const int nk = p.kper / BK;
+
+  auto gload = [&](int s) {
+    const long long ao = a_off(gs0 + s * KB + lkb);
+#pragma unroll
+    for (int i = 0; i < ALD; ++i) ra[i] = *(const floatx4*)(ag[i] + ao);
+#pragma unroll
+    for (int i = 0; i < BLD; ++i) rb[i] = *(const floatx4*)(bg[i] + s * BK);
+  };
+  auto sstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < ALD; ++i) *(floatx4*)(As + (lr + RSTEP * i) * LDS_STRIDE + lc) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BLD; ++i)
+      if (b_ok(i)) *(floatx4*)(Bs + (lr + RSTEP * i) * LDS_STRIDE + lc) = rb[i];
+  };
+
+  gload(0);
+  sstore();
+  __syncthreads();
+
+  for (int s = 0; s < nk; ++s) {
+    const bool more = (s + 1) < nk;
+    if (more) gload(s + 1);
+    // Fragment reads are software-pipelined one 8-k group ahead (two register sets), so
+    // the ds_read latency of group g+1 hides under the 20 MFMAs of group g.
+    floatx4 fa[2], fb[2][GTN];
+    fa[0] = *(const floatx4*)(aw);
+#pragma unroll
+    for (int t = 0; t < GTN; ++t) fb[0][t] = *(const floatx4*)(bw + t * 32 * LDS_STRIDE);
+#pragma unroll
+    for (int g = 0; g < BK / 8; ++g) {
+      const int cur = g & 1, nxt = cur ^ 1;
+      if (g + 1 < BK / 8) {
+        fa[nxt] = *(const floatx4*)(aw + 8 * (g + 1));
+#pragma unroll
+        for (int t = 0; t < GTN; ++t) fb[nxt][t] = *(const floatx4*)(bw + t * 32 * LDS_STRIDE + 8 * (g + 1));
+      }
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+        for (int t = 0; t < GTN; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[cur][qq], fb[cur][t][qq], acc[t], 0, 0, 0);
+      if (PIPE && g + 1 < BK / 8) {
+        // pin the order: the 1 + GTN reads of group g+1 interleave with group g's first MFMAs
+#pragma unroll
+        for (int i = 0; i < 1 + GTN; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 4 * GTN - 1 - GTN, 0);
+      }
+    }
+    __syncthreads();
+    if (more) {
+      sstore();
+      __syncthreads();
+    }
+  }
+
+  // Epilogue. C/D layout of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5),
+  // so rows 4g..4g+3 of a pool window sit in registers 4q..4q+3 of ONE lane.
+  const long long mw = m0 + wave * 32;
+#pragma unroll
+  for (int t = 0; t < GTN; ++t) {
+    const int n = n0 + t * 32 + li;
+    if (n >= p.n_store) continue;
+    if (EPI == EPI_PARTIAL) {
+      float* cp = p.C + (long long)ks * p.split_stride + n;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long long m = mw + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < p.M) cp[m * p.ldc] = acc[t][r];
+      }
+    } else if (EPI == EPI_RELU_POOL4) {
+      const float bn = p.bias[n];
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        const long long m = mw + 8 * qd + 4 * lh;  // first of 4 pooled rows (multiple of 4)
+        if (m >= p.M) continue;
+        const long long w = m / p.s_in;
+        const int tp = (int)(m - w * p.s_in) >> 2;
+        if (tp >= p.t_valid) continue;
+        float mx = fmaxf(fmaxf(acc[t][4 * qd], acc[t][4 * qd + 1]), fmaxf(acc[t][4 * qd + 2], acc[t][4 * qd + 3]));
+        // maxpool(relu(x+b)) == relu(max(x)+b): x -> fl(x+b) and relu are monotone.
+        p.C[(w * p.s_out + tp) * p.ldc + n] = fmaxf(mx + bn, 0.f);
+      }
+    } else {
+      const float bn = p.bias[n];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long long m = mw + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m >= p.M) continue;
+        const long long w = m / p.s_in;
+        const int tpos = (int)(m - w * p.s_in);
+        if (tpos >= p.t_valid) continue;
+        const float v = acc[t][r] + bn;
+        float o;
+        if (EPI == EPI_SIGMOID)
+          o = 1.0f / (1.0f + expf(-v));
+        else
+          o = fmaxf(v, 0.f);
+        p.C[(w * p.s_out + tpos) * p.ldc + n] = o;
+      }
+    }
+  }
+}
+
+}  // namespace expecto

@@ -1,0 +1,136 @@
+// A/B micro-benchmark of beluga_gemm variants on the conv2 / conv4 / fc1 shapes (gfx950).
+// Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/gemm_bench.hip -o tools/gemm_bench
+// Run:   tools/gemm_bench [windows=1000] [rounds=5]
+// Interleaved rounds in one process (cdna_hip_programming.md rule 24); outputs of every
+// variant are compared bitwise with variant 0 (same per-element K order => identical).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../expecto_amd/csrc/gemm_kernel.h"
+
+using namespace expecto;
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e = (x);                                                        \
+    if (e != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+struct Variant {
+  std::string name;
+  int bm;
+  std::function<void(const GemmArgs&, unsigned)> launch;
+};
+
+template <int L, int EPI, int WM, int MINB, int BK, int PIPE = 0>
+Variant mk(const char* name) {
+  return {name, 32 * WM, [](const GemmArgs& a, unsigned nblk) {
+            beluga_gemm<L, EPI, WM, MINB, BK, PIPE><<<nblk, 64 * WM>>>(a);
+          }};
+}
+
+static void fill(float* d, size_t n, float lo, float hi, unsigned seed) {
+  std::vector<float> h(n);
+  std::mt19937 g(seed);
+  std::uniform_real_distribution<float> u(lo, hi);
+  for (auto& x : h) x = u(g);
+  CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+}
+
+int main(int argc, char** argv) {
+  const int nb = argc > 1 ? atoi(argv[1]) : 1000;
+  const int rounds = argc > 2 ? atoi(argv[2]) : 5;
+  const char* which = argc > 3 ? argv[3] : "conv2";
+  struct Shape { const char* name; int cin, cout, s_in, t_valid, s_out, pool; double macs; };
+  Shape shapes[] = {{"conv2", 320, 320, 2000, 496, 500, 1, 1986.0 * 320 * 2560},
+                    {"conv3", 320, 480, 500, 489, 500, 0, 489.0 * 480 * 2560},
+                    {"conv4", 480, 480, 500, 120, 125, 1, 482.0 * 480 * 3840},
+                    {"conv6", 640, 640, 125, 106, 125, 0, 106.0 * 640 * 5120}};
+  Shape sh = shapes[0];
+  for (auto& x : shapes) if (!strcmp(x.name, which)) sh = x;
+  const long long M = (long long)nb * sh.s_in;
+  const size_t xa = (size_t)(M + 64) * sh.cin;
+  const int K = 8 * sh.cin;
+  const int npad = (sh.cout + GBN - 1) / GBN * GBN;
+  float *X, *W, *bias, *C0, *C1;
+  CK(hipMalloc(&X, xa * 4));
+  CK(hipMalloc(&W, (size_t)npad * K * 4));
+  CK(hipMalloc(&bias, npad * 4));
+  const size_t csz = (size_t)nb * sh.s_out * sh.cout;
+  CK(hipMalloc(&C0, csz * 4));
+  CK(hipMalloc(&C1, csz * 4));
+  fill(X, xa, 0.f, 1.f, 1);
+  fill(W, (size_t)npad * K, -0.05f, 0.05f, 2);
+  fill(bias, npad, -0.1f, 0.1f, 3);
+
+  std::vector<Variant> vs;
+  if (sh.pool) {
+    vs.push_back(mk<2, EPI_RELU_POOL4, 4, 2, 32>("wm4_b2_k32"));
+    vs.push_back(mk<2, EPI_RELU_POOL4, 4, 3, 32>("wm4_b3_k32"));
+    vs.push_back(mk<2, EPI_RELU_POOL4, 4, 2, 32, 1>("wm4_b2_pipe"));
+    vs.push_back(mk<2, EPI_RELU_POOL4, 4, 3, 32, 1>("wm4_b3_pipe"));
+    vs.push_back(mk<2, EPI_RELU_POOL4, 8, 1, 32, 1>("wm8_b1_pipe"));
+  } else {
+    vs.push_back(mk<3, EPI_RELU, 4, 2, 32>("wm4_b2_k32"));
+    vs.push_back(mk<3, EPI_RELU, 4, 3, 32>("wm4_b3_k32"));
+    vs.push_back(mk<3, EPI_RELU, 4, 2, 32, 1>("wm4_b2_pipe"));
+    vs.push_back(mk<3, EPI_RELU, 4, 3, 32, 1>("wm4_b3_pipe"));
+    vs.push_back(mk<3, EPI_RELU, 8, 1, 32, 1>("wm8_b1_pipe"));
+  }
+  auto args_for = [&](int bm, float* C) {
+    GemmArgs a{};
+    a.A = X; a.lda = sh.cin; a.M = M; a.B = W; a.ldb = K; a.kper = K; a.taps = 8;
+    a.n_tiles = npad / GBN; a.m_tiles = (M + bm - 1) / bm; a.m_fastest = 0; a.bias = bias;
+    a.C = C; a.ldc = sh.cout; a.n_store = sh.cout; a.s_in = sh.s_in; a.t_valid = sh.t_valid; a.s_out = sh.s_out;
+    return a;
+  };
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<std::vector<float>> times(vs.size());
+  std::vector<float> ref(csz), out(csz);
+  for (int r = 0; r < rounds; ++r) {
+    for (size_t v = 0; v < vs.size(); ++v) {
+      float* C = v == 0 ? C0 : C1;
+      CK(hipMemset(C, 0, csz * 4));
+      GemmArgs a = args_for(vs[v].bm, C);
+      unsigned nblk = (unsigned)(a.m_tiles * a.n_tiles);
+      vs[v].launch(a, nblk);  // warm
+      CK(hipEventRecord(e0));
+      vs[v].launch(a, nblk);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      times[v].push_back(ms);
+      if (r == 0) {
+        CK(hipMemcpy(v == 0 ? ref.data() : out.data(), C, csz * 4, hipMemcpyDeviceToHost));
+        if (v > 0 && memcmp(ref.data(), out.data(), csz * 4) != 0) {
+          size_t bad = 0;
+          for (size_t i = 0; i < csz; ++i) bad += ref[i] != out[i];
+          printf("MISMATCH variant %s: %zu elements differ\n", vs[v].name.c_str(), bad);
+        }
+      }
+    }
+  }
+  const double flops = 2.0 * sh.macs * nb;
+  printf("shape %s windows %d (M=%lld K=%d N=%d)\n", sh.name, nb, M, K, sh.cout);
+  for (size_t v = 0; v < vs.size(); ++v) {
+    auto t = times[v];
+    std::sort(t.begin(), t.end());
+    printf("  %-10s median %8.3f ms  min %8.3f ms  %7.1f TFLOP/s (median)\n", vs[v].name.c_str(), t[t.size() / 2],
+           t[0], flops / (t[t.size() / 2] * 1e-3) / 1e12);
+  }
+  return 0;
+}
