@@ -32,6 +32,10 @@ SIGNATURES = {
     "expecto_beluga_forward_onehot": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, c_vp, c_vp]),
     "expecto_beluga_forward_codes": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_longlong, ctypes.c_int,
                                                     c_vp, c_vp]),
+    "expecto_beluga_forward_segments": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_longlong,
+                                                       ctypes.c_int, c_vp, c_vp, c_vp, ctypes.c_int, c_vp, c_vp]),
+    "expecto_gather_segments": (ctypes.c_int, [c_vp, ctypes.c_longlong, c_vp, ctypes.c_int, ctypes.c_int, c_vp,
+                                               c_vp, c_vp, c_vp]),
     "expecto_beluga_set_profiling": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "expecto_beluga_layer_times": (ctypes.c_int, [c_vp, c_f64p, c_i64p, ctypes.c_int]),
     "expecto_variant_windows": (ctypes.c_int, [c_vp, ctypes.c_longlong, c_vp, c_vp, c_vp, ctypes.c_int, c_vp,

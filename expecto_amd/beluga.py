@@ -102,6 +102,31 @@ class BelugaEngine:
                                                          _lib.stream_ptr(stream)), "forward_codes")
         return out
 
+    def forward_segments(self, codes: torch.Tensor, seg_len: int, win_seg, win_off, win_row=None,
+                         strand_mode: int = _lib.STRAND_BOTH, out: torch.Tensor | None = None, stream=None):
+        """Windows that are slices of longer sequences (shared trunk, bit-identical outputs).
+
+        codes: uint8 [n_seg, >=seg_len] device; win_seg/win_off/win_row: host int arrays
+        (sorted by segment; offsets multiples of 4).  Returns [n_win or 2*n_win, 2002]."""
+        import numpy as np
+
+        if codes.dtype != torch.uint8 or codes.dim() != 2 or codes.shape[1] < seg_len or codes.stride(1) != 1:
+            raise RuntimeError("codes must be uint8 [n_seg, >=seg_len] with contiguous rows")
+        ws = np.ascontiguousarray(win_seg, np.int32)
+        wo = np.ascontiguousarray(win_off, np.int32)
+        wr = None if win_row is None else np.ascontiguousarray(win_row, np.int32)
+        n_win = int(ws.size)
+        rows = 2 * n_win if strand_mode == _lib.STRAND_BOTH else n_win
+        if out is None:
+            out = torch.empty((rows, N_FEATURES), device=codes.device, dtype=torch.float32)
+        if out.shape != (rows, N_FEATURES) or not out.is_contiguous():
+            raise RuntimeError("out must be contiguous [rows, 2002]")
+        _lib.check(self.lib.expecto_beluga_forward_segments(
+            self.handle, _lib.dptr(codes), codes.shape[0], int(seg_len), codes.stride(0), int(strand_mode),
+            ws.ctypes.data, wo.ctypes.data, None if wr is None else wr.ctypes.data, n_win, _lib.dptr(out),
+            _lib.stream_ptr(stream)), "forward_segments")
+        return out
+
     def set_profiling(self, on: bool):
         _lib.check(self.lib.expecto_beluga_set_profiling(self.handle, int(on)), "set_profiling")
 

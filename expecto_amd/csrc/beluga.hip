@@ -46,7 +46,7 @@ constexpr int C1_T = 128;
 __global__ __launch_bounds__(320) void beluga_conv1(const float* __restrict__ x, const uint8_t* __restrict__ codes,
                                                     long long code_stride, int n_src, int mode, long long row0,
                                                     const float* __restrict__ w1, const float* __restrict__ b1,
-                                                    float* __restrict__ out, int out_rows) {
+                                                    float* __restrict__ out, int out_rows, int len) {
   __shared__ floatx4 xs[C1_T + 8];
   const int t0 = blockIdx.x * C1_T;
   const long long win = blockIdx.y;
@@ -55,13 +55,13 @@ __global__ __launch_bounds__(320) void beluga_conv1(const float* __restrict__ x,
   for (int j = tid; j < C1_T + 7; j += 320) {
     const int pos = t0 + j;
     floatx4 v = {0.f, 0.f, 0.f, 0.f};
-    if (pos < kLen) {
+    if (pos < len) {
       if (x) {
-        const float* xr = x + r * (4 * kLen);
+        const float* xr = x + r * (4LL * len);
         v[0] = xr[pos];
-        v[1] = xr[kLen + pos];
-        v[2] = xr[2 * kLen + pos];
-        v[3] = xr[3 * kLen + pos];
+        v[1] = xr[len + pos];
+        v[2] = xr[2 * len + pos];
+        v[3] = xr[3 * len + pos];
       } else {
         long long src = r;
         bool rc = (mode == EXPECTO_STRAND_RC);
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(320) void beluga_conv1(const float* __restrict__ x,
           src = r - n_src;
           rc = true;
         }
-        const int pp = rc ? (kLen - 1 - pos) : pos;
+        const int pp = rc ? (len - 1 - pos) : pos;
         const unsigned c = codes[src * code_stride + pp];
         if (c < 4) {
           const unsigned ch = rc ? 3 - c : c;
@@ -88,7 +88,7 @@ __global__ __launch_bounds__(320) void beluga_conv1(const float* __restrict__ x,
 #pragma unroll
   for (int i = 0; i < 32; ++i) w[i] = w1[co * 32 + i];  // [ci*8 + k] as in the reference
   const float bco = b1[co];
-  const int tmax = min(C1_T, kLen - 7 - t0);
+  const int tmax = min(C1_T, len - 7 - t0);
   float* o = out + (win * out_rows + t0) * 320 + co;
   for (int t = 0; t < tmax; ++t) {
     float s = 0.f;
@@ -112,6 +112,47 @@ __global__ void fc1_reduce(const float* __restrict__ part, int splits, long long
   float s = 0.f;
   for (int k = 0; k < splits; ++k) s += part[k * split_stride + i];
   h1[i] = n < kFc1Out ? fmaxf(s + bias[n], 0.f) : 0.f;
+}
+
+// MaxPool(1,4) floor mode at pool phases p (segment path, SURVEY.md 5 "trunk sharing"):
+// out[(seg*n_ph + i)*s_out + g][c] = max_{j<4} in[seg*s_in + ph[i] + 4g + j][c],
+// g < (t_in - ph[i]) / 4.  ReLU was applied by the producing conv (Beluga.py:32-34 order).
+__global__ void pool4_phases(const float* __restrict__ in, int n_seg, int s_in, int t_in, int C,
+                             int n_ph, int4 ph, int s_out, float* __restrict__ out) {
+  const int c4 = threadIdx.x;           // C/4 float4 lanes
+  const int g = blockIdx.x;
+  const int i = blockIdx.y % n_ph;
+  const long long seg = blockIdx.y / n_ph;
+  const int p = i == 0 ? ph.x : i == 1 ? ph.y : i == 2 ? ph.z : ph.w;
+  if (c4 * 4 >= C || g >= (t_in - p) / 4) return;
+  const float* src = in + (seg * s_in + p + 4LL * g) * C + c4 * 4;
+  floatx4 m = *(const floatx4*)src;
+#pragma unroll
+  for (int j = 1; j < 4; ++j) {
+    const floatx4 v = *(const floatx4*)(src + (long long)j * C);
+    m[0] = fmaxf(m[0], v[0]);
+    m[1] = fmaxf(m[1], v[1]);
+    m[2] = fmaxf(m[2], v[2]);
+    m[3] = fmaxf(m[3], v[3]);
+  }
+  *(floatx4*)(out + ((seg * n_ph + i) * s_out + g) * C + c4 * 4) = m;
+}
+
+// FC1 row table of the windows of one segment chunk: window m of the chunk reads conv6
+// rows [off6, off6+106) of block (segment, pool2 phase).
+__global__ void seg_a_rows(const int* __restrict__ win_seg, const int* __restrict__ win_off,
+                           const int* __restrict__ win_row, int w0, int m_count, int seg_base, int rc, int seg_len,
+                           int n_ph, int4 ph_idx, int s7, long long row_base, long long* __restrict__ a_rows,
+                           long long* __restrict__ c_rows) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= m_count) return;
+  const int w = w0 + m;
+  c_rows[m] = row_base + (win_row ? win_row[w] : w);
+  const int o = rc ? seg_len - 2000 - win_off[w] : win_off[w];
+  const int q = o >> 2, p = q & 3, off6 = (q - p) >> 2;
+  const int pi = p == 0 ? ph_idx.x : p == 1 ? ph_idx.y : p == 2 ? ph_idx.z : ph_idx.w;
+  const long long blk = (long long)(win_seg[w] - seg_base) * n_ph + pi;
+  a_rows[m] = (blk * s7 + off6) * 640;
 }
 
 // ---- weight repacking (reference layouts -> kernel layouts) --------------------------
@@ -186,6 +227,12 @@ struct expecto_beluga {
   float* Q = nullptr;
   float* part = nullptr;
   float* h1 = nullptr;
+  long long* a_rows = nullptr;  // FC1 row table (segment path), max_batch entries
+  long long* c_rows = nullptr;  // FC2 output-row table (segment path), max_batch entries
+  int* win_seg_d = nullptr;     // window tables of the current segment call
+  int* win_off_d = nullptr;
+  int* win_row_d = nullptr;
+  int win_cap = 0;
   size_t bytes = 0;
   std::vector<void*> allocs;
   bool profiling = false;
@@ -258,50 +305,55 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st) {
   return check_launch("beluga_gemm");
 }
 
-// One chunk of nb windows; conv1 input from x (one-hot) or codes.
-int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long long code_stride, int n_src,
-                  int mode, long long row0, int nb, float* y, hipStream_t st) {
+int run_conv1(expecto_beluga* h, const float* x, const uint8_t* codes, long long code_stride, int n_src, int mode,
+              long long row0, int nb, int len, int out_rows, hipStream_t st) {
+  LayerTimer lt(h, 0, st);
+  dim3 grid((len - 7 + C1_T - 1) / C1_T, nb);
+  beluga_conv1<<<grid, dim3(320), 0, st>>>(x, codes, code_stride, n_src, mode, row0, h->w1, h->b1, h->P, out_rows,
+                                           len);
+  return check_launch("beluga_conv1");
+}
+
+// conv layer l (0 = conv2 .. 4 = conv6) over `groups` row groups of s_in rows each.
+int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long groups, int s_in, int t_valid,
+             int s_out, bool pool, hipStream_t st) {
+  const ConvGeo& g = kConv[l];
+  GemmArgs a{};
+  a.A = src;
+  a.lda = g.cin;
+  a.M = groups * s_in;
+  a.B = h->wt[l];
+  a.ldb = 8LL * g.cin;
+  a.kper = 8 * g.cin;
+  a.taps = 8;
+  a.n_tiles = npad_of(g.cout) / GBN;
+  a.m_tiles = (a.M + GBM - 1) / GBM;
+  a.m_fastest = 0;
+  a.bias = h->bt[l];
+  a.C = dst;
+  a.ldc = g.cout;
+  a.n_store = g.cout;
+  a.s_in = s_in;
+  a.t_valid = t_valid;
+  a.s_out = s_out;
+  LayerTimer lt(h, l + 1, st);
+  if (pool) {
+    EXPECTO_REQUIRE(s_in % 4 == 0, "pool epilogue needs 4-aligned row groups");
+    return l == 0 ? launch_gemm<2, EPI_RELU_POOL4>(a, 1, st) : launch_gemm<4, EPI_RELU_POOL4>(a, 1, st);
+  }
+  switch (l) {
+    case 1: return launch_gemm<3, EPI_RELU>(a, 1, st);
+    case 2: return launch_gemm<4, EPI_RELU>(a, 1, st);
+    case 3: return launch_gemm<5, EPI_RELU>(a, 1, st);
+    default: return launch_gemm<6, EPI_RELU>(a, 1, st);
+  }
+}
+
+// FC1 (split-K) + reduce + FC2/sigmoid for nb windows whose conv6 rows are at act
+// (+ a_rows[m] when given, else m*67840).
+int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb, float* y, hipStream_t st,
+           const long long* c_rows = nullptr) {
   int rc;
-  {
-    LayerTimer lt(h, 0, st);
-    dim3 grid((kLen - 7 + C1_T - 1) / C1_T, nb);
-    beluga_conv1<<<grid, dim3(320), 0, st>>>(x, codes, code_stride, n_src, mode, row0, h->w1, h->b1, h->P, kS1);
-    if ((rc = check_launch("beluga_conv1"))) return rc;
-  }
-  float* src = h->P;
-  float* dst = h->Q;
-  for (int l = 0; l < 5; ++l) {
-    const ConvGeo& g = kConv[l];
-    GemmArgs a{};
-    a.A = src;
-    a.lda = g.cin;
-    a.M = (long long)nb * g.s_in;
-    a.B = h->wt[l];
-    a.ldb = 8LL * g.cin;
-    a.kper = 8 * g.cin;
-    a.taps = 8;
-    a.n_tiles = npad_of(g.cout) / GBN;
-    a.m_tiles = (a.M + GBM - 1) / GBM;
-    a.m_fastest = 0;
-    a.bias = h->bt[l];
-    a.C = dst;
-    a.ldc = g.cout;
-    a.n_store = g.cout;
-    a.s_in = g.s_in;
-    a.t_valid = g.t_valid;
-    a.s_out = g.s_out;
-    LayerTimer lt(h, l + 1, st);
-    switch (l) {
-      case 0: rc = launch_gemm<2, EPI_RELU_POOL4>(a, 1, st); break;
-      case 1: rc = launch_gemm<3, EPI_RELU>(a, 1, st); break;
-      case 2: rc = launch_gemm<4, EPI_RELU_POOL4>(a, 1, st); break;
-      case 3: rc = launch_gemm<5, EPI_RELU>(a, 1, st); break;
-      default: rc = launch_gemm<6, EPI_RELU>(a, 1, st); break;
-    }
-    if (rc) return rc;
-    std::swap(src, dst);
-  }
-  // src now holds act5 (buffer Q): FC1 reads rows 0..105 of each window as one row.
   const long long m_tiles = (nb + GBM - 1) / GBM;
   const int n_tiles1 = npad_of(kFc1Out) / GBN;
   int splits = kFcSplits[0];
@@ -311,7 +363,8 @@ int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long 
   }
   {
     GemmArgs a{};
-    a.A = src;
+    a.A = act;
+    a.a_rows = a_rows;
     a.lda = (long long)kFc1In;
     a.M = nb;
     a.B = h->fc1w;
@@ -348,6 +401,7 @@ int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long 
     a.m_tiles = m_tiles;
     a.m_fastest = 1;
     a.bias = h->fc2b;
+    a.c_rows = c_rows;
     a.C = y;
     a.ldc = kNFeat;
     a.n_store = kNFeat;
@@ -356,6 +410,140 @@ int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long 
     a.s_out = 1;
     LayerTimer lt(h, 8, st);
     if ((rc = launch_gemm<8, EPI_SIGMOID>(a, 1, st))) return rc;
+  }
+  return EXPECTO_OK;
+}
+
+// One chunk of nb independent windows; conv1 input from x (one-hot) or codes.
+int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long long code_stride, int n_src,
+                  int mode, long long row0, int nb, float* y, hipStream_t st) {
+  int rc;
+  if ((rc = run_conv1(h, x, codes, code_stride, n_src, mode, row0, nb, kLen, kS1, st))) return rc;
+  float* src = h->P;
+  float* dst = h->Q;
+  for (int l = 0; l < 5; ++l) {
+    const ConvGeo& g = kConv[l];
+    if ((rc = run_conv(h, l, src, dst, nb, g.s_in, g.t_valid, g.s_out, g.pool != 0, st))) return rc;
+    std::swap(src, dst);
+  }
+  return run_fc(h, src, nullptr, nb, y, st);  // src = act5 (buffer Q), 106 x 640 rows per window
+}
+
+// ---- segment path: windows that are slices of longer sequences share the trunk --------
+// A segment of L codes (L % 4 == 0); a window at offset o (o % 4 == 0, o + 2000 <= L).
+// conv1..conv4 run once over the segment; pool1 is fused into conv2 (phase 0 serves every
+// window since o % 4 == 0); pool2 runs separately for each phase p = (o/4) % 4 present;
+// conv5/conv6 run per (segment, phase) block; FC1 reads each window's 106 conv6 rows
+// through a row table.  Every per-window output element is computed with the same operands
+// and K order as the per-window path, so results are bit-identical to it.
+struct SegGeo {
+  int L, T1, S1, P1, T3, T4, S5, T5, T6;
+  size_t p_rows_floats, q_rows_floats;  // per segment, given n_ph phases
+};
+
+SegGeo seg_geo(int L, int n_ph) {
+  SegGeo g{};
+  g.L = L;
+  g.T1 = L - 7;
+  g.S1 = (g.T1 + 3) / 4 * 4;
+  g.P1 = (g.T1 - 7) / 4;
+  g.T3 = g.P1 - 7;
+  g.T4 = g.T3 - 7;
+  g.S5 = g.T4 / 4;        // rows of the phase-0 pool2 block (the longest)
+  g.T5 = g.S5 - 7;
+  g.T6 = g.T5 - 7;
+  const size_t p_conv1 = (size_t)g.S1 * 320, p_conv3 = (size_t)g.T3 * 480, p_pool2 = (size_t)n_ph * g.S5 * 480,
+               p_conv6 = (size_t)n_ph * g.T6 * 640;
+  const size_t q_pool1 = (size_t)g.P1 * 320, q_conv4 = (size_t)g.T4 * 480, q_conv5 = (size_t)n_ph * g.T5 * 640;
+  g.p_rows_floats = std::max(std::max(p_conv1, p_conv3), std::max(p_pool2, p_conv6));
+  g.q_rows_floats = std::max(q_pool1, std::max(q_conv4, q_conv5));
+  return g;
+}
+
+int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, long long code_stride, int mode,
+                     const int* win_seg, const int* win_off, const int* win_row, int n_win, float* y,
+                     hipStream_t st) {
+  EXPECTO_REQUIRE(L >= kLen && L % 4 == 0, "segment length must be >= 2000 and a multiple of 4");
+  // phases present (fwd and, for BOTH, the mirrored rc offsets)
+  int present[4] = {0, 0, 0, 0};
+  for (int w = 0; w < n_win; ++w) {
+    EXPECTO_REQUIRE(win_seg[w] >= 0 && win_seg[w] < n_seg, "window segment out of range");
+    EXPECTO_REQUIRE(w == 0 || win_seg[w] >= win_seg[w - 1], "windows must be sorted by segment");
+    const int o = win_off[w];
+    EXPECTO_REQUIRE(o >= 0 && o % 4 == 0 && o + kLen <= L, "window offset must be 4-aligned inside the segment");
+    present[(o >> 2) & 3] = 1;
+    if (mode == EXPECTO_STRAND_BOTH) present[((L - kLen - o) >> 2) & 3] = 1;
+  }
+  int n_ph = 0, ph[4] = {0, 0, 0, 0}, ph_idx[4] = {0, 0, 0, 0};
+  for (int p = 0; p < 4; ++p)
+    if (present[p]) {
+      ph_idx[p] = n_ph;
+      ph[n_ph++] = p;
+    }
+  const SegGeo g = seg_geo(L, std::max(n_ph, 1));
+  const size_t p_cap = p_floats(h->max_batch) - 16 * 640, q_cap = q_floats(h->max_batch) - 16 * 640;
+  const int seg_cap = (int)std::min<size_t>(p_cap / g.p_rows_floats, q_cap / g.q_rows_floats);
+  EXPECTO_REQUIRE(seg_cap >= 1, "segment too long for this handle's workspace (raise max_batch)");
+  // window ranges per segment
+  std::vector<int> first(n_seg + 1, n_win);
+  for (int w = n_win - 1; w >= 0; --w) first[win_seg[w]] = w;
+  for (int sg = n_seg - 1; sg >= 0; --sg) first[sg] = std::min(first[sg], first[sg + 1]);
+  if (n_win > h->win_cap) {
+    if (h->win_seg_d) EXPECTO_HIP_CHECK(hipFree(h->win_seg_d));
+    if (h->win_off_d) EXPECTO_HIP_CHECK(hipFree(h->win_off_d));
+    if (h->win_row_d) EXPECTO_HIP_CHECK(hipFree(h->win_row_d));
+    h->win_seg_d = h->win_off_d = h->win_row_d = nullptr;
+    h->win_cap = 0;
+    EXPECTO_HIP_CHECK(hipMalloc(&h->win_seg_d, n_win * sizeof(int)));
+    EXPECTO_HIP_CHECK(hipMalloc(&h->win_off_d, n_win * sizeof(int)));
+    EXPECTO_HIP_CHECK(hipMalloc(&h->win_row_d, n_win * sizeof(int)));
+    h->win_cap = n_win;
+  }
+  if (win_row) {
+    for (int w = 0; w < n_win; ++w) EXPECTO_REQUIRE(win_row[w] >= 0 && win_row[w] < n_win, "window row out of range");
+    EXPECTO_HIP_CHECK(hipMemcpyAsync(h->win_row_d, win_row, n_win * sizeof(int), hipMemcpyHostToDevice, st));
+  }
+  EXPECTO_HIP_CHECK(hipMemcpyAsync(h->win_seg_d, win_seg, n_win * sizeof(int), hipMemcpyHostToDevice, st));
+  EXPECTO_HIP_CHECK(hipMemcpyAsync(h->win_off_d, win_off, n_win * sizeof(int), hipMemcpyHostToDevice, st));
+  const int strands = mode == EXPECTO_STRAND_BOTH ? 2 : 1;
+  int rc;
+  for (int sd = 0; sd < strands; ++sd) {
+    const bool is_rc = (mode == EXPECTO_STRAND_RC) || sd == 1;
+    for (int s0 = 0; s0 < n_seg;) {
+      // grow the chunk while the segment buffers and the FC workspace (<= max_batch windows) fit
+      int s1 = s0 + 1;
+      while (s1 < n_seg && s1 - s0 < seg_cap && first[s1 + 1] - first[s0] <= h->max_batch) ++s1;
+      const int w0 = first[s0], nw = first[s1] - first[s0];
+      EXPECTO_REQUIRE(nw <= h->max_batch, "more windows in one segment than max_batch");
+      const int ns = s1 - s0;
+      // conv1 from codes: virtual rows = segments; rc mode mirrors inside the kernel
+      if ((rc = run_conv1(h, nullptr, codes + (long long)s0 * code_stride, code_stride, ns,
+                          is_rc ? EXPECTO_STRAND_RC : EXPECTO_STRAND_FWD, 0, ns, L, g.S1, st)))
+        return rc;
+      // conv2 + pool1 (P -> Q), conv3 (Q -> P), conv4 unpooled (P -> Q)
+      if ((rc = run_conv(h, 0, h->P, h->Q, ns, g.S1, g.P1, g.P1, true, st))) return rc;
+      if ((rc = run_conv(h, 1, h->Q, h->P, ns, g.P1, g.T3, g.T3, false, st))) return rc;
+      if ((rc = run_conv(h, 2, h->P, h->Q, ns, g.T3, g.T4, g.T4, false, st))) return rc;
+      {  // pool2 phases (Q -> P)
+        LayerTimer lt(h, 3, st);
+        dim3 grid(g.S5, ns * n_ph);
+        pool4_phases<<<grid, dim3(480 / 4), 0, st>>>(h->Q, ns, g.T4, g.T4, 480, n_ph,
+                                                     make_int4(ph[0], ph[1], ph[2], ph[3]), g.S5, h->P);
+        if ((rc = check_launch("pool4_phases"))) return rc;
+      }
+      // conv5 (P -> Q), conv6 (Q -> P) over (segment, phase) blocks
+      if ((rc = run_conv(h, 3, h->P, h->Q, (long long)ns * n_ph, g.S5, g.T5, g.T5, false, st))) return rc;
+      if ((rc = run_conv(h, 4, h->Q, h->P, (long long)ns * n_ph, g.T5, g.T6, g.T6, false, st))) return rc;
+      if (nw > 0) {
+        seg_a_rows<<<dim3((nw + 255) / 256), dim3(256), 0, st>>>(
+            h->win_seg_d, h->win_off_d, win_row ? h->win_row_d : nullptr, w0, nw, s0, is_rc ? 1 : 0, L, n_ph,
+            make_int4(ph_idx[0], ph_idx[1], ph_idx[2], ph_idx[3]), g.T6, (long long)sd * n_win, h->a_rows,
+            h->c_rows);
+        if ((rc = check_launch("seg_a_rows"))) return rc;
+        if ((rc = run_fc(h, h->P, h->a_rows, nw, y, st, h->c_rows))) return rc;
+      }
+      s0 = s1;
+    }
   }
   return EXPECTO_OK;
 }
@@ -409,6 +597,12 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   if ((rc = dalloc(h, &h->P, pf)) || (rc = dalloc(h, &h->Q, qf)) || (rc = dalloc(h, &h->part, partf)) ||
       (rc = dalloc(h, &h->h1, (size_t)max_batch * kHidLd)))
     return fail(rc);
+  {
+    float* rows = nullptr;
+    if ((rc = dalloc(h, &rows, (size_t)max_batch * 4))) return fail(rc);
+    h->a_rows = reinterpret_cast<long long*>(rows);
+    h->c_rows = h->a_rows + max_batch;
+  }
   EXPECTO_HIP_CHECK(hipMemsetAsync(h->P, 0, pf * sizeof(float), st));
   EXPECTO_HIP_CHECK(hipMemsetAsync(h->Q, 0, qf * sizeof(float), st));
   EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
@@ -418,6 +612,9 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
 
 void expecto_beluga_destroy(expecto_beluga_t h) {
   if (!h) return;
+  if (h->win_seg_d) (void)hipFree(h->win_seg_d);
+  if (h->win_off_d) (void)hipFree(h->win_off_d);
+  if (h->win_row_d) (void)hipFree(h->win_row_d);
   for (void* p : h->allocs) hipFree(p);
   for (hipEvent_t e : h->ev_pool) hipEventDestroy(e);
   delete h;
@@ -457,6 +654,20 @@ int expecto_beluga_forward_codes(expecto_beluga_t h, const uint8_t* codes, int n
     if (rc) return rc;
   }
   return EXPECTO_OK;
+}
+
+int expecto_beluga_forward_segments(expecto_beluga_t h, const uint8_t* codes, int n_seg, int seg_len,
+                                    long long code_stride, int strand_mode, const int* win_seg, const int* win_off,
+                                    const int* win_row, int n_win, float* y, void* stream) {
+  EXPECTO_REQUIRE(h != nullptr, "null handle");
+  EXPECTO_REQUIRE(n_seg >= 0 && n_win >= 0, "negative count");
+  EXPECTO_REQUIRE(strand_mode >= 0 && strand_mode <= 2, "bad strand mode");
+  if (n_win == 0 || n_seg == 0) return EXPECTO_OK;
+  EXPECTO_REQUIRE(codes && y && win_seg && win_off, "null argument");
+  EXPECTO_REQUIRE(code_stride >= seg_len, "code_stride < seg_len");
+  EXPECTO_HIP_CHECK(hipSetDevice(h->device));
+  return forward_segments(h, codes, n_seg, seg_len, code_stride, strand_mode, win_seg, win_off, win_row, n_win, y,
+                          as_stream(stream));
 }
 
 int expecto_beluga_set_profiling(expecto_beluga_t h, int on) {

@@ -38,6 +38,8 @@ struct GemmArgs {
   int t_valid;  // valid output positions (pooled count for EPI_RELU_POOL4)
   int s_out;    // rows per window in C
   long long split_stride;
+  const long long* a_rows;  // optional: A row m starts at A + a_rows[m] (FC1 over segment windows)
+  const long long* c_rows;  // optional: C row of M row m (non-pool epilogues; FC2 output order)
 };
 
 // LAYER only makes the symbol distinct per layer (rocprof attributes time per layer).
@@ -90,7 +92,7 @@ __global__ __launch_bounds__(64 * WM, MINB * WM / 4) void beluga_gemm(GemmArgs p
   for (int i = 0; i < ALD; ++i) {
     long long m = m0 + lr + RSTEP * i;
     if (m > p.M - 1) m = p.M - 1;  // clamp: tail rows read valid memory, never stored
-    ag[i] = p.A + m * p.lda + lcc;
+    ag[i] = p.A + (p.a_rows ? p.a_rows[m] : m * p.lda) + lcc;
   }
   const float* bg[BLD];
 #pragma unroll
@@ -218,7 +220,8 @@ __global__ __launch_bounds__(64 * WM, MINB * WM / 4) void beluga_gemm(GemmArgs p
           o = 1.0f / (1.0f + expf(-v));
         else
           o = fmaxf(v, 0.f);
-        p.C[(w * p.s_out + tpos) * p.ldc + n] = o;
+        const long long orow = p.c_rows ? p.c_rows[m] : (w * p.s_out + tpos);
+        p.C[orow * p.ldc + n] = o;
       }
     }
   }

@@ -65,6 +65,27 @@ __global__ void tss_windows_kernel(const uint8_t* __restrict__ genome, long long
   *reinterpret_cast<unsigned*>(codes + (g * n_shift + j) * kLen + i4) = packed;
 }
 
+// grid: (ceil(seg_len/1024), n); 4 codes per thread.
+__global__ void gather_segments_kernel(const uint8_t* __restrict__ genome, long long genome_len,
+                                       const long long* __restrict__ start, int seg_len,
+                                       const int* __restrict__ splice_pos, const uint8_t* __restrict__ splice_code,
+                                       uint8_t* __restrict__ codes) {
+  const long long i = blockIdx.y;
+  const int j4 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (j4 >= seg_len) return;
+  const long long base = start[i];
+  const int sp = splice_code ? splice_pos[i] : -1;
+  unsigned packed = 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const long long q = base + j4 + e;
+    unsigned c = (q >= 0 && q < genome_len) ? genome[q] : 4u;
+    if (j4 + e == sp) c = splice_code[i];
+    packed |= c << (8 * e);
+  }
+  *reinterpret_cast<unsigned*>(codes + i * seg_len + j4) = packed;
+}
+
 __global__ void diff_kernel(const float4* __restrict__ a, const float4* __restrict__ b, long long n4,
                             float4* __restrict__ out) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
@@ -180,6 +201,18 @@ int expecto_tss_windows(const uint8_t* genome, long long genome_len, const long 
   tss_windows_kernel<<<grid, dim3(256), 0, as_stream(stream)>>>(genome, genome_len, tss_off, strand, shifts, n_shift,
                                                                 codes);
   return check_launch("tss_windows");
+}
+
+int expecto_gather_segments(const uint8_t* genome, long long genome_len, const long long* start, int n, int seg_len,
+                            const int* splice_pos, const uint8_t* splice_code, uint8_t* codes, void* stream) {
+  EXPECTO_REQUIRE(n >= 0 && seg_len > 0 && seg_len % 4 == 0, "bad segment shape (seg_len % 4 == 0)");
+  if (n == 0) return EXPECTO_OK;
+  EXPECTO_REQUIRE(n <= 65535, "at most 65535 segments per call");
+  EXPECTO_REQUIRE(genome && start && codes && (!splice_code || splice_pos), "null argument");
+  dim3 grid((seg_len / 4 + 255) / 256, n);
+  gather_segments_kernel<<<grid, dim3(256), 0, as_stream(stream)>>>(genome, genome_len, start, seg_len, splice_pos,
+                                                                    splice_code, codes);
+  return check_launch("gather_segments");
 }
 
 int expecto_diff(const float* alt, const float* ref, long long count, float* out, void* stream) {

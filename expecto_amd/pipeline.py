@@ -69,10 +69,32 @@ def match_counts(fasta, vs: VariantSet):
     return np.array(rm, bool), np.array(am, bool)
 
 
-class VariantPipeline:
-    """Holds the device genome + model engine; computes shift sweeps for variant batches."""
+def gather_segments(lib, dg, start: torch.Tensor, seg_len: int, splice_pos=None, splice_code=None,
+                    out: torch.Tensor | None = None) -> torch.Tensor:
+    """uint8 [n, seg_len] genome slices (+ optional single-base splice) on the device."""
+    n = start.numel()
+    codes = out if out is not None else torch.empty((n, seg_len), dtype=torch.uint8, device=start.device)
+    st = _lib.stream_ptr()
+    for i0 in range(0, n, 65535):
+        i1 = min(n, i0 + 65535)
+        _lib.check(lib.expecto_gather_segments(
+            _lib.dptr(dg.codes), dg.codes.numel(), _lib.dptr(start[i0:i1]), i1 - i0, seg_len,
+            None if splice_pos is None else _lib.dptr(splice_pos[i0:i1]),
+            None if splice_code is None else _lib.dptr(splice_code[i0:i1]), _lib.dptr(codes[i0:i1]), st),
+            "gather_segments")
+    return codes
 
-    def __init__(self, engine, fasta, dgenome, inputsize: int = 2000):
+
+class VariantPipeline:
+    """Holds the device genome + model engine; computes shift sweeps for variant batches.
+
+    SNVs go through the segment path: per (allele, variant) ONE sequence covering every
+    shift's window (length 2000 + max_shift - min_shift), so the conv trunk is computed once
+    per sequence instead of once per shift (outputs bit-identical to the per-window path).
+    Indels/MNPs, whose windows are length-changing splices, use the per-window path with
+    host-built codes; shift lists that are not 4-aligned use per-window device windows."""
+
+    def __init__(self, engine, fasta, dgenome, inputsize: int = 2000, use_segments: bool = True):
         if inputsize != 2000:
             raise ValueError("Beluga's FC1 fixes the input size at 2000 (Beluga.py:43)")
         self.engine = engine
@@ -80,54 +102,68 @@ class VariantPipeline:
         self.dg = dgenome
         self.device = dgenome.codes.device
         self.lib = _lib.load()
+        self.use_segments = use_segments
 
     def prepare(self, vs: VariantSet, shifts) -> dict:
-        """Host checks + the device-resident variant table (offsets, allele codes, shifts)."""
-        n = len(vs)
-        snv = np.array([len(r) == 1 and len(a) == 1 for r, a in zip(vs.ref, vs.alt)], bool)
-        off = np.array([self.dg.offset(c, int(p)) for c, p in zip(vs.chrom, vs.pos)], np.int64)
-        self._check_window_chars(off[snv], shifts)
-        rc = np.array([_allele_code(r) if s else 4 for r, s in zip(vs.ref, snv)], np.uint8)
-        ac = np.array([_allele_code(a) if s else 4 for a, s in zip(vs.alt, snv)], np.uint8)
-        prep = {"n": n, "S": len(shifts), "shifts": list(shifts),
-                "off": torch.from_numpy(off).to(self.device), "rc": torch.from_numpy(rc).to(self.device),
-                "ac": torch.from_numpy(ac).to(self.device),
-                "sh": torch.tensor(list(shifts), dtype=torch.int32, device=self.device), "host": None}
-        if n and not snv.all():
+        """Host checks + the device-resident variant tables (done once, outside the hot loop)."""
+        n, S = len(vs), len(shifts)
+        shifts = list(shifts)
+        snv = np.array([len(r) == 1 and len(a) == 1 for r, a in zip(vs.ref, vs.alt)], bool).reshape(-1)
+        off = np.array([self.dg.offset(c, int(p)) for c, p in zip(vs.chrom, vs.pos)], np.int64).reshape(-1)
+        snv_idx, ind_idx = np.nonzero(snv)[0], np.nonzero(~snv)[0]
+        self._check_window_chars(off[snv_idx], shifts)
+        rc = np.array([_allele_code(vs.ref[v]) for v in snv_idx], np.uint8).reshape(-1)
+        ac = np.array([_allele_code(vs.alt[v]) for v in snv_idx], np.uint8).reshape(-1)
+        ns = snv_idx.size
+        dev = self.device
+        prep = {"n": n, "S": S, "shifts": shifts, "snv_idx": torch.from_numpy(snv_idx).to(dev),
+                "ind_idx": torch.from_numpy(ind_idx).to(dev), "n_snv": ns, "n_ind": ind_idx.size,
+                "seg": None, "win": None, "ind_codes": None}
+        lo_s, hi_s = min(shifts), max(shifts)
+        if ns and S > 1 and self.use_segments and all((x - lo_s) % 4 == 0 for x in shifts):
+            L = 2000 + hi_s - lo_s
+            # segment a*ns + v; window (a, v, j) at offset shifts[j] - lo_s -> row (a*S + j)*ns + v
+            a_i, v_i, j_i = np.meshgrid(np.arange(2), np.arange(ns), np.arange(S), indexing="ij")
+            prep["seg"] = {
+                "L": L,
+                "start": torch.from_numpy(np.concatenate([off[snv_idx], off[snv_idx]]) + lo_s - 999).to(dev),
+                "splice_pos": torch.full((2 * ns,), 999 - lo_s, dtype=torch.int32, device=dev),
+                "splice_code": torch.from_numpy(np.concatenate([rc, ac])).to(dev),
+                "win_seg": (a_i * ns + v_i).ravel().astype(np.int32),
+                "win_off": (np.asarray(shifts)[j_i.ravel()] - lo_s).astype(np.int32),
+                "win_row": ((a_i * S + j_i) * ns + v_i).ravel().astype(np.int32),
+            }
+        elif ns:
+            prep["win"] = {"off": torch.from_numpy(off[snv_idx]).to(dev), "rc": torch.from_numpy(rc).to(dev),
+                           "ac": torch.from_numpy(ac).to(dev),
+                           "sh": torch.tensor(shifts, dtype=torch.int32, device=dev)}
+        if ind_idx.size:
             # indels / MNPs: length-changing splice + floor crop on the host (chromatin.py:164,209)
-            idx = np.nonzero(~snv)[0]
-            host = np.empty((2, len(shifts), idx.size, 2000), np.uint8)
-            for k, v in enumerate(idx):
+            host = np.empty((2, S, ind_idx.size, 2000), np.uint8)
+            for k, v in enumerate(ind_idx):
                 for j, sh in enumerate(shifts):
                     for a, allele in enumerate((vs.ref[v], vs.alt[v])):
                         w = fetch_window(self.fasta, vs.chrom[v], int(vs.pos[v]), vs.ref[v], allele, sh)
                         c = seq_codes(w)
                         host[a, j, k, :] = 4
                         host[a, j, k, :c.size] = c
-            prep["host"] = (torch.from_numpy(idx).to(self.device), torch.from_numpy(host).to(self.device))
+            prep["ind_codes"] = torch.from_numpy(host).to(dev)
         return prep
 
-    def window_codes(self, prep: dict, out: torch.Tensor | None = None) -> torch.Tensor:
-        """uint8 [2 alleles, S, n, 2000] on the device (no host work)."""
-        n, S = prep["n"], prep["S"]
-        codes = out if out is not None else torch.empty((2, S, n, 2000), dtype=torch.uint8, device=self.device)
-        if n == 0:
-            return codes
+    def _snv_window_codes(self, prep: dict) -> torch.Tensor:
+        """uint8 [2 alleles, S, n_snv, 2000] per-window codes on the device."""
+        ns, S, w = prep["n_snv"], prep["S"], prep["win"]
+        codes = torch.empty((2, S, ns, 2000), dtype=torch.uint8, device=self.device)
         st = _lib.stream_ptr()
-        for v0 in range(0, n, 65535):
-            v1 = min(n, v0 + 65535)
-            # the kernel writes [2][S][nv][2000]; split batches go through a scratch slab
-            blk = codes if (v0 == 0 and v1 == n) else torch.empty((2, S, v1 - v0, 2000), dtype=torch.uint8,
-                                                                   device=self.device)
+        for v0 in range(0, ns, 65535):
+            v1 = min(ns, v0 + 65535)
+            blk = codes if (v0 == 0 and v1 == ns) else torch.empty((2, S, v1 - v0, 2000), dtype=torch.uint8,
+                                                                    device=self.device)
             _lib.check(self.lib.expecto_variant_windows(
-                _lib.dptr(self.dg.codes), self.dg.codes.numel(), _lib.dptr(prep["off"][v0:v1]),
-                _lib.dptr(prep["rc"][v0:v1]), _lib.dptr(prep["ac"][v0:v1]), v1 - v0, _lib.dptr(prep["sh"]), S,
-                _lib.dptr(blk), st), "variant_windows")
+                _lib.dptr(self.dg.codes), self.dg.codes.numel(), _lib.dptr(w["off"][v0:v1]), _lib.dptr(w["rc"][v0:v1]),
+                _lib.dptr(w["ac"][v0:v1]), v1 - v0, _lib.dptr(w["sh"]), S, _lib.dptr(blk), st), "variant_windows")
             if blk is not codes:
                 codes[:, :, v0:v1] = blk
-        if prep["host"] is not None:
-            idx, host = prep["host"]
-            codes[:, :, idx] = host
         return codes
 
     def _check_window_chars(self, off, shifts):
@@ -143,16 +179,32 @@ class VariantPipeline:
             b = bad[i[np.nonzero(hit)[0][0]]]
             raise KeyError(chr(self.dg.host.invalid_chars[np.searchsorted(bad, b)]))
 
-    def predict(self, vs, shifts=None, out: torch.Tensor | None = None, codes: torch.Tensor | None = None):
+    def predict(self, vs, shifts=None, out: torch.Tensor | None = None):
         """y [2 strands, 2 alleles, S, n, 2002] fp32 on the device.  `vs` is a VariantSet
         (prepared here) or the dict returned by prepare()."""
         prep = vs if isinstance(vs, dict) else self.prepare(vs, shifts)
-        n, S = prep["n"], prep["S"]
-        codes = self.window_codes(prep, codes)
-        flat = codes.view(2 * S * n, 2000)
+        n, S, ns, ni = prep["n"], prep["S"], prep["n_snv"], prep["n_ind"]
         if out is None:
             out = torch.empty((2, 2, S, n, 2002), dtype=torch.float32, device=self.device)
-        self.engine.forward_codes(flat, _lib.STRAND_BOTH, out=out.view(4 * S * n, 2002))
+        if ns:
+            y = out if ni == 0 else torch.empty((2, 2, S, ns, 2002), dtype=torch.float32, device=self.device)
+            seg = prep["seg"]
+            if seg is not None:
+                scodes = gather_segments(self.lib, self.dg, seg["start"], seg["L"], seg["splice_pos"],
+                                         seg["splice_code"])
+                self.engine.forward_segments(scodes, seg["L"], seg["win_seg"], seg["win_off"], seg["win_row"],
+                                             _lib.STRAND_BOTH, out=y.view(4 * S * ns, 2002))
+            else:
+                codes = self._snv_window_codes(prep)
+                self.engine.forward_codes(codes.view(2 * S * ns, 2000), _lib.STRAND_BOTH,
+                                          out=y.view(4 * S * ns, 2002))
+            if ni:
+                out.index_copy_(3, prep["snv_idx"], y)
+        if ni:
+            yi = torch.empty((2, 2, S, ni, 2002), dtype=torch.float32, device=self.device)
+            self.engine.forward_codes(prep["ind_codes"].view(2 * S * ni, 2000), _lib.STRAND_BOTH,
+                                      out=yi.view(4 * S * ni, 2002))
+            out.index_copy_(3, prep["ind_idx"], yi)
         return out
 
     def diff(self, y: torch.Tensor) -> torch.Tensor:

@@ -27,6 +27,7 @@ from . import dist as edist
 from .beluga import Beluga, seeded
 from .features import TSS_SHIFTS, fwd_rc_average, tss_pos_weights, tss_reduce
 from .genome import DeviceGenome, Fasta
+from .pipeline import gather_segments
 
 
 class TSSPipeline:
@@ -53,11 +54,31 @@ class TSSPipeline:
                 _lib.dptr(self.sh_d), S, _lib.dptr(codes), _lib.stream_ptr()), "tss_windows")
         return codes
 
-    def predict(self, chroms, tss, strands) -> torch.Tensor:
-        """[2 (fwd, rc), G, S, 2002] fp32."""
+    def predict(self, chroms, tss, strands, use_segments: bool = True) -> torch.Tensor:
+        """[2 (fwd, rc), G, S, 2002] fp32.
+
+        Segment path: one sequence per gene covering all 200 windows (41.8 kb), trunk computed
+        once (bit-identical to the per-window path, which is kept for use_segments=False)."""
         G, S = len(chroms), len(self.shifts)
-        codes = self.window_codes(chroms, tss, strands)
         y = torch.empty((2, G, S, 2002), dtype=torch.float32, device=self.dev)
+        if G == 0:
+            return y
+        sh = np.asarray(self.shifts)
+        if use_segments and all((x - sh.min()) % 4 == 0 for x in sh):
+            strands = np.asarray(strands, np.int64)
+            off = np.array([self.dg.offset(c, int(t)) for c, t in zip(chroms, tss)], np.int64)
+            rel = sh[None, :] * strands[:, None]                  # window start - (tss_off - 999)
+            lo = rel.min(1)
+            L = 2000 + int((rel.max(1) - lo).max())
+            L += (-L) % 4
+            start = torch.from_numpy(off + lo - 999).to(self.dev)
+            codes = gather_segments(self.lib, self.dg, start, L)
+            win_seg = np.repeat(np.arange(G), S).astype(np.int32)
+            win_off = (rel - lo[:, None]).ravel().astype(np.int32)
+            self.engine.forward_segments(codes, L, win_seg, win_off, None, _lib.STRAND_BOTH,
+                                         out=y.view(2 * G * S, 2002))
+            return y
+        codes = self.window_codes(chroms, tss, strands)
         self.engine.forward_codes(codes.view(G * S, 2000), _lib.STRAND_BOTH, out=y.view(2 * G * S, 2002))
         return y
 

@@ -81,6 +81,27 @@ int expecto_beluga_forward_onehot(expecto_beluga_t h, const float* x, int n, flo
 int expecto_beluga_forward_codes(expecto_beluga_t h, const uint8_t* codes, int n, long long code_stride,
                                  int strand_mode, float* y, void* stream);
 
+/* Windows that are slices of longer sequences ("segments") with a shared trunk: segment i
+ * is seg_len codes at codes + i*code_stride (seg_len % 4 == 0); window w is the 2000 codes at
+ * offset win_off[w] (a multiple of 4) of segment win_seg[w] (HOST arrays, sorted by segment).
+ * conv1..conv4 run once per segment, conv5/conv6 once per (segment, pool2 phase), FC once per
+ * window; every output equals the per-window forward bit for bit.  y has n_win rows (FWD:
+ * the windows; RC: their reverse complements) or 2*n_win rows (BOTH: fwd rows then rc rows);
+ * window w lands in row win_row[w] of its strand block (HOST array, a permutation of
+ * 0..n_win-1; NULL = row w).
+ * Replaces the per-shift re-encoding + forward of chromatin.py:243-279 and the 200-window
+ * TSS tiling of compute_expecto_features.py:105-122. */
+int expecto_beluga_forward_segments(expecto_beluga_t h, const uint8_t* codes, int n_seg, int seg_len,
+                                    long long code_stride, int strand_mode, const int* win_seg, const int* win_off,
+                                    const int* win_row, int n_win, float* y, void* stream);
+
+/* Genome slices for segments: codes[i*seg_len + j] = genome[start[i] + j] (zero code outside
+ * [0, genome_len)), with codes[i*seg_len + splice_pos[i]] = splice_code[i] when splice_code
+ * is not NULL (the fetchSeqs allele splice of chromatin.py:209 for SNVs). */
+int expecto_gather_segments(const uint8_t* genome, long long genome_len, const long long* start, int n,
+                            int seg_len, const int* splice_pos, const uint8_t* splice_code, uint8_t* codes,
+                            void* stream);
+
 /* Per-layer device time accumulated over forward calls while profiling is on (ms).
  * Layers: 0 conv1, 1 conv2, 2 conv3, 3 conv4, 4 conv5, 5 conv6, 6 fc1, 7 fc1-reduce, 8 fc2.
  * `calls` receives the number of launches per layer.  Returns the number of layers. */

@@ -92,3 +92,65 @@ def test_variant_feature_reduction_matches_predict_py():
         strand = np.array([r[-3] == "+" for r in rows])
         out[name] = variant_features(eff, dist, strand, shifts).cpu().numpy()
         assert_close(out[name], feats[name], rtol=1e-9, atol=1e-12, what=f"variant features {name}")
+
+
+def _engine():
+    import math
+    from expecto_amd import beluga
+    return beluga.seeded(0, gain=math.sqrt(6.0), max_batch=300).cuda().engine()
+
+
+def test_segment_path_is_bitwise_equal_to_per_window_variants():
+    """Trunk sharing across shifts (segment path) reproduces the per-window forward exactly."""
+    import torch
+    from expecto_amd import synthetic
+    from expecto_amd.genome import DeviceGenome, Fasta
+    from expecto_amd.pipeline import VariantPipeline, VariantSet, shift_order
+    g = synthetic.genome_bytes(**GENOME_ARGS)
+    fa = Fasta.from_dict(g)
+    snv = synthetic.snvs(g, 23, seed=4)
+    vs = VariantSet([s[0] for s in snv], np.array([s[1] for s in snv]), [s[2] for s in snv], [s[3] for s in snv])
+    eng = _engine()
+    dg = DeviceGenome(fa)
+    for shifts in (shift_order(800), shift_order(200), [0, 400, -400]):
+        seg = VariantPipeline(eng, fa, dg, use_segments=True)
+        win = VariantPipeline(eng, fa, dg, use_segments=False)
+        ps = seg.prepare(vs, shifts)
+        assert ps["seg"] is not None
+        a = seg.predict(ps)
+        b = win.predict(vs, shifts)
+        assert torch.equal(a, b), f"segment path differs for shifts {shifts}: {float((a - b).abs().max())}"
+
+
+def test_segment_path_mixed_snv_and_indel_batch():
+    import torch
+    from expecto_amd import synthetic
+    from expecto_amd.genome import DeviceGenome, Fasta
+    from expecto_amd.pipeline import VariantPipeline, VariantSet, shift_order
+    g = synthetic.genome_bytes(**GENOME_ARGS)
+    fa = Fasta.from_dict(g)
+    snv = synthetic.snvs(g, 6, seed=9)
+    rows = [(c, p, r, a) for c, p, r, a in snv]
+    base = chr(g["chr2"][30000 - 1]).upper()
+    rows.insert(2, ("chr2", 30000, base, base + "GA"))
+    rows.insert(5, ("chr1", 25000, chr(g["chr1"][24999]).upper() + chr(g["chr1"][25000]).upper(),
+                    chr(g["chr1"][24999]).upper()))
+    vs = VariantSet([r[0] for r in rows], np.array([r[1] for r in rows]), [r[2] for r in rows], [r[3] for r in rows])
+    eng = _engine()
+    dg = DeviceGenome(fa)
+    a = VariantPipeline(eng, fa, dg, use_segments=True).predict(vs, shift_order(400))
+    b = VariantPipeline(eng, fa, dg, use_segments=False).predict(vs, shift_order(400))
+    assert torch.equal(a, b)
+
+
+def test_segment_path_is_bitwise_equal_to_per_window_tss():
+    import torch
+    from expecto_amd import synthetic
+    from expecto_amd.genome import DeviceGenome, Fasta
+    from expecto_amd.tss import TSSPipeline
+    fa = Fasta.from_dict(synthetic.genome_bytes(**GENOME_ARGS))
+    pipe = TSSPipeline(_engine(), DeviceGenome(fa))
+    genes = (["chr1", "chr2", "chr3"], [30000, 29123, 31000], [1, -1, -1])
+    a = pipe.predict(*genes, use_segments=True)
+    b = pipe.predict(*genes, use_segments=False)
+    assert torch.equal(a, b)
