@@ -33,6 +33,10 @@ from expecto_amd.pipeline import VariantPipeline, VariantSet  # noqa: E402
 
 METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+# bf16 dense MFMA peak: 256 CU x 4 SIMD x 1024 FLOP/clk (v_mfma_f32_32x32x16_bf16: 32768 FLOP
+# per 32 cycles) x 2.4 GHz = 2516.6 TFLOP/s (MI355X_MICROARCH.md "~2.5 PF dense")
+BF16_MFMA_PEAK_TFLOPS = 256 * 4 * 1024 * 2.4e9 / 1e12
+BF16X6_PRODUCTS = 6               # bf16 MFMA products per fp32 multiply-add in the bf16x6 kernel
 
 # per-window dense MACs of each layer, for the roofline of each kernel
 LAYER_MACS = {
@@ -40,9 +44,16 @@ LAYER_MACS = {
     "conv4": 482 * 480 * 3840, "conv5": 113 * 640 * 3840, "conv6": 106 * 640 * 5120,
     "fc1": 67840 * 2003, "fc1_reduce": 0, "fc2": 2003 * 2002,
 }
-KERNEL_NAMES = {"conv2": "beluga_gemm<2, 1>", "conv3": "beluga_gemm<3, 0>", "conv4": "beluga_gemm<4, 1>",
-                "conv5": "beluga_gemm<5, 0>", "conv6": "beluga_gemm<6, 0>", "fc1": "beluga_gemm<7, 3>",
-                "fc2": "beluga_gemm<8, 2>", "conv1": "beluga_conv1", "fc1_reduce": "fc1_reduce"}
+GEMM_LAYER_EPI = {"conv2": (2, 1), "conv3": (3, 0), "conv4": (4, 1), "conv5": (5, 0), "conv6": (6, 0),
+                  "fc1": (7, 3), "fc2": (8, 2)}
+
+
+def kernel_name(layer: str, precision: str) -> str:
+    """rocprofv3 kernel name of a layer's launch (per-window path)."""
+    if layer not in GEMM_LAYER_EPI:
+        return {"conv1": "beluga_conv1", "fc1_reduce": "fc1_reduce"}[layer]
+    l, e = GEMM_LAYER_EPI[layer]
+    return f"beluga_gemm_x6<{l}, {e}, 4, 1>" if precision == "bf16x6" else f"beluga_gemm<{l}, {e}, 4, 2, 32, 1>"
 WINDOW_MACS = sum(LAYER_MACS.values())
 
 
@@ -136,11 +147,19 @@ def main():
     dom = max((k for k in layers if LAYER_MACS[k]), key=lambda k: layers[k][0])
     dom_ms, dom_calls = layers[dom]
     dom_flops_launch = 2.0 * LAYER_MACS[dom] * total_rows / dom_calls
-    achieved = dom_flops_launch / (dom_ms / dom_calls / 1e3) / 1e12
+    algo_tflops = dom_flops_launch / (dom_ms / dom_calls / 1e3) / 1e12
+    if eng.precision == "bf16x6":
+        # roofline of the bf16 MFMA pipe: executed bf16 FLOPs = 6 x the fp32 algorithmic FLOPs
+        achieved, peak, flops_launch = BF16X6_PRODUCTS * algo_tflops, BF16_MFMA_PEAK_TFLOPS, \
+            BF16X6_PRODUCTS * dom_flops_launch
+    else:
+        achieved, peak, flops_launch = algo_tflops, FP32_MFMA_PEAK_TFLOPS, dom_flops_launch
     rec = {
         "metric": METRIC, "value": value, "unit": "variants/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32",
+        "vs_baseline": None,
+        "dtype": "fp32 (bf16x6: exact 3-way bf16 split, 6 MFMA products, fp32 accumulate)"
+                 if eng.precision == "bf16x6" else "fp32",
         "data": "synthetic: seeded genome (24 x 2 Mbp), seeded SNVs, seeded Beluga weights x sqrt(6)",
         "config": {"workload": f"configs[1]: {n} SNVs/GPU, shifts {shifts}, ref+alt x fwd+rc = "
                                f"{rows} Beluga windows/step/GPU (window gen + forward + diff)",
@@ -148,10 +167,12 @@ def main():
         "windows_per_s": world * total_rows / el,
         "variants_200shift_per_s": world * total_rows / el / 800.0,
         "forward_tflops": 2.0 * WINDOW_MACS * world * total_rows / el / 1e12,
-        "roofline": {"bound": "mfma", "kernel": KERNEL_NAMES[dom], "layer": dom, "achieved": achieved,
-                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
+        "roofline": {"bound": "mfma", "kernel": kernel_name(dom, eng.precision), "layer": dom, "achieved": achieved,
+                     "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
                      "traffic": None, "avg_launch_ms": dom_ms / dom_calls,
-                     "algorithmic_flops_per_launch": dom_flops_launch},
+                     "mfma_flops_per_launch": flops_launch,
+                     "algorithmic_fp32_flops_per_launch": dom_flops_launch,
+                     "algorithmic_fp32_tflops": algo_tflops, "precision": eng.precision},
         "layer_ms_per_step": {k: ms / args.steps for k, (ms, c) in layers.items()},
         "device_forward_ms_per_step": fwd_ms / args.steps,
     }

@@ -36,6 +36,8 @@ SIGNATURES = {
                                                        ctypes.c_int, c_vp, c_vp, c_vp, ctypes.c_int, c_vp, c_vp]),
     "expecto_gather_segments": (ctypes.c_int, [c_vp, ctypes.c_longlong, c_vp, ctypes.c_int, ctypes.c_int, c_vp,
                                                c_vp, c_vp, c_vp]),
+    "expecto_beluga_set_precision": (ctypes.c_int, [c_vp, ctypes.c_int]),
+    "expecto_beluga_get_precision": (ctypes.c_int, [c_vp]),
     "expecto_beluga_set_profiling": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "expecto_beluga_layer_times": (ctypes.c_int, [c_vp, c_f64p, c_i64p, ctypes.c_int]),
     "expecto_variant_windows": (ctypes.c_int, [c_vp, ctypes.c_longlong, c_vp, c_vp, c_vp, ctypes.c_int, c_vp,
@@ -52,6 +54,8 @@ SIGNATURES = {
 }
 
 STRAND_FWD, STRAND_RC, STRAND_BOTH = 0, 1, 2
+PRECISION_FP32, PRECISION_BF16X6 = 0, 1
+PRECISIONS = {"fp32": PRECISION_FP32, "bf16x6": PRECISION_BF16X6}
 N_LAYERS = 9
 LAYER_NAMES = ("conv1", "conv2", "conv3", "conv4", "conv5", "conv6", "fc1", "fc1_reduce", "fc2")
 

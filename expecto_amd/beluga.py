@@ -56,6 +56,15 @@ class BelugaEngine:
         self.handle = h
         self.device = device
         self.max_batch = max_batch
+        import os
+        self.set_precision(os.environ.get("EXPECTO_PRECISION", "bf16x6"))
+
+    def set_precision(self, precision: str):
+        """'bf16x6' (default, fp32-faithful split-bf16 MFMA) or 'fp32' (exact fp32 MFMA)."""
+        if precision not in _lib.PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(_lib.PRECISIONS)}")
+        _lib.check(self.lib.expecto_beluga_set_precision(self.handle, _lib.PRECISIONS[precision]), "set_precision")
+        self.precision = precision
 
     def __del__(self):
         h = getattr(self, "handle", None)

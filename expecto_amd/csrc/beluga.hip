@@ -235,6 +235,7 @@ struct expecto_beluga {
   int win_cap = 0;
   size_t bytes = 0;
   std::vector<void*> allocs;
+  int precision = EXPECTO_PRECISION_BF16X6;
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, int>> pending;  // (layer, event index of start)
@@ -294,6 +295,10 @@ struct LayerTimer {
   }
 };
 
+// Arithmetic of the MFMA GEMMs: exact fp32 (v_mfma_f32_32x32x2_f32) or the fp32-faithful
+// 3-way bf16 split (six v_mfma_f32_32x32x16_bf16 products per k-step, gemm_kernel.h).
+thread_local int g_precision = EXPECTO_PRECISION_BF16X6;
+
 template <int LAYER, int EPI>
 int launch_gemm(const GemmArgs& a, int splits, hipStream_t st) {
   const long long nblk = a.m_tiles * a.n_tiles * splits;
@@ -301,7 +306,10 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st) {
   EXPECTO_REQUIRE(a.kper % GBK == 0 && a.kper > 0, "gemm K not a multiple of 32");
   EXPECTO_REQUIRE(a.lda % 4 == 0 && a.ldb % 4 == 0, "gemm leading dims must be multiples of 4");
   EXPECTO_REQUIRE(a.taps == 1 || (a.taps == 8 && a.lda % GBK == 0), "conv GEMM needs Cin % 32 == 0");
-  beluga_gemm<LAYER, EPI, kWM, kMinBlocks, GBK, kPipe><<<dim3((unsigned)nblk), dim3(64 * kWM), 0, st>>>(a);
+  if (g_precision == EXPECTO_PRECISION_BF16X6)
+    beluga_gemm_x6<LAYER, EPI, kWM, 1><<<dim3((unsigned)nblk), dim3(64 * kWM), 0, st>>>(a);
+  else
+    beluga_gemm<LAYER, EPI, kWM, kMinBlocks, GBK, kPipe><<<dim3((unsigned)nblk), dim3(64 * kWM), 0, st>>>(a);
   return check_launch("beluga_gemm");
 }
 
@@ -418,6 +426,7 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
 int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long long code_stride, int n_src,
                   int mode, long long row0, int nb, float* y, hipStream_t st) {
   int rc;
+  g_precision = h->precision;
   if ((rc = run_conv1(h, x, codes, code_stride, n_src, mode, row0, nb, kLen, kS1, st))) return rc;
   float* src = h->P;
   float* dst = h->Q;
@@ -464,6 +473,7 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
                      const int* win_seg, const int* win_off, const int* win_row, int n_win, float* y,
                      hipStream_t st) {
   EXPECTO_REQUIRE(L >= kLen && L % 4 == 0, "segment length must be >= 2000 and a multiple of 4");
+  g_precision = h->precision;
   // phases present (fwd and, for BOTH, the mirrored rc offsets)
   int present[4] = {0, 0, 0, 0};
   for (int w = 0; w < n_win; ++w) {
@@ -669,6 +679,15 @@ int expecto_beluga_forward_segments(expecto_beluga_t h, const uint8_t* codes, in
   return forward_segments(h, codes, n_seg, seg_len, code_stride, strand_mode, win_seg, win_off, win_row, n_win, y,
                           as_stream(stream));
 }
+
+int expecto_beluga_set_precision(expecto_beluga_t h, int precision) {
+  EXPECTO_REQUIRE(h != nullptr, "null handle");
+  EXPECTO_REQUIRE(precision == EXPECTO_PRECISION_FP32 || precision == EXPECTO_PRECISION_BF16X6, "bad precision");
+  h->precision = precision;
+  return EXPECTO_OK;
+}
+
+int expecto_beluga_get_precision(expecto_beluga_t h) { return h ? h->precision : EXPECTO_EINVAL; }
 
 int expecto_beluga_set_profiling(expecto_beluga_t h, int on) {
   EXPECTO_REQUIRE(h != nullptr, "null handle");

@@ -42,6 +42,58 @@ struct GemmArgs {
   const long long* c_rows;  // optional: C row of M row m (non-pool epilogues; FC2 output order)
 };
 
+// Epilogue shared by both GEMM kernels. C/D layout of 32x32 MFMA (every dtype on gfx950):
+// col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5), so rows 4g..4g+3 of a pool window sit
+// in registers 4q..4q+3 of ONE lane.
+template <int EPI>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, const floatx16 (&acc)[GTN], long long mw, int n0,
+                                              int ks, int li, int lh) {
+#pragma unroll
+  for (int t = 0; t < GTN; ++t) {
+    const int n = n0 + t * 32 + li;
+    if (n >= p.n_store) continue;
+    if (EPI == EPI_PARTIAL) {
+      float* cp = p.C + (long long)ks * p.split_stride + n;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long long m = mw + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < p.M) cp[m * p.ldc] = acc[t][r];
+      }
+    } else if (EPI == EPI_RELU_POOL4) {
+      const float bn = p.bias[n];
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        const long long m = mw + 8 * qd + 4 * lh;  // first of 4 pooled rows (multiple of 4)
+        if (m >= p.M) continue;
+        const long long w = m / p.s_in;
+        const int tp = (int)(m - w * p.s_in) >> 2;
+        if (tp >= p.t_valid) continue;
+        float mx = fmaxf(fmaxf(acc[t][4 * qd], acc[t][4 * qd + 1]), fmaxf(acc[t][4 * qd + 2], acc[t][4 * qd + 3]));
+        // maxpool(relu(x+b)) == relu(max(x)+b): x -> fl(x+b) and relu are monotone.
+        p.C[(w * p.s_out + tp) * p.ldc + n] = fmaxf(mx + bn, 0.f);
+      }
+    } else {
+      const float bn = p.bias[n];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long long m = mw + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m >= p.M) continue;
+        const long long w = m / p.s_in;
+        const int tpos = (int)(m - w * p.s_in);
+        if (tpos >= p.t_valid) continue;
+        const float v = acc[t][r] + bn;
+        float o;
+        if (EPI == EPI_SIGMOID)
+          o = 1.0f / (1.0f + expf(-v));
+        else
+          o = fmaxf(v, 0.f);
+        const long long orow = p.c_rows ? p.c_rows[m] : (w * p.s_out + tpos);
+        p.C[orow * p.ldc + n] = o;
+      }
+    }
+  }
+}
+
 // LAYER only makes the symbol distinct per layer (rocprof attributes time per layer).
 template <int LAYER, int EPI, int WM = 4, int MINB = 2, int BK = 32, int PIPE = 0>
 __global__ __launch_bounds__(64 * WM, MINB * WM / 4) void beluga_gemm(GemmArgs p) {
@@ -178,53 +230,161 @@ __global__ __launch_bounds__(64 * WM, MINB * WM / 4) void beluga_gemm(GemmArgs p
     }
   }
 
-  // Epilogue. C/D layout of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5),
-  // so rows 4g..4g+3 of a pool window sit in registers 4q..4q+3 of ONE lane.
-  const long long mw = m0 + wave * 32;
+  gemm_epilogue<EPI>(p, acc, m0 + wave * 32, n0, ks, li, lh);
+}
+
+// ---- fp32-faithful split-bf16 variant ("bf16x6") -------------------------------------
+// Every fp32 operand x is split exactly into three bf16 terms x = x0 + x1 + x2 (+ <2^-24|x|)
+// while it is staged into LDS; each 16-deep k-step issues the six v_mfma_f32_32x32x16_bf16
+// products of combined order <= 2 (x0y0, x0y1, x1y0, x0y2, x1y1, x2y0) into the same fp32
+// accumulator.  Products of bf16 terms are exact in fp32, so the result is fp32-accurate
+// (tools/split_precision_study.py: 0.06 of the parity bound on alt-ref diffs, vs 0.08 for
+// oneDNN fp32) at 6 x 1/16 = 3/8 the MFMA cycles of v_mfma_f32_32x32x2_f32.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split3(const floatx4 x, bf16x4& h, bf16x4& m, bf16x4& l) {
 #pragma unroll
-  for (int t = 0; t < GTN; ++t) {
-    const int n = n0 + t * 32 + li;
-    if (n >= p.n_store) continue;
-    if (EPI == EPI_PARTIAL) {
-      float* cp = p.C + (long long)ks * p.split_stride + n;
+  for (int j = 0; j < 4; ++j) {
+    const __bf16 a = (__bf16)x[j];
+    const float r = x[j] - (float)a;
+    const __bf16 b = (__bf16)r;
+    h[j] = a;
+    m[j] = b;
+    l[j] = (__bf16)(r - (float)b);
+  }
+}
+
+template <int LAYER, int EPI, int WM = 4, int MINB = 2>
+__global__ __launch_bounds__(64 * WM, MINB * WM / 4) void beluga_gemm_x6(GemmArgs p) {
+  constexpr int BM = 32 * WM;
+  constexpr int NT = 64 * WM;
+  constexpr int BK = GBK;                        // one 32-wide K block per stage
+  constexpr int F4 = BK / 4;
+  constexpr int RSTEP = NT / F4;
+  constexpr int ALD = BM / RSTEP;
+  constexpr int BLD = (GBN + RSTEP - 1) / RSTEP;
+  constexpr int RS = 40;                         // LDS row stride in bf16 (80 B): b128 reads conflict-free
+  constexpr int APL = BM * RS, BPL = GBN * RS;    // plane sizes (bf16 elements)
+  __shared__ __attribute__((aligned(16))) __bf16 smem[3 * APL + 3 * BPL];
+  __bf16* As = smem;
+  __bf16* Bs = smem + 3 * APL;
+
+  const unsigned nblk = gridDim.x, bid = blockIdx.x;
+  const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
+  const unsigned lin = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  long long mt;
+  int nt, ks;
+  if (p.m_fastest) {
+    mt = lin % p.m_tiles;
+    const long long rest = lin / p.m_tiles;
+    nt = (int)(rest % p.n_tiles);
+    ks = (int)(rest / p.n_tiles);
+  } else {
+    nt = (int)(lin % (unsigned)p.n_tiles);
+    const long long rest = lin / (unsigned)p.n_tiles;
+    mt = rest % p.m_tiles;
+    ks = (int)(rest / p.m_tiles);
+  }
+
+  const int tid = threadIdx.x;
+  const int lr = tid / F4, lc = (tid % F4) * 4;
+  const long long m0 = mt * BM;
+  const int n0 = nt * GBN;
+  const int gs0 = ks * (p.kper / GBK);
+  const float* ag[ALD];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const long long m = mw + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (m < p.M) cp[m * p.ldc] = acc[t][r];
-      }
-    } else if (EPI == EPI_RELU_POOL4) {
-      const float bn = p.bias[n];
+  for (int i = 0; i < ALD; ++i) {
+    long long m = m0 + lr + RSTEP * i;
+    if (m > p.M - 1) m = p.M - 1;
+    ag[i] = p.A + (p.a_rows ? p.a_rows[m] : m * p.lda) + lc;
+  }
+  const float* bg[BLD];
 #pragma unroll
-      for (int qd = 0; qd < 4; ++qd) {
-        const long long m = mw + 8 * qd + 4 * lh;  // first of 4 pooled rows (multiple of 4)
-        if (m >= p.M) continue;
-        const long long w = m / p.s_in;
-        const int tp = (int)(m - w * p.s_in) >> 2;
-        if (tp >= p.t_valid) continue;
-        float mx = fmaxf(fmaxf(acc[t][4 * qd], acc[t][4 * qd + 1]), fmaxf(acc[t][4 * qd + 2], acc[t][4 * qd + 3]));
-        // maxpool(relu(x+b)) == relu(max(x)+b): x -> fl(x+b) and relu are monotone.
-        p.C[(w * p.s_out + tp) * p.ldc + n] = fmaxf(mx + bn, 0.f);
-      }
-    } else {
-      const float bn = p.bias[n];
+  for (int i = 0; i < BLD; ++i) {
+    const int r = min(lr + RSTEP * i, GBN - 1);
+    bg[i] = p.B + (long long)(n0 + r) * p.ldb + (long long)gs0 * GBK + lc;
+  }
+  auto a_off = [&](int gs) -> long long {
+    const int chunk = gs / p.taps, tap = gs - chunk * p.taps;
+    return (long long)tap * p.lda + chunk * GBK;
+  };
+  floatx4 ra[ALD], rb[BLD];
+  auto gload = [&](int s) {
+    const long long ao = a_off(gs0 + s);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const long long m = mw + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (m >= p.M) continue;
-        const long long w = m / p.s_in;
-        const int tpos = (int)(m - w * p.s_in);
-        if (tpos >= p.t_valid) continue;
-        const float v = acc[t][r] + bn;
-        float o;
-        if (EPI == EPI_SIGMOID)
-          o = 1.0f / (1.0f + expf(-v));
-        else
-          o = fmaxf(v, 0.f);
-        const long long orow = p.c_rows ? p.c_rows[m] : (w * p.s_out + tpos);
-        p.C[orow * p.ldc + n] = o;
+    for (int i = 0; i < ALD; ++i) ra[i] = *(const floatx4*)(ag[i] + ao);
+#pragma unroll
+    for (int i = 0; i < BLD; ++i) rb[i] = *(const floatx4*)(bg[i] + s * BK);
+  };
+  auto sstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < ALD; ++i) {
+      bf16x4 h, m, l;
+      split3(ra[i], h, m, l);
+      __bf16* d = As + (lr + RSTEP * i) * RS + lc;
+      *(bf16x4*)(d) = h;
+      *(bf16x4*)(d + APL) = m;
+      *(bf16x4*)(d + 2 * APL) = l;
+    }
+#pragma unroll
+    for (int i = 0; i < BLD; ++i) {
+      if ((GBN % RSTEP == 0) || (lr + RSTEP * i < GBN)) {
+        bf16x4 h, m, l;
+        split3(rb[i], h, m, l);
+        __bf16* d = Bs + (lr + RSTEP * i) * RS + lc;
+        *(bf16x4*)(d) = h;
+        *(bf16x4*)(d + BPL) = m;
+        *(bf16x4*)(d + 2 * BPL) = l;
       }
     }
+  };
+
+  const int wave = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
+  floatx16 acc[GTN];
+#pragma unroll
+  for (int t = 0; t < GTN; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  // 16-deep k-step kq: lane half h reads columns 16kq + 8h .. +7 of its row (A and B alike)
+  const __bf16* aw = As + (wave * 32 + li) * RS + 8 * lh;
+  const __bf16* bw = Bs + li * RS + 8 * lh;
+  const int nk = p.kper / BK;
+
+  gload(0);
+  sstore();
+  __syncthreads();
+  for (int s = 0; s < nk; ++s) {
+    const bool more = (s + 1) < nk;
+    if (more) gload(s + 1);
+#pragma unroll
+    for (int kq = 0; kq < 2; ++kq) {
+      const bf16x8 a0 = *(const bf16x8*)(aw + 16 * kq);
+      const bf16x8 a1 = *(const bf16x8*)(aw + APL + 16 * kq);
+      const bf16x8 a2 = *(const bf16x8*)(aw + 2 * APL + 16 * kq);
+#pragma unroll
+      for (int t = 0; t < GTN; ++t) {
+        const __bf16* bt = bw + t * 32 * RS + 16 * kq;
+        const bf16x8 b0 = *(const bf16x8*)(bt);
+        const bf16x8 b1 = *(const bf16x8*)(bt + BPL);
+        const bf16x8 b2 = *(const bf16x8*)(bt + 2 * BPL);
+        floatx16 c = acc[t];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, c, 0, 0, 0);
+        acc[t] = c;
+      }
+    }
+    __syncthreads();
+    if (more) {
+      sstore();
+      __syncthreads();
+    }
   }
+  gemm_epilogue<EPI>(p, acc, m0 + wave * 32, n0, ks, li, lh);
 }
 
 }  // namespace expecto

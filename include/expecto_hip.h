@@ -54,6 +54,16 @@ enum {
                                (encodeSeqs row order, chromatin.py:170-171)             */
 };
 
+/* GEMM arithmetic (expecto_beluga_set_precision).  Both are fp32-accurate:
+ *  FP32   exact fp32 products and accumulation (v_mfma_f32_32x32x2_f32);
+ *  BF16X6 every fp32 operand split exactly into three bf16 terms, the six products of
+ *         combined order <= 2 accumulated in fp32 (v_mfma_f32_32x32x16_bf16); representation
+ *         error < 2^-24 relative, products exact -- default, ~1.4x faster. */
+enum {
+  EXPECTO_PRECISION_FP32 = 0,
+  EXPECTO_PRECISION_BF16X6 = 1,
+};
+
 /* Number of parameter tensors and their order (the reference state-dict keys,
  * SURVEY.md 2.2): model.0.{0,2,6,8,12,14}.{weight,bias}, model.1.2.1.{weight,bias},
  * model.1.4.1.{weight,bias}. */
@@ -101,6 +111,9 @@ int expecto_beluga_forward_segments(expecto_beluga_t h, const uint8_t* codes, in
 int expecto_gather_segments(const uint8_t* genome, long long genome_len, const long long* start, int n,
                             int seg_len, const int* splice_pos, const uint8_t* splice_code, uint8_t* codes,
                             void* stream);
+
+int expecto_beluga_set_precision(expecto_beluga_t h, int precision);
+int expecto_beluga_get_precision(expecto_beluga_t h);
 
 /* Per-layer device time accumulated over forward calls while profiling is on (ms).
  * Layers: 0 conv1, 1 conv2, 2 conv3, 3 conv4, 4 conv5, 5 conv6, 6 fc1, 7 fc1-reduce, 8 fc2.

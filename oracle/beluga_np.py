@@ -83,7 +83,7 @@ def forward_torch_cpu(sd: dict, x, threads: int | None = None):
 
     if threads is not None:
         torch.set_num_threads(threads)
-    x = torch.as_tensor(x, dtype=torch.float32)
+    x = torch.as_tensor(x, dtype=sd[CONV_KEYS[0] + ".weight"].dtype)
     if x.dim() == 3:
         x = x.unsqueeze(2)
     with torch.no_grad():

@@ -10,11 +10,12 @@ from conftest import GOLDEN, assert_close
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def model():
+@pytest.fixture(scope="module", params=["bf16x6", "fp32"])
+def model(request):
     import torch
     from expecto_amd import beluga
     m = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=96).cuda()
+    m.engine().set_precision(request.param)
     yield m
     torch.cuda.synchronize()
 
@@ -76,6 +77,23 @@ def test_forward_dense_float_input_vs_cpu_oracle(model, cpu_sd):
     got = model.forward(torch.from_numpy(x).cuda()).cpu().numpy()
     want = forward_torch_cpu(cpu_sd, torch.from_numpy(x)).numpy()
     assert_close(got, want, what="dense input")
+
+
+def test_accuracy_vs_float64(model, cpu_sd):
+    """Both GEMM precisions are fp32-accurate: error vs a float64 forward within 3x the
+    reference's own fp32 (oneDNN) error, on 9 random windows."""
+    import torch
+    from oracle.beluga_np import forward_torch_cpu
+    from expecto_amd.encode import codes_to_onehot
+    rng = np.random.default_rng(42)
+    x = codes_to_onehot(rng.integers(0, 5, (9, 2000)).astype(np.uint8), with_rc=False).astype(np.float32)
+    xt = torch.from_numpy(x).unsqueeze(2)
+    y64 = forward_torch_cpu({k: v.double() for k, v in cpu_sd.items()}, xt.double()).numpy()
+    y32 = forward_torch_cpu(cpu_sd, xt).numpy()
+    got = model.forward(xt.cuda()).cpu().numpy()
+    e_ref = np.abs(y32 - y64).max()
+    e_got = np.abs(got - y64).max()
+    assert e_got <= 3 * e_ref + 1e-6, (e_got, e_ref)
 
 
 def test_empty_batch_and_errors(model):

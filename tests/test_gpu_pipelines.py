@@ -94,13 +94,16 @@ def test_variant_feature_reduction_matches_predict_py():
         assert_close(out[name], feats[name], rtol=1e-9, atol=1e-12, what=f"variant features {name}")
 
 
-def _engine():
+def _engine(precision="bf16x6"):
     import math
     from expecto_amd import beluga
-    return beluga.seeded(0, gain=math.sqrt(6.0), max_batch=300).cuda().engine()
+    eng = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=300).cuda().engine()
+    eng.set_precision(precision)
+    return eng
 
 
-def test_segment_path_is_bitwise_equal_to_per_window_variants():
+@pytest.mark.parametrize("precision", ["bf16x6", "fp32"])
+def test_segment_path_is_bitwise_equal_to_per_window_variants(precision):
     """Trunk sharing across shifts (segment path) reproduces the per-window forward exactly."""
     import torch
     from expecto_amd import synthetic
@@ -110,7 +113,7 @@ def test_segment_path_is_bitwise_equal_to_per_window_variants():
     fa = Fasta.from_dict(g)
     snv = synthetic.snvs(g, 23, seed=4)
     vs = VariantSet([s[0] for s in snv], np.array([s[1] for s in snv]), [s[2] for s in snv], [s[3] for s in snv])
-    eng = _engine()
+    eng = _engine(precision)
     dg = DeviceGenome(fa)
     for shifts in (shift_order(800), shift_order(200), [0, 400, -400]):
         seg = VariantPipeline(eng, fa, dg, use_segments=True)

@@ -17,7 +17,16 @@ def split(t):
     lo = (t - hi).to(torch.bfloat16).float()
     return hi, lo
 
+def split3(t):
+    a = t.to(torch.bfloat16).float()
+    b = (t - a).to(torch.bfloat16).float()
+    c = (t - a - b).to(torch.bfloat16).float()
+    return a, b, c
+
 def op3(f, x, w, terms):
+    if terms == 6:   # 3-way split, products of combined order <= 2 (x0y0 x0y1 x1y0 x0y2 x1y1 x2y0)
+        x0, x1, x2 = split3(x); w0, w1, w2 = split3(w)
+        return f(x0, w0) + (f(x0, w1) + f(x1, w0)) + (f(x0, w2) + f(x1, w1) + f(x2, w0))
     xh, xl = split(x); wh, wl = split(w)
     out = f(xh, wh)
     if terms >= 3:
@@ -59,7 +68,7 @@ x = torch.from_numpy(codes_to_onehot(codes, with_rc=False).astype(np.float32)).u
 with torch.no_grad():
     y64 = None
     base = forward({k: v.double() for k, v in sd.items()}, x.double(), "fp32")
-    for mode in ("fp32", 3, 4):
+    for mode in ("fp32", 3, 6):
         y = forward(sd, x, mode).double()
         n = len(refs)
         d_ref = base[n:] - base[:n]
