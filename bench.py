@@ -79,6 +79,65 @@ def cpu_baseline(sd_cpu, codes: np.ndarray, seconds: float, threads: int, window
                       f"oracle/beluga_np.forward_torch_cpu (torch CPU fp32, oneDNN), {el:.1f} s"}
 
 
+def make_variants(genome, n, seed):
+    snvs = synthetic.snvs(genome, n, seed=seed)
+    return VariantSet([v[0] for v in snvs], np.array([v[1] for v in snvs]), [v[2] for v in snvs],
+                      [v[3] for v in snvs])
+
+
+def time_workload(pipe, eng, prep, shifts, n, steps, warmup, dev, world):
+    """Time `steps` steps (window generation + forward + diff) with HIP-event layer timing."""
+    S = len(shifts)
+    y = torch.empty((2, 2, S, n, 2002), dtype=torch.float32, device=dev)
+
+    def step():
+        pipe.predict(prep, out=y)
+        return pipe.diff(y)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    eng.set_profiling(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    el = time.perf_counter() - t0
+    layers = eng.layer_times()
+    eng.set_profiling(False)
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = float(t.item())
+    return el, layers
+
+
+def roofline(layers, precision):
+    """MFMA roofline of the dominant GEMM kernel from executed work per launch (library counts)
+    and its average launch duration (HIP events on the launch stream)."""
+    dom = max((k for k in GEMM_LAYER_EPI), key=lambda k: layers[k][0])
+    ms, calls, macs = layers[dom]
+    fp32_flops_launch = 2.0 * macs / calls
+    fp32_tflops = fp32_flops_launch / (ms / calls / 1e3) / 1e12
+    if precision == "bf16x6":
+        mult, peak = BF16X6_PRODUCTS, BF16_MFMA_PEAK_TFLOPS
+    else:
+        mult, peak = 1, FP32_MFMA_PEAK_TFLOPS
+    achieved = mult * fp32_tflops
+    return {"bound": "mfma", "kernel": kernel_name(dom, precision), "layer": dom, "achieved": achieved,
+            "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
+            "avg_launch_ms": ms / calls, "launches": calls, "mfma_flops_per_launch": mult * fp32_flops_launch,
+            "fp32_flops_per_launch": fp32_flops_launch, "fp32_tflops": fp32_tflops, "precision": precision}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -89,6 +148,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the cfg3 / 200-window extra workloads")
     args = ap.parse_args()
 
     rank, world, local = edist.init("nccl")
@@ -101,59 +161,18 @@ def main():
 
     genome = synthetic.genome_bytes(n_contigs=24, contig_len=2_000_000, seed=0)
     fasta = Fasta.from_dict(genome)
-    snvs = synthetic.snvs(genome, n, seed=1 + rank)
-    vs = VariantSet([s[0] for s in snvs], np.array([s[1] for s in snvs]), [s[2] for s in snvs],
-                    [s[3] for s in snvs])
-    model = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=rows)
+    vs = make_variants(genome, n, 1 + rank)
+    model = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=min(rows, 8192))
     sd_cpu = {k: v.detach().clone() for k, v in model.state_dict().items()} if (rank == 0 and world == 1) else None
     model = model.cuda()
     eng = model.engine()
     pipe = VariantPipeline(eng, fasta, DeviceGenome(fasta, device=dev))
     prep = pipe.prepare(vs, shifts)                          # variant table resident in HBM
-    y = torch.empty((2, 2, S, n, 2002), dtype=torch.float32, device=dev)
 
-
-    def step():
-        pipe.predict(prep, out=y)
-        return pipe.diff(y)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    eng.set_profiling(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    el = time.perf_counter() - t0
-    layers = eng.layer_times()
-    eng.set_profiling(False)
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        el = float(t.item())
-
+    el, layers = time_workload(pipe, eng, prep, shifts, n, args.steps, args.warmup, dev, world)
     total_rows = rows * args.steps
     value = world * n * args.steps / el
-    fwd_ms = sum(ms for ms, _ in layers.values())
-    dom = max((k for k in layers if LAYER_MACS[k]), key=lambda k: layers[k][0])
-    dom_ms, dom_calls = layers[dom]
-    dom_flops_launch = 2.0 * LAYER_MACS[dom] * total_rows / dom_calls
-    algo_tflops = dom_flops_launch / (dom_ms / dom_calls / 1e3) / 1e12
-    if eng.precision == "bf16x6":
-        # roofline of the bf16 MFMA pipe: executed bf16 FLOPs = 6 x the fp32 algorithmic FLOPs
-        achieved, peak, flops_launch = BF16X6_PRODUCTS * algo_tflops, BF16_MFMA_PEAK_TFLOPS, \
-            BF16X6_PRODUCTS * dom_flops_launch
-    else:
-        achieved, peak, flops_launch = algo_tflops, FP32_MFMA_PEAK_TFLOPS, dom_flops_launch
+    exec_macs = sum(m for _, _, m in layers.values())
     rec = {
         "metric": METRIC, "value": value, "unit": "variants/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
@@ -165,17 +184,34 @@ def main():
                                f"{rows} Beluga windows/step/GPU (window gen + forward + diff)",
                    "variants_per_gpu": n, "windows_per_variant": 4 * S, "parallelism": f"dp{world} (variant shards)"},
         "windows_per_s": world * total_rows / el,
-        "variants_200shift_per_s": world * total_rows / el / 800.0,
-        "forward_tflops": 2.0 * WINDOW_MACS * world * total_rows / el / 1e12,
-        "roofline": {"bound": "mfma", "kernel": kernel_name(dom, eng.precision), "layer": dom, "achieved": achieved,
-                     "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
-                     "traffic": None, "avg_launch_ms": dom_ms / dom_calls,
-                     "mfma_flops_per_launch": flops_launch,
-                     "algorithmic_fp32_flops_per_launch": dom_flops_launch,
-                     "algorithmic_fp32_tflops": algo_tflops, "precision": eng.precision},
-        "layer_ms_per_step": {k: ms / args.steps for k, (ms, c) in layers.items()},
-        "device_forward_ms_per_step": fwd_ms / args.steps,
+        "dense_equivalent_tflops": 2.0 * WINDOW_MACS * world * total_rows / el / 1e12,
+        "executed_fp32_tflops": 2.0 * exec_macs * world / el / 1e12,
+        "roofline": roofline(layers, eng.precision),
+        "layer_ms_per_step": {k: ms / args.steps for k, (ms, c, m) in layers.items()},
+        "reuse": "alt-cone (SNV alt windows recompute <=20 of 106 conv6 rows; bit-identical)" if S == 1 else
+                 "segments (trunk shared across shifts; bit-identical)",
     }
+    if world == 1 and not args.no_extras:
+        extras = {}
+        # configs[2]: the +-800 shift sweep (9 shifts) -- segment path (trunk shared across shifts)
+        sh9 = shift_order(800)
+        v3 = make_variants(genome, 400, 101)
+        p3 = pipe.prepare(v3, sh9)
+        el3, l3 = time_workload(pipe, eng, p3, sh9, 400, 2, 1, dev, 1)
+        extras["cfg3_shift_sweep_800"] = {
+            "variants_per_s": 400 * 2 / el3, "windows_per_variant": 36, "dense_windows_per_s": 400 * 36 * 2 / el3,
+            "executed_fp32_tflops": 2.0 * sum(m for _, _, m in l3.values()) / el3 / 1e12,
+            "roofline": roofline(l3, eng.precision)}
+        # the metric's literal unit: a variant scored with 200 windows (+-20 kb, stride 200) x ref/alt x fwd/rc
+        sh200 = list(range(-20000, 20000, 200))
+        v200 = make_variants(genome, 24, 202)
+        p200 = pipe.prepare(v200, sh200)
+        el2, l2 = time_workload(pipe, eng, p200, sh200, 24, 2, 1, dev, 1)
+        extras["variant_200_windows"] = {
+            "variants_per_s": 24 * 2 / el2, "windows_per_variant": 800, "dense_windows_per_s": 24 * 800 * 2 / el2,
+            "executed_fp32_tflops": 2.0 * sum(m for _, _, m in l2.values()) / el2 / 1e12,
+            "roofline": roofline(l2, eng.precision)}
+        rec["extra_workloads"] = extras
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from expecto_amd.encode import seqs_to_codes
         g1 = genome["chr1"]

@@ -36,10 +36,12 @@ SIGNATURES = {
                                                        ctypes.c_int, c_vp, c_vp, c_vp, ctypes.c_int, c_vp, c_vp]),
     "expecto_gather_segments": (ctypes.c_int, [c_vp, ctypes.c_longlong, c_vp, ctypes.c_int, ctypes.c_int, c_vp,
                                                c_vp, c_vp, c_vp]),
+    "expecto_beluga_forward_pairs": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_longlong, c_vp,
+                                                    ctypes.c_int, c_vp, c_vp, ctypes.c_longlong, c_vp]),
     "expecto_beluga_set_precision": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "expecto_beluga_get_precision": (ctypes.c_int, [c_vp]),
     "expecto_beluga_set_profiling": (ctypes.c_int, [c_vp, ctypes.c_int]),
-    "expecto_beluga_layer_times": (ctypes.c_int, [c_vp, c_f64p, c_i64p, ctypes.c_int]),
+    "expecto_beluga_layer_times": (ctypes.c_int, [c_vp, c_f64p, c_i64p, c_f64p, ctypes.c_int]),
     "expecto_variant_windows": (ctypes.c_int, [c_vp, ctypes.c_longlong, c_vp, c_vp, c_vp, ctypes.c_int, c_vp,
                                                ctypes.c_int, c_vp, c_vp]),
     "expecto_tss_windows": (ctypes.c_int, [c_vp, ctypes.c_longlong, c_vp, c_vp, ctypes.c_int, c_vp, ctypes.c_int,

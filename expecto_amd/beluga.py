@@ -136,16 +136,44 @@ class BelugaEngine:
             _lib.stream_ptr(stream)), "forward_segments")
         return out
 
+    def forward_pairs(self, ref_codes: torch.Tensor, alt_codes: torch.Tensor, var_pos, y_ref: torch.Tensor,
+                      y_alt: torch.Tensor, strand_stride: int, strand_mode: int = _lib.STRAND_BOTH, stream=None):
+        """SNV ref/alt window pairs with alt-cone reuse (bit-identical to two full forwards).
+
+        ref_codes/alt_codes: uint8 [n, >=2000] device, differing at most at var_pos[v] (int32
+        device tensor, or host ints which are copied to the device here).  Row (strand s, variant v) of the outputs is s*strand_stride + v; y_ref/y_alt are
+        device views whose first element is row 0 (they may alias one larger tensor)."""
+        import numpy as np
+
+        for c in (ref_codes, alt_codes):
+            if c.dtype != torch.uint8 or c.dim() != 2 or c.shape[1] < INPUT_LEN or c.stride(1) != 1:
+                raise RuntimeError("codes must be uint8 [n, >=2000] with contiguous rows")
+        if ref_codes.shape != alt_codes.shape or ref_codes.stride(0) != alt_codes.stride(0):
+            raise RuntimeError("ref and alt codes must have the same shape and stride")
+        n = ref_codes.shape[0]
+        if isinstance(var_pos, torch.Tensor) and var_pos.is_cuda:
+            pos = var_pos.to(torch.int32).contiguous()
+        else:
+            pos = torch.from_numpy(np.ascontiguousarray(var_pos, np.int32)).to(ref_codes.device)
+        if pos.numel() != n:
+            raise RuntimeError("one variant position per window pair")
+        _lib.check(self.lib.expecto_beluga_forward_pairs(
+            self.handle, _lib.dptr(ref_codes), _lib.dptr(alt_codes), n, ref_codes.stride(0), _lib.dptr(pos),
+            int(strand_mode), _lib.dptr(y_ref), _lib.dptr(y_alt), int(strand_stride), _lib.stream_ptr(stream)),
+            "forward_pairs")
+
     def set_profiling(self, on: bool):
         _lib.check(self.lib.expecto_beluga_set_profiling(self.handle, int(on)), "set_profiling")
 
     def layer_times(self):
+        """{layer: (device ms, launches, executed multiply-adds)} accumulated while profiling."""
         ms = (ctypes.c_double * _lib.N_LAYERS)()
         calls = (ctypes.c_longlong * _lib.N_LAYERS)()
-        n = self.lib.expecto_beluga_layer_times(self.handle, ms, calls, _lib.N_LAYERS)
+        macs = (ctypes.c_double * _lib.N_LAYERS)()
+        n = self.lib.expecto_beluga_layer_times(self.handle, ms, calls, macs, _lib.N_LAYERS)
         if n < 0:
             _lib.check(n, "layer_times")
-        return {_lib.LAYER_NAMES[i]: (ms[i], calls[i]) for i in range(_lib.N_LAYERS)}
+        return {_lib.LAYER_NAMES[i]: (ms[i], calls[i], macs[i]) for i in range(_lib.N_LAYERS)}
 
     def device_bytes(self) -> int:
         return int(self.lib.expecto_beluga_device_bytes(self.handle))

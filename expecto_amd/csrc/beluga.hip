@@ -155,6 +155,62 @@ __global__ void seg_a_rows(const int* __restrict__ win_seg, const int* __restric
   a_rows[m] = (blk * s7 + off6) * 640;
 }
 
+// ---- alt-cone reuse for SNV ref/alt window pairs ---------------------------------------
+// A conv6 row t of a window depends on input positions [16t, 16t+309] (receptive field 310).
+// An SNV at window index p therefore changes only rows t in [ceil((p-309)/16), floor(p/16)]
+// (at most 20 of 106).  The alt window is computed as: the ref window's conv6 rows, with the
+// 20 rows starting at r0 replaced by the conv6 rows of a 616-bp "patch" sequence cut from the
+// alt window at 16*r0 (16-aligned, so pool1/pool2 groups coincide with the window's).  Every
+// row is produced by the same kernels from the same operands -> bit-identical alt outputs.
+constexpr int kPatchLen = 616;   // 16*19 + 310 rounded up to 4 -> 20 conv6 rows
+constexpr int kPatchRows = 20;
+constexpr int kPatchMaxRow0 = 106 - kPatchRows;
+
+__device__ __forceinline__ int patch_row0(int p) {
+  const int t_lo = p >= 309 ? (p - 309 + 15) / 16 : 0;
+  return t_lo < kPatchMaxRow0 ? t_lo : kPatchMaxRow0;
+}
+
+// m = strand*nv + (v - v0); strand 1 = reverse complement of the alt window.
+__global__ void pair_patch_codes(const uint8_t* __restrict__ alt, long long stride, int nv, int v0,
+                                 const int* __restrict__ var_pos, uint8_t* __restrict__ out) {
+  const int m = blockIdx.y;
+  const int s = m / nv, v = v0 + m % nv;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= kPatchLen) return;
+  const int pv = min(max(var_pos[v], 0), kLen - 1);
+  const int p = s ? kLen - 1 - pv : pv;
+  const int start = 16 * patch_row0(p);
+  const uint8_t* a = alt + (long long)v * stride;
+  uint8_t c;
+  if (s) {
+    const uint8_t f = a[kLen - 1 - (start + i)];
+    c = f < 4 ? (uint8_t)(3 - f) : f;
+  } else {
+    c = a[start + i];
+  }
+  out[(long long)m * kPatchLen + i] = c;
+}
+
+// act6[m][r0 + r][:] = patch6[m][r][:] for r < 19 (640 channels, float4 lanes)
+__global__ void pair_patch_apply(const float* __restrict__ patch6, float* __restrict__ act6, int nv, int v0,
+                                 const int* __restrict__ var_pos) {
+  const int m = blockIdx.y;
+  const int r = blockIdx.x;
+  const int c4 = threadIdx.x;  // 160 lanes
+  const int s = m / nv, v = v0 + m % nv;
+  const int pv = min(max(var_pos[v], 0), kLen - 1);
+  const int p = s ? kLen - 1 - pv : pv;
+  const int r0 = patch_row0(p);
+  const floatx4 x = *(const floatx4*)(patch6 + ((long long)m * kPatchRows + r) * 640 + 4 * c4);
+  *(floatx4*)(act6 + ((long long)m * 106 + r0 + r) * 640 + 4 * c4) = x;
+}
+
+__global__ void pair_rows(long long* __restrict__ c_rows, int M, int nv, int v0, long long strand_stride) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m < M) c_rows[m] = (long long)(m / nv) * strand_stride + v0 + m % nv;
+}
+
 // ---- weight repacking (reference layouts -> kernel layouts) --------------------------
 __global__ void repack_conv(const float* __restrict__ W, int cout, int cin, int npad, float* __restrict__ Wt) {
   const long long K = 8LL * cin;
@@ -232,6 +288,9 @@ struct expecto_beluga {
   int* win_seg_d = nullptr;     // window tables of the current segment call
   int* win_off_d = nullptr;
   int* win_row_d = nullptr;
+  float* P2 = nullptr;           // patch trunk buffers (alt-cone path), lazily allocated
+  float* Q2 = nullptr;
+  uint8_t* patch_codes = nullptr;
   int win_cap = 0;
   size_t bytes = 0;
   std::vector<void*> allocs;
@@ -242,6 +301,7 @@ struct expecto_beluga {
   size_t ev_next = 0;
   double ms[kNumLayers] = {};
   long long calls[kNumLayers] = {};
+  double macs[kNumLayers] = {};  // executed multiply-adds per layer while profiling (host-side count)
 };
 
 namespace {
@@ -314,11 +374,12 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st) {
 }
 
 int run_conv1(expecto_beluga* h, const float* x, const uint8_t* codes, long long code_stride, int n_src, int mode,
-              long long row0, int nb, int len, int out_rows, hipStream_t st) {
+              long long row0, int nb, int len, int out_rows, hipStream_t st, float* dst = nullptr) {
   LayerTimer lt(h, 0, st);
+  if (h->profiling) h->macs[0] += (double)nb * (len - 7) * 320 * 32;
   dim3 grid((len - 7 + C1_T - 1) / C1_T, nb);
-  beluga_conv1<<<grid, dim3(320), 0, st>>>(x, codes, code_stride, n_src, mode, row0, h->w1, h->b1, h->P, out_rows,
-                                           len);
+  beluga_conv1<<<grid, dim3(320), 0, st>>>(x, codes, code_stride, n_src, mode, row0, h->w1, h->b1,
+                                           dst ? dst : h->P, out_rows, len);
   return check_launch("beluga_conv1");
 }
 
@@ -345,6 +406,7 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
   a.t_valid = t_valid;
   a.s_out = s_out;
   LayerTimer lt(h, l + 1, st);
+  if (h->profiling) h->macs[l + 1] += (double)a.M * g.cout * a.kper;
   if (pool) {
     EXPECTO_REQUIRE(s_in % 4 == 0, "pool epilogue needs 4-aligned row groups");
     return l == 0 ? launch_gemm<2, EPI_RELU_POOL4>(a, 1, st) : launch_gemm<4, EPI_RELU_POOL4>(a, 1, st);
@@ -387,6 +449,7 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     a.n_store = kHidLd;
     a.split_stride = (long long)nb * kHidLd;
     LayerTimer lt(h, 6, st);
+    if (h->profiling) h->macs[6] += (double)nb * kFc1Out * kFc1In;
     if ((rc = launch_gemm<7, EPI_PARTIAL>(a, splits, st))) return rc;
   }
   {
@@ -417,6 +480,7 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     a.t_valid = 1;
     a.s_out = 1;
     LayerTimer lt(h, 8, st);
+    if (h->profiling) h->macs[8] += (double)nb * kNFeat * kFc1Out;
     if ((rc = launch_gemm<8, EPI_SIGMOID>(a, 1, st))) return rc;
   }
   return EXPECTO_OK;
@@ -515,6 +579,8 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
   }
   EXPECTO_HIP_CHECK(hipMemcpyAsync(h->win_seg_d, win_seg, n_win * sizeof(int), hipMemcpyHostToDevice, st));
   EXPECTO_HIP_CHECK(hipMemcpyAsync(h->win_off_d, win_off, n_win * sizeof(int), hipMemcpyHostToDevice, st));
+  // the tables are caller-owned pageable host memory: finish the copies before returning
+  EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
   const int strands = mode == EXPECTO_STRAND_BOTH ? 2 : 1;
   int rc;
   for (int sd = 0; sd < strands; ++sd) {
@@ -554,6 +620,69 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
       }
       s0 = s1;
     }
+  }
+  return EXPECTO_OK;
+}
+// Trunk (conv1..conv6) of nseg segments of length L with pool2 phase 0 only (segment
+// starts 16-aligned relative to the windows they stand in for); conv6 rows end in `pbuf`.
+int run_trunk_phase0(expecto_beluga* h, const uint8_t* codes, long long stride, int nseg, int L, float* pbuf,
+                     float* qbuf, SegGeo& g, hipStream_t st) {
+  int rc;
+  g = seg_geo(L, 1);
+  if ((rc = run_conv1(h, nullptr, codes, stride, nseg, EXPECTO_STRAND_FWD, 0, nseg, L, g.S1, st, pbuf))) return rc;
+  if ((rc = run_conv(h, 0, pbuf, qbuf, nseg, g.S1, g.P1, g.P1, true, st))) return rc;
+  if ((rc = run_conv(h, 1, qbuf, pbuf, nseg, g.P1, g.T3, g.T3, false, st))) return rc;
+  if ((rc = run_conv(h, 2, pbuf, qbuf, nseg, g.T3, g.T4, g.T4, false, st))) return rc;
+  {
+    LayerTimer lt(h, 3, st);
+    pool4_phases<<<dim3(g.S5, nseg), dim3(480 / 4), 0, st>>>(qbuf, nseg, g.T4, g.T4, 480, 1, make_int4(0, 0, 0, 0),
+                                                             g.S5, pbuf);
+    if ((rc = check_launch("pool4_phases"))) return rc;
+  }
+  if ((rc = run_conv(h, 3, pbuf, qbuf, nseg, g.S5, g.T5, g.T5, false, st))) return rc;
+  return run_conv(h, 4, qbuf, pbuf, nseg, g.T5, g.T6, g.T6, false, st);
+}
+
+int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int n, long long stride,
+                  const int* var_pos, int mode, float* y_ref, float* y_alt, long long strand_stride, hipStream_t st) {
+  g_precision = h->precision;
+  const int strands = mode == EXPECTO_STRAND_BOTH ? 2 : 1;
+  if (!h->P2) {
+    const SegGeo g = seg_geo(kPatchLen, 1);
+    size_t pf = (size_t)h->max_batch * g.p_rows_floats + 16 * 640, qf = (size_t)h->max_batch * g.q_rows_floats + 16 * 640;
+    int rc;
+    if ((rc = dalloc(h, &h->P2, pf)) || (rc = dalloc(h, &h->Q2, qf))) return rc;
+    float* pc = nullptr;
+    if ((rc = dalloc(h, &pc, ((size_t)h->max_batch * kPatchLen + 3) / 4))) return rc;
+    h->patch_codes = reinterpret_cast<uint8_t*>(pc);
+  }
+  const int nv_max = std::max(1, h->max_batch / strands);
+  int rc;
+  for (int v0 = 0; v0 < n; v0 += nv_max) {
+    const int nv = std::min(nv_max, n - v0), R = strands * nv;
+    // ref windows: full per-window trunk, conv6 rows stay in Q
+    if ((rc = run_conv1(h, nullptr, ref + (long long)v0 * stride, stride, nv, mode, 0, R, kLen, kS1, st))) return rc;
+    float* src = h->P;
+    float* dst = h->Q;
+    for (int l = 0; l < 5; ++l) {
+      const ConvGeo& g = kConv[l];
+      if ((rc = run_conv(h, l, src, dst, R, g.s_in, g.t_valid, g.s_out, g.pool != 0, st))) return rc;
+      std::swap(src, dst);
+    }
+    float* act6 = src;
+    pair_rows<<<dim3((R + 255) / 256), dim3(256), 0, st>>>(h->c_rows, R, nv, v0, strand_stride);
+    if ((rc = check_launch("pair_rows"))) return rc;
+    if ((rc = run_fc(h, act6, nullptr, R, y_ref, st, h->c_rows))) return rc;
+    // alt windows: 600-bp patch trunk, patch rows spliced into the ref conv6 rows
+    pair_patch_codes<<<dim3((kPatchLen + 255) / 256, R), dim3(256), 0, st>>>(alt + 0, stride, nv, v0, var_pos,
+                                                                            h->patch_codes);
+    if ((rc = check_launch("pair_patch_codes"))) return rc;
+    SegGeo pg;
+    if ((rc = run_trunk_phase0(h, h->patch_codes, kPatchLen, R, kPatchLen, h->P2, h->Q2, pg, st))) return rc;
+    EXPECTO_REQUIRE(pg.T6 == kPatchRows, "patch geometry");
+    pair_patch_apply<<<dim3(kPatchRows, R), dim3(160), 0, st>>>(h->P2, act6, nv, v0, var_pos);
+    if ((rc = check_launch("pair_patch_apply"))) return rc;
+    if ((rc = run_fc(h, act6, nullptr, R, y_alt, st, h->c_rows))) return rc;
   }
   return EXPECTO_OK;
 }
@@ -680,6 +809,20 @@ int expecto_beluga_forward_segments(expecto_beluga_t h, const uint8_t* codes, in
                           as_stream(stream));
 }
 
+int expecto_beluga_forward_pairs(expecto_beluga_t h, const uint8_t* ref_codes, const uint8_t* alt_codes, int n,
+                                 long long code_stride, const int* var_pos, int strand_mode, float* y_ref,
+                                 float* y_alt, long long strand_stride, void* stream) {
+  EXPECTO_REQUIRE(h != nullptr, "null handle");
+  EXPECTO_REQUIRE(n >= 0, "negative count");
+  EXPECTO_REQUIRE(strand_mode == EXPECTO_STRAND_FWD || strand_mode == EXPECTO_STRAND_BOTH, "strand mode FWD or BOTH");
+  if (n == 0) return EXPECTO_OK;
+  EXPECTO_REQUIRE(ref_codes && alt_codes && var_pos && y_ref && y_alt, "null argument");
+  EXPECTO_REQUIRE(code_stride >= kLen, "code_stride < 2000");
+  EXPECTO_HIP_CHECK(hipSetDevice(h->device));
+  return forward_pairs(h, ref_codes, alt_codes, n, code_stride, var_pos, strand_mode, y_ref, y_alt, strand_stride,
+                       as_stream(stream));
+}
+
 int expecto_beluga_set_precision(expecto_beluga_t h, int precision) {
   EXPECTO_REQUIRE(h != nullptr, "null handle");
   EXPECTO_REQUIRE(precision == EXPECTO_PRECISION_FP32 || precision == EXPECTO_PRECISION_BF16X6, "bad precision");
@@ -703,11 +846,12 @@ int expecto_beluga_set_profiling(expecto_beluga_t h, int on) {
   if (on) {
     std::fill(h->ms, h->ms + kNumLayers, 0.0);
     std::fill(h->calls, h->calls + kNumLayers, 0LL);
+    std::fill(h->macs, h->macs + kNumLayers, 0.0);
   }
   return EXPECTO_OK;
 }
 
-int expecto_beluga_layer_times(expecto_beluga_t h, double* ms, long long* calls, int max_layers) {
+int expecto_beluga_layer_times(expecto_beluga_t h, double* ms, long long* calls, double* macs, int max_layers) {
   EXPECTO_REQUIRE(h != nullptr, "null handle");
   int rc = resolve_events(h);
   if (rc) return rc;
@@ -715,6 +859,7 @@ int expecto_beluga_layer_times(expecto_beluga_t h, double* ms, long long* calls,
   for (int i = 0; i < n; ++i) {
     if (ms) ms[i] = h->ms[i];
     if (calls) calls[i] = h->calls[i];
+    if (macs) macs[i] = h->macs[i];
   }
   return kNumLayers;
 }

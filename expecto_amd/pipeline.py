@@ -94,7 +94,8 @@ class VariantPipeline:
     Indels/MNPs, whose windows are length-changing splices, use the per-window path with
     host-built codes; shift lists that are not 4-aligned use per-window device windows."""
 
-    def __init__(self, engine, fasta, dgenome, inputsize: int = 2000, use_segments: bool = True):
+    def __init__(self, engine, fasta, dgenome, inputsize: int = 2000, use_segments: bool = True,
+                 use_pairs: bool = True):
         if inputsize != 2000:
             raise ValueError("Beluga's FC1 fixes the input size at 2000 (Beluga.py:43)")
         self.engine = engine
@@ -103,6 +104,7 @@ class VariantPipeline:
         self.device = dgenome.codes.device
         self.lib = _lib.load()
         self.use_segments = use_segments
+        self.use_pairs = use_pairs
 
     def prepare(self, vs: VariantSet, shifts) -> dict:
         """Host checks + the device-resident variant tables (done once, outside the hot loop)."""
@@ -194,6 +196,16 @@ class VariantPipeline:
                                          seg["splice_code"])
                 self.engine.forward_segments(scodes, seg["L"], seg["win_seg"], seg["win_off"], seg["win_row"],
                                              _lib.STRAND_BOTH, out=y.view(4 * S * ns, 2002))
+            elif self.use_pairs:
+                # alt-cone reuse per shift: the alt window recomputes only the SNV's cone
+                codes = self._snv_window_codes(prep)
+                yf = y.view(2 * 2 * S * ns, 2002)
+                if "pair_pos" not in prep:
+                    prep["pair_pos"] = [torch.full((ns,), 999 - sh, dtype=torch.int32, device=self.device)
+                                        for sh in prep["shifts"]]
+                for j in range(S):
+                    self.engine.forward_pairs(codes[0, j], codes[1, j], prep["pair_pos"][j], yf[j * ns:],
+                                              yf[(S + j) * ns:], 2 * S * ns, _lib.STRAND_BOTH)
             else:
                 codes = self._snv_window_codes(prep)
                 self.engine.forward_codes(codes.view(2 * S * ns, 2000), _lib.STRAND_BOTH,

@@ -112,14 +112,28 @@ int expecto_gather_segments(const uint8_t* genome, long long genome_len, const l
                             int seg_len, const int* splice_pos, const uint8_t* splice_code, uint8_t* codes,
                             void* stream);
 
+/* SNV ref/alt window pairs with alt-cone reuse: ref_codes/alt_codes are n windows each
+ * (2000 codes at + v*code_stride) that differ at most at window index var_pos[v] (DEVICE array).
+ * The ref windows run the full forward; each alt window reuses the ref conv6 rows outside the
+ * SNV's receptive-field cone (<= 20 of 106 rows, recomputed from a 616-bp patch), so the alt
+ * trunk costs ~30 % of a window -- outputs are bit-identical to the full alt forward.
+ * strand_mode FWD (rows: fwd) or BOTH (fwd and reverse complement).  Output row of (strand s,
+ * variant v) is s*strand_stride + v in y_ref and in y_alt (chromatin.py:262-281 row order
+ * when strand_stride = n). */
+int expecto_beluga_forward_pairs(expecto_beluga_t h, const uint8_t* ref_codes, const uint8_t* alt_codes, int n,
+                                 long long code_stride, const int* var_pos, int strand_mode, float* y_ref,
+                                 float* y_alt, long long strand_stride, void* stream);
+
 int expecto_beluga_set_precision(expecto_beluga_t h, int precision);
 int expecto_beluga_get_precision(expecto_beluga_t h);
 
-/* Per-layer device time accumulated over forward calls while profiling is on (ms).
- * Layers: 0 conv1, 1 conv2, 2 conv3, 3 conv4, 4 conv5, 5 conv6, 6 fc1, 7 fc1-reduce, 8 fc2.
- * `calls` receives the number of launches per layer.  Returns the number of layers. */
+/* Per-layer device time accumulated over forward calls while profiling is on (ms), launches
+ * (`calls`) and executed multiply-adds (`macs`: GEMM M x N x K actually run, including the
+ * few padding rows; reuse paths execute fewer than the dense per-window count).
+ * Layers: 0 conv1, 1 conv2, 2 conv3, 3 conv4 (+ pool2 on the segment/patch paths), 4 conv5,
+ * 5 conv6, 6 fc1, 7 fc1-reduce, 8 fc2.  Returns the number of layers. */
 int expecto_beluga_set_profiling(expecto_beluga_t h, int on);
-int expecto_beluga_layer_times(expecto_beluga_t h, double* ms, long long* calls, int max_layers);
+int expecto_beluga_layer_times(expecto_beluga_t h, double* ms, long long* calls, double* macs, int max_layers);
 
 /* SNV windows from a device-resident genome (uint8 codes as above).  For variant v and
  * shift s the 2000-code window is genome[off_v + shift - 999 + i], i = 0..1999, with the

@@ -157,3 +157,44 @@ def test_segment_path_is_bitwise_equal_to_per_window_tss():
     a = pipe.predict(*genes, use_segments=True)
     b = pipe.predict(*genes, use_segments=False)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("precision", ["bf16x6", "fp32"])
+def test_pair_path_alt_cone_is_bitwise_equal(precision):
+    """Alt-cone reuse (only the SNV's receptive-field rows recomputed) == full alt forward,
+    for SNVs anywhere in the window, both strands."""
+    import torch
+    eng = _engine(precision)
+    rng = np.random.default_rng(7)
+    pos = np.array([0, 5, 100, 308, 309, 310, 500, 998, 999, 1000, 1500, 1690, 1700, 1701, 1990, 1999], np.int32)
+    n = pos.size
+    ref = torch.from_numpy(rng.integers(0, 5, (n, 2000)).astype(np.uint8)).cuda()
+    alt = ref.clone()
+    newb = torch.from_numpy(((ref.cpu().numpy()[np.arange(n), pos] + 1 + rng.integers(0, 3, n)) % 4)
+                            .astype(np.uint8)).cuda()
+    alt[torch.arange(n), torch.from_numpy(pos).long()] = newb
+    y = torch.empty((2, 2, n, 2002), device="cuda")
+    yv = y.view(4 * n, 2002)
+    eng.forward_pairs(ref, alt, pos, yv[0:], yv[n:], 2 * n, 2)
+    want_ref = eng.forward_codes(ref, 2)
+    want_alt = eng.forward_codes(alt, 2)
+    assert torch.equal(y[:, 0].reshape(2 * n, 2002), want_ref)
+    d = (y[:, 1].reshape(2 * n, 2002) - want_alt).abs().amax(-1).view(2, n).cpu().numpy()
+    assert (d == 0).all(), f"alt rows differ: strand x window max|diff| = {d} (positions {pos})"
+    assert not torch.equal(want_ref, want_alt)
+
+
+def test_variant_pipeline_pairs_equal_per_window():
+    import torch
+    from expecto_amd import synthetic
+    from expecto_amd.genome import DeviceGenome, Fasta
+    from expecto_amd.pipeline import VariantPipeline, VariantSet
+    g = synthetic.genome_bytes(**GENOME_ARGS)
+    fa = Fasta.from_dict(g)
+    snv = synthetic.snvs(g, 37, seed=12)
+    vs = VariantSet([s[0] for s in snv], np.array([s[1] for s in snv]), [s[2] for s in snv], [s[3] for s in snv])
+    eng = _engine()
+    dg = DeviceGenome(fa)
+    a = VariantPipeline(eng, fa, dg, use_pairs=True).predict(vs, [0])
+    b = VariantPipeline(eng, fa, dg, use_pairs=False).predict(vs, [0])
+    assert torch.equal(a, b)

@@ -17,5 +17,5 @@ print(f"n={n} max_batch={mb}: {dt*1e3:.1f} ms, {n/dt:.1f} windows/s, {2*macs_per
 eng.set_profiling(True)
 out = eng.forward_codes(codes, 0)
 torch.cuda.synchronize()
-for k, (ms, c) in eng.layer_times().items():
+for k, (ms, c, _m) in eng.layer_times().items():
     print(f"  {k:11s} {ms:9.2f} ms  ({c} launches)")
