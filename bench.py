@@ -138,6 +138,27 @@ def roofline(layers, precision):
             "fp32_flops_per_launch": fp32_flops_launch, "fp32_tflops": fp32_tflops, "precision": precision}
 
 
+def pmc_traffic(key, kernel):
+    """HBM bytes per launch of ``kernel`` from the newest committed rocprofv3 --pmc summary
+    (profiles/<tag>/traffic.json, written by tools/collect_profiles.py from FETCH_SIZE and
+    WRITE_SIZE passes of this same bench command).  None unless that profile was taken on the
+    same workload key (variants, shifts, precision, max_batch): PMC counters cannot be read
+    live next to the HIP-event timing."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*",
+                                              "traffic.json")), reverse=True):
+        try:
+            t = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if t.get("profile_key") != key:
+            continue
+        for name, v in t["kernels"].items():
+            if kernel in name:
+                return v["hbm_bytes"], t["source"]
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -173,6 +194,12 @@ def main():
     total_rows = rows * args.steps
     value = world * n * args.steps / el
     exec_macs = sum(m for _, _, m in layers.values())
+    key = {"variants": n, "shifts": shifts, "precision": eng.precision, "max_batch": min(rows, 8192)}
+    roof = roofline(layers, eng.precision)
+    roof["traffic"], src = pmc_traffic(key, roof["kernel"])
+    if roof["traffic"] is not None:
+        roof["traffic_unit"] = "bytes/launch (HBM read+write)"
+        roof["traffic_source"] = src
     rec = {
         "metric": METRIC, "value": value, "unit": "variants/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
@@ -186,8 +213,9 @@ def main():
         "windows_per_s": world * total_rows / el,
         "dense_equivalent_tflops": 2.0 * WINDOW_MACS * world * total_rows / el / 1e12,
         "executed_fp32_tflops": 2.0 * exec_macs * world / el / 1e12,
-        "roofline": roofline(layers, eng.precision),
+        "roofline": roof,
         "layer_ms_per_step": {k: ms / args.steps for k, (ms, c, m) in layers.items()},
+        "profile_key": key,
         "reuse": "alt-cone (SNV alt windows recompute <=20 of 106 conv6 rows; bit-identical)" if S == 1 else
                  "segments (trunk shared across shifts; bit-identical)",
     }
