@@ -53,7 +53,7 @@ def kernel_name(layer: str, precision: str) -> str:
     if layer not in GEMM_LAYER_EPI:
         return {"conv1": "beluga_conv1", "fc1_reduce": "fc1_reduce"}[layer]
     l, e = GEMM_LAYER_EPI[layer]
-    return f"beluga_gemm_x6<{l}, {e}, 4, 1>" if precision == "bf16x6" else f"beluga_gemm<{l}, {e}, 4, 2, 32, 1>"
+    return f"beluga_gemm_x6p<{l}, {e}, 0>" if precision == "bf16x6" else f"beluga_gemm<{l}, {e}, 4, 2, 32, 1>"
 WINDOW_MACS = sum(LAYER_MACS.values())
 
 

@@ -1,8 +1,10 @@
-// Beluga forward for MI355X (gfx950 / CDNA4): conv1 one-hot kernel + fp32-MFMA
-// implicit-GEMM kernels with fused bias/ReLU/MaxPool/Sigmoid epilogues.
+// Beluga forward for MI355X (gfx950 / CDNA4): conv1 one-hot kernel + MFMA implicit-GEMM
+// kernels (fp32 MFMA, or the fp32-faithful bf16x6 split) with fused bias/ReLU/MaxPool/
+// Sigmoid epilogues.
 //
 // Replaces the ATen ops launched by Beluga.forward (reference Beluga.py:18-51,
-// SURVEY.md 2.2).  Layout in HBM (per window, channel-last, fp32):
+// SURVEY.md 2.2).  Layout in HBM (per window, channel-last; fp32 rows on the fp32 path,
+// bf16 planes [row][C/32][3][32] on the bf16x6 path, gemm_kernel.h store_act):
 //   act0 [1996][320]  conv1 out (1993 valid)          -> buffer P
 //   act1 [ 496][320]  conv2+pool (496 valid)          -> buffer Q
 //   act2 [ 492][480]  conv3 (489 valid)               -> buffer P
@@ -46,7 +48,7 @@ constexpr int C1_T = 128;
 __global__ __launch_bounds__(320) void beluga_conv1(const float* __restrict__ x, const uint8_t* __restrict__ codes,
                                                     long long code_stride, int n_src, int mode, long long row0,
                                                     const float* __restrict__ w1, const float* __restrict__ b1,
-                                                    float* __restrict__ out, int out_rows, int len) {
+                                                    float* __restrict__ out, int out_rows, int len, int x3) {
   __shared__ floatx4 xs[C1_T + 8];
   const int t0 = blockIdx.x * C1_T;
   const long long win = blockIdx.y;
@@ -89,7 +91,7 @@ __global__ __launch_bounds__(320) void beluga_conv1(const float* __restrict__ x,
   for (int i = 0; i < 32; ++i) w[i] = w1[co * 32 + i];  // [ci*8 + k] as in the reference
   const float bco = b1[co];
   const int tmax = min(C1_T, len - 7 - t0);
-  float* o = out + (win * out_rows + t0) * 320 + co;
+  const long long orow = win * out_rows + t0;
   for (int t = 0; t < tmax; ++t) {
     float s = 0.f;
 #pragma unroll
@@ -100,42 +102,50 @@ __global__ __launch_bounds__(320) void beluga_conv1(const float* __restrict__ x,
       s = fmaf(w[16 + k], v[2], s);
       s = fmaf(w[24 + k], v[3], s);
     }
-    o[(long long)t * 320] = fmaxf(s + bco, 0.f);
+    const float v = fmaxf(s + bco, 0.f);
+    if (x3)
+      store_act<true>(out, orow + t, 320, co, v);
+    else
+      store_act<false>(out, orow + t, 320, co, v);
   }
 }
 
 __global__ void fc1_reduce(const float* __restrict__ part, int splits, long long split_stride, long long count,
-                           const float* __restrict__ bias, float* __restrict__ h1) {
+                           const float* __restrict__ bias, float* __restrict__ h1, int x3) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
-  const int n = (int)(i % kHidLd);
+  const long long row = i / kHidLd;
+  const int n = (int)(i - row * kHidLd);
   float s = 0.f;
   for (int k = 0; k < splits; ++k) s += part[k * split_stride + i];
-  h1[i] = n < kFc1Out ? fmaxf(s + bias[n], 0.f) : 0.f;
+  const float v = n < kFc1Out ? fmaxf(s + bias[n], 0.f) : 0.f;
+  if (x3)
+    store_act<true>(h1, row, kHidLd, n, v);
+  else
+    h1[i] = v;
 }
 
 // MaxPool(1,4) floor mode at pool phases p (segment path, SURVEY.md 5 "trunk sharing"):
 // out[(seg*n_ph + i)*s_out + g][c] = max_{j<4} in[seg*s_in + ph[i] + 4g + j][c],
 // g < (t_in - ph[i]) / 4.  ReLU was applied by the producing conv (Beluga.py:32-34 order).
+// One thread per channel; on the bf16x6 path the values are recovered exactly from their
+// planes, pooled, and re-split (so the planes equal those of the pooled fp32 value).
 __global__ void pool4_phases(const float* __restrict__ in, int n_seg, int s_in, int t_in, int C,
-                             int n_ph, int4 ph, int s_out, float* __restrict__ out) {
-  const int c4 = threadIdx.x;           // C/4 float4 lanes
+                             int n_ph, int4 ph, int s_out, float* __restrict__ out, int x3) {
+  const int c = threadIdx.x;
   const int g = blockIdx.x;
   const int i = blockIdx.y % n_ph;
   const long long seg = blockIdx.y / n_ph;
   const int p = i == 0 ? ph.x : i == 1 ? ph.y : i == 2 ? ph.z : ph.w;
-  if (c4 * 4 >= C || g >= (t_in - p) / 4) return;
-  const float* src = in + (seg * s_in + p + 4LL * g) * C + c4 * 4;
-  floatx4 m = *(const floatx4*)src;
+  if (c >= C || g >= (t_in - p) / 4) return;
+  const long long r0 = seg * s_in + p + 4LL * g, orow = (seg * n_ph + i) * s_out + g;
+  float m = x3 ? load_x3(in, r0, C, c) : in[r0 * C + c];
 #pragma unroll
-  for (int j = 1; j < 4; ++j) {
-    const floatx4 v = *(const floatx4*)(src + (long long)j * C);
-    m[0] = fmaxf(m[0], v[0]);
-    m[1] = fmaxf(m[1], v[1]);
-    m[2] = fmaxf(m[2], v[2]);
-    m[3] = fmaxf(m[3], v[3]);
-  }
-  *(floatx4*)(out + ((seg * n_ph + i) * s_out + g) * C + c4 * 4) = m;
+  for (int j = 1; j < 4; ++j) m = fmaxf(m, x3 ? load_x3(in, r0 + j, C, c) : in[(r0 + j) * C + c]);
+  if (x3)
+    store_act<true>(out, orow, C, c, m);
+  else
+    out[orow * C + c] = m;
 }
 
 // FC1 row table of the windows of one segment chunk: window m of the chunk reads conv6
@@ -192,18 +202,21 @@ __global__ void pair_patch_codes(const uint8_t* __restrict__ alt, long long stri
   out[(long long)m * kPatchLen + i] = c;
 }
 
-// act6[m][r0 + r][:] = patch6[m][r][:] for r < 19 (640 channels, float4 lanes)
+// act6[m][r0 + r][:] = patch6[m][r][:] for r < 20: one conv6 row = row16 16-byte lanes
+// (640 fp32 = 160, or 640 channels of bf16 planes = 240)
 __global__ void pair_patch_apply(const float* __restrict__ patch6, float* __restrict__ act6, int nv, int v0,
-                                 const int* __restrict__ var_pos) {
+                                 const int* __restrict__ var_pos, int row16) {
   const int m = blockIdx.y;
   const int r = blockIdx.x;
-  const int c4 = threadIdx.x;  // 160 lanes
+  const int c4 = threadIdx.x;
+  if (c4 >= row16) return;
   const int s = m / nv, v = v0 + m % nv;
   const int pv = min(max(var_pos[v], 0), kLen - 1);
   const int p = s ? kLen - 1 - pv : pv;
   const int r0 = patch_row0(p);
-  const floatx4 x = *(const floatx4*)(patch6 + ((long long)m * kPatchRows + r) * 640 + 4 * c4);
-  *(floatx4*)(act6 + ((long long)m * 106 + r0 + r) * 640 + 4 * c4) = x;
+  const floatx4* src = reinterpret_cast<const floatx4*>(patch6) + ((long long)m * kPatchRows + r) * row16;
+  floatx4* dst = reinterpret_cast<floatx4*>(act6) + ((long long)m * 106 + r0 + r) * row16;
+  dst[c4] = src[c4];
 }
 
 __global__ void pair_rows(long long* __restrict__ c_rows, int M, int nv, int v0, long long strand_stride) {
@@ -279,6 +292,9 @@ struct expecto_beluga {
   float* fc1b = nullptr;
   float* fc2w = nullptr;
   float* fc2b = nullptr;
+  float* wp[5] = {};             // bf16x6: weight planes of conv2..6, FC1, FC2 (split_planes)
+  float* fc1p = nullptr;
+  float* fc2p = nullptr;
   float* P = nullptr;
   float* Q = nullptr;
   float* part = nullptr;
@@ -320,6 +336,21 @@ int dalloc(expecto_beluga* h, float** p, size_t nfloat) {
 
 int npad_of(int n) { return (n + GBN - 1) / GBN * GBN; }
 
+// floats to allocate for `elements` activation elements in either format (6 B per bf16x6 element)
+size_t act_alloc(size_t elements) { return elements + (elements + 1) / 2; }
+
+// bf16 planes of a repacked fp32 B [rows][K] for the bf16x6 GEMM
+int make_planes(expecto_beluga* h, const float* W, long long rows, long long K, float** out, hipStream_t st) {
+  int rc;
+  if ((rc = dalloc(h, out, act_alloc((size_t)(rows * K))))) return rc;
+  const long long n4 = rows * K / 4;
+  split_planes<<<dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st>>>(W, rows, (int)K,
+                                                                           reinterpret_cast<__bf16*>(*out));
+  return check_launch("split_planes");
+}
+
+// Activation buffers are sized in ELEMENTS (p_floats/q_floats) and allocated with 1.5 floats
+// per element, so they hold either fp32 rows or bf16 planes (6 B per element).
 size_t p_floats(int nb) { return (size_t)nb * kS1 * 320 + 16 * 640; }
 size_t q_floats(int nb) { return (size_t)nb * 496 * 320 + 16 * 640; }
 
@@ -346,11 +377,11 @@ struct LayerTimer {
     if (h->ev_next + 2 > h->ev_pool.size()) resolve_events(h);
     idx = (int)h->ev_next;
     h->ev_next += 2;
-    hipEventRecord(h->ev_pool[idx], st);
+    (void)hipEventRecord(h->ev_pool[idx], st);
   }
   ~LayerTimer() {
     if (idx < 0) return;
-    hipEventRecord(h->ev_pool[idx + 1], st);
+    (void)hipEventRecord(h->ev_pool[idx + 1], st);
     h->pending.push_back({layer, idx});
   }
 };
@@ -359,6 +390,10 @@ struct LayerTimer {
 // 3-way bf16 split (six v_mfma_f32_32x32x16_bf16 products per k-step, gemm_kernel.h).
 thread_local int g_precision = EXPECTO_PRECISION_BF16X6;
 
+// activations stored as bf16 planes (bf16x6 path) or fp32 rows
+int x3_act() { return g_precision == EXPECTO_PRECISION_BF16X6 ? 1 : 0; }
+long long gemm_bm() { return g_precision == EXPECTO_PRECISION_BF16X6 ? X6P_BM : GBM; }
+
 template <int LAYER, int EPI>
 int launch_gemm(const GemmArgs& a, int splits, hipStream_t st) {
   const long long nblk = a.m_tiles * a.n_tiles * splits;
@@ -366,9 +401,11 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st) {
   EXPECTO_REQUIRE(a.kper % GBK == 0 && a.kper > 0, "gemm K not a multiple of 32");
   EXPECTO_REQUIRE(a.lda % 4 == 0 && a.ldb % 4 == 0, "gemm leading dims must be multiples of 4");
   EXPECTO_REQUIRE(a.taps == 1 || (a.taps == 8 && a.lda % GBK == 0), "conv GEMM needs Cin % 32 == 0");
-  if (g_precision == EXPECTO_PRECISION_BF16X6)
-    beluga_gemm_x6<LAYER, EPI, kWM, 1><<<dim3((unsigned)nblk), dim3(64 * kWM), 0, st>>>(a);
-  else
+  EXPECTO_REQUIRE(a.m_tiles * gemm_bm() >= a.M, "gemm M tiles do not cover M");
+  if (g_precision == EXPECTO_PRECISION_BF16X6) {
+    EXPECTO_REQUIRE(a.Bp != nullptr && a.lda % GBK == 0 && a.ldb % GBK == 0, "bf16x6 GEMM needs planes, K % 32");
+    beluga_gemm_x6p<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
+  } else
     beluga_gemm<LAYER, EPI, kWM, kMinBlocks, GBK, kPipe><<<dim3((unsigned)nblk), dim3(64 * kWM), 0, st>>>(a);
   return check_launch("beluga_gemm");
 }
@@ -379,7 +416,7 @@ int run_conv1(expecto_beluga* h, const float* x, const uint8_t* codes, long long
   if (h->profiling) h->macs[0] += (double)nb * (len - 7) * 320 * 32;
   dim3 grid((len - 7 + C1_T - 1) / C1_T, nb);
   beluga_conv1<<<grid, dim3(320), 0, st>>>(x, codes, code_stride, n_src, mode, row0, h->w1, h->b1,
-                                           dst ? dst : h->P, out_rows, len);
+                                           dst ? dst : h->P, out_rows, len, x3_act());
   return check_launch("beluga_conv1");
 }
 
@@ -392,11 +429,12 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
   a.lda = g.cin;
   a.M = groups * s_in;
   a.B = h->wt[l];
+  a.Bp = h->wp[l];
   a.ldb = 8LL * g.cin;
   a.kper = 8 * g.cin;
   a.taps = 8;
   a.n_tiles = npad_of(g.cout) / GBN;
-  a.m_tiles = (a.M + GBM - 1) / GBM;
+  a.m_tiles = (a.M + gemm_bm() - 1) / gemm_bm();
   a.m_fastest = 0;
   a.bias = h->bt[l];
   a.C = dst;
@@ -424,7 +462,7 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
 int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb, float* y, hipStream_t st,
            const long long* c_rows = nullptr) {
   int rc;
-  const long long m_tiles = (nb + GBM - 1) / GBM;
+  const long long m_tiles = (nb + gemm_bm() - 1) / gemm_bm();
   const int n_tiles1 = npad_of(kFc1Out) / GBN;
   int splits = kFcSplits[0];
   for (int s : kFcSplits) {
@@ -438,6 +476,7 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     a.lda = (long long)kFc1In;
     a.M = nb;
     a.B = h->fc1w;
+    a.Bp = h->fc1p;
     a.ldb = kFc1In;
     a.kper = kFc1In / splits;
     a.taps = 1;
@@ -456,7 +495,7 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     LayerTimer lt(h, 7, st);
     const long long count = (long long)nb * kHidLd;
     fc1_reduce<<<dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st>>>(h->part, splits, count, count, h->fc1b,
-                                                                            h->h1);
+                                                                            h->h1, x3_act());
     if ((rc = check_launch("fc1_reduce"))) return rc;
   }
   {
@@ -465,6 +504,7 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     a.lda = kHidLd;
     a.M = nb;
     a.B = h->fc2w;
+    a.Bp = h->fc2p;
     a.ldb = kHidLd;
     a.kper = kHidLd;
     a.taps = 1;
@@ -603,8 +643,8 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
       {  // pool2 phases (Q -> P)
         LayerTimer lt(h, 3, st);
         dim3 grid(g.S5, ns * n_ph);
-        pool4_phases<<<grid, dim3(480 / 4), 0, st>>>(h->Q, ns, g.T4, g.T4, 480, n_ph,
-                                                     make_int4(ph[0], ph[1], ph[2], ph[3]), g.S5, h->P);
+        pool4_phases<<<grid, dim3(480), 0, st>>>(h->Q, ns, g.T4, g.T4, 480, n_ph,
+                                               make_int4(ph[0], ph[1], ph[2], ph[3]), g.S5, h->P, x3_act());
         if ((rc = check_launch("pool4_phases"))) return rc;
       }
       // conv5 (P -> Q), conv6 (Q -> P) over (segment, phase) blocks
@@ -635,8 +675,8 @@ int run_trunk_phase0(expecto_beluga* h, const uint8_t* codes, long long stride, 
   if ((rc = run_conv(h, 2, pbuf, qbuf, nseg, g.T3, g.T4, g.T4, false, st))) return rc;
   {
     LayerTimer lt(h, 3, st);
-    pool4_phases<<<dim3(g.S5, nseg), dim3(480 / 4), 0, st>>>(qbuf, nseg, g.T4, g.T4, 480, 1, make_int4(0, 0, 0, 0),
-                                                             g.S5, pbuf);
+    pool4_phases<<<dim3(g.S5, nseg), dim3(480), 0, st>>>(qbuf, nseg, g.T4, g.T4, 480, 1, make_int4(0, 0, 0, 0),
+                                                         g.S5, pbuf, x3_act());
     if ((rc = check_launch("pool4_phases"))) return rc;
   }
   if ((rc = run_conv(h, 3, pbuf, qbuf, nseg, g.S5, g.T5, g.T5, false, st))) return rc;
@@ -651,7 +691,7 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
     const SegGeo g = seg_geo(kPatchLen, 1);
     size_t pf = (size_t)h->max_batch * g.p_rows_floats + 16 * 640, qf = (size_t)h->max_batch * g.q_rows_floats + 16 * 640;
     int rc;
-    if ((rc = dalloc(h, &h->P2, pf)) || (rc = dalloc(h, &h->Q2, qf))) return rc;
+    if ((rc = dalloc(h, &h->P2, act_alloc(pf))) || (rc = dalloc(h, &h->Q2, act_alloc(qf)))) return rc;
     float* pc = nullptr;
     if ((rc = dalloc(h, &pc, ((size_t)h->max_batch * kPatchLen + 3) / 4))) return rc;
     h->patch_codes = reinterpret_cast<uint8_t*>(pc);
@@ -680,7 +720,8 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
     SegGeo pg;
     if ((rc = run_trunk_phase0(h, h->patch_codes, kPatchLen, R, kPatchLen, h->P2, h->Q2, pg, st))) return rc;
     EXPECTO_REQUIRE(pg.T6 == kPatchRows, "patch geometry");
-    pair_patch_apply<<<dim3(kPatchRows, R), dim3(160), 0, st>>>(h->P2, act6, nv, v0, var_pos);
+    pair_patch_apply<<<dim3(kPatchRows, R), dim3(256), 0, st>>>(h->P2, act6, nv, v0, var_pos,
+                                                                x3_act() ? 240 : 160);
     if ((rc = check_launch("pair_patch_apply"))) return rc;
     if ((rc = run_fc(h, act6, nullptr, R, y_alt, st, h->c_rows))) return rc;
   }
@@ -717,6 +758,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
     repack_conv<<<dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st>>>(params[2 + 2 * l], g.cout, g.cin, np,
                                                                           h->wt[l]);
     pad_copy<<<dim3((np + 255) / 256), dim3(256), 0, st>>>(params[3 + 2 * l], g.cout, np, h->bt[l]);
+    if ((rc = make_planes(h, h->wt[l], np, K, &h->wp[l], st))) return fail(rc);
   }
   const int np1 = npad_of(kFc1Out), np2 = npad_of(kNFeat);
   if ((rc = dalloc(h, &h->fc1w, (size_t)np1 * kFc1In)) || (rc = dalloc(h, &h->fc1b, np1)) ||
@@ -729,12 +771,15 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
     const long long tot2 = (long long)np2 * kHidLd;
     repack_fc2<<<dim3((unsigned)((tot2 + 255) / 256)), dim3(256), 0, st>>>(params[14], np2, h->fc2w);
     pad_copy<<<dim3((np2 + 255) / 256), dim3(256), 0, st>>>(params[15], kNFeat, np2, h->fc2b);
+    if ((rc = make_planes(h, h->fc1w, np1, kFc1In, &h->fc1p, st)) ||
+        (rc = make_planes(h, h->fc2w, np2, kHidLd, &h->fc2p, st)))
+      return fail(rc);
   }
   if ((rc = check_launch("repack"))) return fail(rc);
   const size_t pf = p_floats(max_batch), qf = q_floats(max_batch);
   const size_t partf = (size_t)kFcSplits[5] * max_batch * kHidLd;
-  if ((rc = dalloc(h, &h->P, pf)) || (rc = dalloc(h, &h->Q, qf)) || (rc = dalloc(h, &h->part, partf)) ||
-      (rc = dalloc(h, &h->h1, (size_t)max_batch * kHidLd)))
+  if ((rc = dalloc(h, &h->P, act_alloc(pf))) || (rc = dalloc(h, &h->Q, act_alloc(qf))) ||
+      (rc = dalloc(h, &h->part, partf)) || (rc = dalloc(h, &h->h1, act_alloc((size_t)max_batch * kHidLd))))
     return fail(rc);
   {
     float* rows = nullptr;
@@ -742,8 +787,8 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
     h->a_rows = reinterpret_cast<long long*>(rows);
     h->c_rows = h->a_rows + max_batch;
   }
-  EXPECTO_HIP_CHECK(hipMemsetAsync(h->P, 0, pf * sizeof(float), st));
-  EXPECTO_HIP_CHECK(hipMemsetAsync(h->Q, 0, qf * sizeof(float), st));
+  EXPECTO_HIP_CHECK(hipMemsetAsync(h->P, 0, act_alloc(pf) * sizeof(float), st));
+  EXPECTO_HIP_CHECK(hipMemsetAsync(h->Q, 0, act_alloc(qf) * sizeof(float), st));
   EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
   *out = h;
   return EXPECTO_OK;
@@ -754,8 +799,8 @@ void expecto_beluga_destroy(expecto_beluga_t h) {
   if (h->win_seg_d) (void)hipFree(h->win_seg_d);
   if (h->win_off_d) (void)hipFree(h->win_off_d);
   if (h->win_row_d) (void)hipFree(h->win_row_d);
-  for (void* p : h->allocs) hipFree(p);
-  for (hipEvent_t e : h->ev_pool) hipEventDestroy(e);
+  for (void* p : h->allocs) (void)hipFree(p);
+  for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
   delete h;
 }
 

@@ -40,12 +40,59 @@ struct GemmArgs {
   long long split_stride;
   const long long* a_rows;  // optional: A row m starts at A + a_rows[m] (FC1 over segment windows)
   const long long* c_rows;  // optional: C row of M row m (non-pool epilogues; FC2 output order)
+  const void* Bp;           // x6p only: B as bf16 planes [Npad][K/32][3][32] (split_planes)
 };
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// Exact 3-way bf16 split x = x0 + x1 + x2 (RNE at each level; 3 x 8 significant bits cover
+// fp32's 24).  Every split site (weights, epilogues, pooling, reduce) uses this one routine,
+// so a value always has the same planes wherever it was split.
+__device__ __forceinline__ void split1(const float x, __bf16& x0, __bf16& x1, __bf16& x2) {
+  x0 = (__bf16)x;
+  const float r = x - (float)x0;
+  x1 = (__bf16)r;
+  x2 = (__bf16)(r - (float)x1);
+}
+
+__device__ __forceinline__ void split3(const floatx4 x, bf16x4& h, bf16x4& m, bf16x4& l) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    __bf16 a, b, c;
+    split1(x[j], a, b, c);
+    h[j] = a;
+    m[j] = b;
+    l[j] = c;
+  }
+}
+
+// Activation storage.  fp32 path: row-major [rows][ld] floats.  bf16x6 path ("x3"): bf16
+// planes [rows][ld/32][3][32] -- each 32-channel block of a row holds its x0, x1, x2 planes
+// back to back (192 B), so a consumer's 32-deep K block is one contiguous 192-B run per row.
+__device__ __forceinline__ long long x3_index(long long row, long long ld, int n) {
+  return ((row * (ld >> 5) + (n >> 5)) * 3) * 32 + (n & 31);
+}
+
+template <bool X3>
+__device__ __forceinline__ void store_act(float* C, long long row, long long ld, int n, float v) {
+  if constexpr (X3) {
+    __bf16* d = reinterpret_cast<__bf16*>(C) + x3_index(row, ld, n);
+    split1(v, d[0], d[32], d[64]);
+  } else {
+    C[row * ld + n] = v;
+  }
+}
+
+__device__ __forceinline__ float load_x3(const float* A, long long row, long long ld, int n) {
+  const __bf16* s = reinterpret_cast<const __bf16*>(A) + x3_index(row, ld, n);
+  return (float)s[0] + ((float)s[32] + (float)s[64]);   // exact: recovers the split value
+}
 
 // Epilogue shared by both GEMM kernels. C/D layout of 32x32 MFMA (every dtype on gfx950):
 // col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5), so rows 4g..4g+3 of a pool window sit
 // in registers 4q..4q+3 of ONE lane.
-template <int EPI>
+template <int EPI, bool X3 = false>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, const floatx16 (&acc)[GTN], long long mw, int n0,
                                               int ks, int li, int lh) {
 #pragma unroll
@@ -70,7 +117,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, const floatx16 
         if (tp >= p.t_valid) continue;
         float mx = fmaxf(fmaxf(acc[t][4 * qd], acc[t][4 * qd + 1]), fmaxf(acc[t][4 * qd + 2], acc[t][4 * qd + 3]));
         // maxpool(relu(x+b)) == relu(max(x)+b): x -> fl(x+b) and relu are monotone.
-        p.C[(w * p.s_out + tp) * p.ldc + n] = fmaxf(mx + bn, 0.f);
+        store_act<X3>(p.C, w * p.s_out + tp, p.ldc, n, fmaxf(mx + bn, 0.f));
       }
     } else {
       const float bn = p.bias[n];
@@ -82,13 +129,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& p, const floatx16 
         const int tpos = (int)(m - w * p.s_in);
         if (tpos >= p.t_valid) continue;
         const float v = acc[t][r] + bn;
-        float o;
-        if (EPI == EPI_SIGMOID)
-          o = 1.0f / (1.0f + expf(-v));
-        else
-          o = fmaxf(v, 0.f);
         const long long orow = p.c_rows ? p.c_rows[m] : (w * p.s_out + tpos);
-        p.C[orow * p.ldc + n] = o;
+        if (EPI == EPI_SIGMOID)
+          p.C[orow * p.ldc + n] = 1.0f / (1.0f + expf(-v));
+        else
+          store_act<X3>(p.C, orow, p.ldc, n, fmaxf(v, 0.f));
       }
     }
   }
@@ -240,20 +285,6 @@ __global__ __launch_bounds__(64 * WM, MINB * WM / 4) void beluga_gemm(GemmArgs p
 // accumulator.  Products of bf16 terms are exact in fp32, so the result is fp32-accurate
 // (tools/split_precision_study.py: 0.06 of the parity bound on alt-ref diffs, vs 0.08 for
 // oneDNN fp32) at 6 x 1/16 = 3/8 the MFMA cycles of v_mfma_f32_32x32x2_f32.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ void split3(const floatx4 x, bf16x4& h, bf16x4& m, bf16x4& l) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const __bf16 a = (__bf16)x[j];
-    const float r = x[j] - (float)a;
-    const __bf16 b = (__bf16)r;
-    h[j] = a;
-    m[j] = b;
-    l[j] = (__bf16)(r - (float)b);
-  }
-}
 
 template <int LAYER, int EPI, int WM = 4, int MINB = 2>
 __global__ __launch_bounds__(64 * WM, MINB * WM / 4) void beluga_gemm_x6(GemmArgs p) {
@@ -385,6 +416,235 @@ __global__ __launch_bounds__(64 * WM, MINB * WM / 4) void beluga_gemm_x6(GemmArg
     }
   }
   gemm_epilogue<EPI>(p, acc, m0 + wave * 32, n0, ks, li, lh);
+}
+
+// ---- bf16x6 on pre-split planes with LDS-DMA staging ("x6p", the library's bf16x6 GEMM) ----
+// Same arithmetic and the same MFMA order per accumulator as beluga_gemm_x6 above, hence the
+// same bits (tools/gemm_bench checks it).  What changes is the data movement:
+//  * B (weights) is split once at handle creation into planes [n][k/32][3][32] (split_planes);
+//  * A (activations) is split once by the PRODUCING layer's epilogue into the same planes
+//    layout (store_act<true>); beluga_gemm_x6 re-split every Toeplitz element once per tap;
+//  * both tiles arrive by global_load_lds_dwordx4 (no VGPR round trip, no ds_write) into a
+//    double-buffered LDS ring, one raw barrier per 32-deep K block; each wave stages its own
+//    64 A rows, so it waits for them with its own counted vmcnt, not a barrier;
+//  * each wave owns 64 x 160 (2 x 5 accumulators, 160 AGPRs), four waves = 256 x 160, one
+//    workgroup per CU; B fragments are prefetched one 12-MFMA unit ahead and the LDS-DMA
+//    pieces are issued between units (sched_group_barrier-pinned).
+// Stage = A planes 48 KB + B planes 30 KB + 2 KB pad = 80 KB; two stages fill the CU's LDS.
+// Per wave and stage: 12 A pieces (its rows x 3 planes) + 8 B pieces (30 real + 2 dummies).
+// LDS-DMA writes lane-linear 1 KiB pieces (16 rows x 64 B), so conflict-free ds_read_b128
+// comes from an XOR swizzle on the per-lane SOURCE address, undone on the read:
+//   position = chunk ^ ((row >> 2) & 3)   (the 16 lanes of one ds_read_b128 lane group read
+//                                          16 distinct rows mod 16 at one chunk)
+// tools/gemm_bench, conv2 shape, 1000 windows: 228 fp32-equivalent TF/s vs 190 for
+// beluga_gemm_x6 and 140 for the fp32 MFMA kernel.
+constexpr int X6P_BM = 256;
+constexpr int X6P_B_PLANE = GBN * 64;                     // 10 KB
+constexpr int X6P_A_PLANE = X6P_BM * 64;                  // 16 KB
+constexpr int X6P_A_BYTES = 3 * X6P_A_PLANE;
+constexpr int X6P_STAGE = X6P_A_BYTES + 3 * X6P_B_PLANE + 2048;   // 81,920 B
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
+  __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)lds_dst, 16, 0, 0);
+}
+
+// TM: timing-only probes for tools/gemm_bench (wrong results): 2 = no LDS-DMA in the loop,
+// 4 = no barrier in the loop, 8 = LDS-DMA always from stage 0's (L2-hot) addresses.
+template <int LAYER, int EPI, int TM = 0>
+__global__ __launch_bounds__(256, 1) void beluga_gemm_x6p(GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * X6P_STAGE];
+
+  const unsigned nblk = gridDim.x, bid = blockIdx.x;
+  const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
+  const unsigned lin = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  long long mt;
+  int nt, ks;
+  if (p.m_fastest) {
+    mt = lin % p.m_tiles;
+    const long long rest = lin / p.m_tiles;
+    nt = (int)(rest % p.n_tiles);
+    ks = (int)(rest / p.n_tiles);
+  } else {
+    nt = (int)(lin % (unsigned)p.n_tiles);
+    const long long rest = lin / (unsigned)p.n_tiles;
+    mt = rest % p.m_tiles;
+    ks = (int)(rest / p.m_tiles);
+  }
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
+  const long long m0 = mt * X6P_BM;
+  const int n0 = nt * GBN;
+  const int kb_total = (int)(p.ldb / GBK);
+  const int gs0 = ks * (p.kper / GBK);
+  const long long lda_kb = p.lda / GBK;            // K blocks per A row
+
+  // A pieces: wave w stages its own rows 64w .. 64w+63: 4 pieces (16 rows x 64 B) per plane
+  const __bf16* Ap = (const __bf16*)p.A;
+  const __bf16* asrc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = wave * 64 + j * 16 + (lane >> 2);
+    long long m = m0 + r;
+    if (m > p.M - 1) m = p.M - 1;
+    const int c = (lane & 3) ^ ((r >> 2) & 3);
+    asrc[j] = Ap + (p.a_rows ? p.a_rows[m] / GBK : m * lda_kb) * 96 + 8 * c;
+  }
+  const __bf16* bsrc[8];
+  const __bf16* Bp = (const __bf16*)p.Bp;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int g = min(wave + 4 * j, 29);
+    const int pl = g / 10, r = 16 * (g % 10) + (lane >> 2);
+    const int c = (lane & 3) ^ ((r >> 2) & 3);
+    bsrc[j] = Bp + ((long long)(n0 + r) * kb_total + gs0) * 96 + pl * 32 + 8 * c;
+  }
+  // A piece i (0..11) = plane i / 4, row group i % 4
+  auto issue_a = [&](int s, int buf, int i0, int ni) {
+    if constexpr ((TM & 8) != 0) s = 0;
+    const int gs = gs0 + s;
+    const int chunk = gs / p.taps, tap = gs - chunk * p.taps;
+    const long long ao = ((long long)tap * lda_kb + chunk) * 96;
+    char* base = smem + buf * X6P_STAGE;
+    for (int i = i0; i < i0 + ni; ++i)
+      glds16(asrc[i % 4] + ao + (i / 4) * 32, base + (i / 4) * X6P_A_PLANE + (wave * 4 + i % 4) * 1024);
+  };
+  auto issue_b = [&](int s, int buf, int j0, int nj) {
+    if constexpr ((TM & 8) != 0) s = 0;
+    char* base = smem + buf * X6P_STAGE + X6P_A_BYTES;
+    for (int j = j0; j < j0 + nj; ++j) glds16(bsrc[j] + s * 96, base + (wave + 4 * j) * 1024);
+  };
+
+  floatx16 acc[2][GTN];
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int t = 0; t < GTN; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mb][t][r] = 0.f;
+
+  const int sw = (li >> 2) & 3;                    // same 64-B-row swizzle for A and B planes
+  const int arow = (wave * 64 + li) * 64;
+  const int brow = X6P_A_BYTES + li * 64;
+  const int nk = p.kper / GBK;
+
+  auto read_a = [&](const char* base, int kq, bf16x8 (&a)[2][3]) {
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+      const char* ar = base + arow + mb * 32 * 64 + 16 * ((2 * kq + lh) ^ sw);
+      a[mb][0] = *(const bf16x8*)(ar);
+      a[mb][1] = *(const bf16x8*)(ar + X6P_A_PLANE);
+      a[mb][2] = *(const bf16x8*)(ar + 2 * X6P_A_PLANE);
+    }
+  };
+  auto read_b = [&](const char* base, int kq, int t, bf16x8 (&b)[3]) {
+    const char* br = base + brow + t * 32 * 64 + 16 * ((2 * kq + lh) ^ sw);
+    b[0] = *(const bf16x8*)(br);
+    b[1] = *(const bf16x8*)(br + X6P_B_PLANE);
+    b[2] = *(const bf16x8*)(br + 2 * X6P_B_PLANE);
+  };
+  auto unit = [&](const bf16x8 (&a)[2][3], int t, const bf16x8 (&b)[3]) {
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+      floatx16 c = acc[mb][t];
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][2], b[0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][1], b[1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][0], b[2], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][1], b[0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][0], b[1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][0], b[0], c, 0, 0, 0);
+      acc[mb][t] = c;
+    }
+  };
+  auto pin = [&](int nv) {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if ((i & 1) == 0 && i < 2 * nv) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+    }
+  };
+
+  issue_a(0, 0, 0, 12);
+  issue_b(0, 0, 0, 8);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  bf16x8 as[2][2][3];  // [kq][mb][plane]
+  read_a(smem, 0, as[0]);
+  for (int s = 0; s < nk; ++s) {
+    const int buf = s & 1;
+    const int sn = (TM & 2) ? s : min(s + 1, nk - 1);
+    const char* base = smem + buf * X6P_STAGE;
+    const char* nbase = smem + (buf ^ 1) * X6P_STAGE;
+    const bool go = !(TM & 2);
+    bf16x8 b0[3], b1[3];
+    read_b(base, 0, 0, b0);
+    read_a(base, 1, as[1]);
+    // kq = 0 on as[0]; stage s+1's 12 A pieces go out first, then its 8 B pieces
+    read_b(base, 0, 1, b1);
+    if (go) issue_a(sn, buf ^ 1, 0, 3);
+    unit(as[0], 0, b0);
+    pin(3);
+    read_b(base, 0, 2, b0);
+    if (go) issue_a(sn, buf ^ 1, 3, 3);
+    unit(as[0], 1, b1);
+    pin(3);
+    read_b(base, 0, 3, b1);
+    if (go) issue_a(sn, buf ^ 1, 6, 3);
+    unit(as[0], 2, b0);
+    pin(3);
+    read_b(base, 0, 4, b0);
+    if (go) issue_a(sn, buf ^ 1, 9, 3);
+    unit(as[0], 3, b1);
+    pin(3);
+    read_b(base, 1, 0, b1);
+    if (go) issue_b(sn, buf ^ 1, 0, 3);
+    unit(as[0], 4, b0);
+    pin(3);
+    read_b(base, 1, 1, b0);
+    if (go) issue_b(sn, buf ^ 1, 3, 3);
+    unit(as[1], 0, b1);
+    pin(3);
+    read_b(base, 1, 2, b1);
+    if (go) issue_b(sn, buf ^ 1, 6, 2);
+    unit(as[1], 1, b0);
+    pin(2);
+    // this wave's 12 A pieces of stage s+1 are older than its 8 B pieces: vmcnt(8)
+    if constexpr (!(TM & 2)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    read_b(base, 1, 3, b0);
+    unit(as[1], 2, b1);
+    pin(0);
+    read_a(nbase, 0, as[0]);
+    read_b(base, 1, 4, b1);
+    unit(as[1], 3, b0);
+    pin(0);
+    unit(as[1], 4, b1);
+    pin(0);
+    if constexpr (!(TM & 4)) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    asm volatile("" ::: "memory");
+  }
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb) gemm_epilogue<EPI, true>(p, acc[mb], m0 + wave * 64 + mb * 32, n0, ks, li, lh);
+}
+
+// B planes for beluga_gemm_x6p from a K-contiguous fp32 B [rows][K] (K % 32 == 0).
+__global__ void split_planes(const float* __restrict__ W, long long rows, int K, __bf16* __restrict__ Bp) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * K / 4) return;
+  const long long e = 4 * i, n = e / K;
+  const int k = (int)(e - n * K), kb = k / GBK, j = k % GBK;
+  bf16x4 h, m, l;
+  split3(*(const floatx4*)(W + e), h, m, l);
+  __bf16* d = Bp + ((n * (K / GBK) + kb) * 3) * GBK + j;
+  *(bf16x4*)d = h;
+  *(bf16x4*)(d + GBK) = m;
+  *(bf16x4*)(d + 2 * GBK) = l;
 }
 
 }  // namespace expecto

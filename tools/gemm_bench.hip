@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstdint>
 #include <cstring>
 #include <functional>
 #include <random>
@@ -39,6 +40,11 @@ Variant mk6(const char* name) {
   return {name, 32 * WM, [](const GemmArgs& a, unsigned nblk) {
             beluga_gemm_x6<L, EPI, WM, MINB><<<nblk, 64 * WM>>>(a);
           }};
+}
+
+template <int L, int EPI, int TM = 0>
+Variant mk6p(const char* name) {
+  return {name, X6P_BM, [](const GemmArgs& a, unsigned nblk) { beluga_gemm_x6p<L, EPI, TM><<<nblk, 256>>>(a); }};
 }
 
 template <int L, int EPI, int WM, int MINB, int BK, int PIPE = 0>
@@ -77,27 +83,35 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&bias, npad * 4));
   const size_t csz = (size_t)nb * sh.s_out * sh.cout;
   CK(hipMalloc(&C0, csz * 4));
-  CK(hipMalloc(&C1, csz * 4));
+  CK(hipMalloc(&C1, csz * 6));   // x6p writes bf16 planes (6 B per element)
   fill(X, xa, 0.f, 1.f, 1);
   fill(W, (size_t)npad * K, -0.05f, 0.05f, 2);
   fill(bias, npad, -0.1f, 0.1f, 3);
 
   std::vector<Variant> vs;
+  __bf16* Bp;
+  CK(hipMalloc(&Bp, (size_t)npad * K * 6));
+  split_planes<<<(unsigned)(((long long)npad * K / 4 + 255) / 256), 256>>>(W, npad, K, Bp);
+  __bf16* Xp;
+  CK(hipMalloc(&Xp, xa * 6));
+  split_planes<<<(unsigned)((xa / 4 + 255) / 256), 256>>>(X, (long long)(M + 64), sh.cin, Xp);
+  CK(hipDeviceSynchronize());
+  // variant 0 is the reference for the bitwise comparison: x6 and x6d must agree exactly
   if (sh.pool) {
-    vs.push_back(mk<2, EPI_RELU_POOL4, 4, 2, 32, 1>("f32_pipe"));
-    vs.push_back(mk6<2, EPI_RELU_POOL4, 4, 2>("x6_wm4_b2"));
     vs.push_back(mk6<2, EPI_RELU_POOL4, 4, 1>("x6_wm4_b1"));
-    vs.push_back(mk6<2, EPI_RELU_POOL4, 8, 1>("x6_wm8_b1"));
+    vs.push_back(mk6p<2, EPI_RELU_POOL4>("x6p"));
+    vs.push_back(mk6p<2, EPI_RELU_POOL4, 2>("x6p_noglds"));
+    vs.push_back(mk<2, EPI_RELU_POOL4, 4, 2, 32, 1>("f32_pipe"));
   } else {
-    vs.push_back(mk<3, EPI_RELU, 4, 2, 32, 1>("f32_pipe"));
-    vs.push_back(mk6<3, EPI_RELU, 4, 2>("x6_wm4_b2"));
     vs.push_back(mk6<3, EPI_RELU, 4, 1>("x6_wm4_b1"));
-    vs.push_back(mk6<3, EPI_RELU, 8, 1>("x6_wm8_b1"));
+    vs.push_back(mk6p<3, EPI_RELU>("x6p"));
+    vs.push_back(mk<3, EPI_RELU, 4, 2, 32, 1>("f32_pipe"));
   }
   auto args_for = [&](int bm, float* C) {
     GemmArgs a{};
     a.A = X; a.lda = sh.cin; a.M = M; a.B = W; a.ldb = K; a.kper = K; a.taps = 8;
     a.n_tiles = npad / GBN; a.m_tiles = (M + bm - 1) / bm; a.m_fastest = 0; a.bias = bias;
+    a.Bp = Bp;
     a.C = C; a.ldc = sh.cout; a.n_store = sh.cout; a.s_in = sh.s_in; a.t_valid = sh.t_valid; a.s_out = sh.s_out;
     return a;
   };
@@ -109,8 +123,9 @@ int main(int argc, char** argv) {
   for (int r = 0; r < rounds; ++r) {
     for (size_t v = 0; v < vs.size(); ++v) {
       float* C = v == 0 ? C0 : C1;
-      CK(hipMemset(C, 0, csz * 4));
+      CK(hipMemset(C, 0, v == 0 ? csz * 4 : csz * 6));
       GemmArgs a = args_for(vs[v].bm, C);
+      if (vs[v].name.rfind("x6p", 0) == 0) a.A = (const float*)Xp;
       unsigned nblk = (unsigned)(a.m_tiles * a.n_tiles);
       vs[v].launch(a, nblk);  // warm
       CK(hipEventRecord(e0));
@@ -121,7 +136,18 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       times[v].push_back(ms);
       if (r == 0) {
-        CK(hipMemcpy(v == 0 ? ref.data() : out.data(), C, csz * 4, hipMemcpyDeviceToHost));
+        if (vs[v].name.rfind("x6p", 0) == 0) {   // decode planes [row][cout/32][3][32]
+          std::vector<uint16_t> pl(csz * 3);
+          CK(hipMemcpy(pl.data(), C, csz * 6, hipMemcpyDeviceToHost));
+          auto f = [](uint16_t b) { uint32_t u = (uint32_t)b << 16; float x; memcpy(&x, &u, 4); return x; };
+          for (size_t i = 0; i < csz; ++i) {
+            const size_t row = i / sh.cout, n = i % sh.cout;
+            const size_t k = ((row * (sh.cout / 32) + n / 32) * 3) * 32 + n % 32;
+            out[i] = f(pl[k]) + (f(pl[k + 32]) + f(pl[k + 64]));
+          }
+        } else {
+          CK(hipMemcpy(v == 0 ? ref.data() : out.data(), C, csz * 4, hipMemcpyDeviceToHost));
+        }
         if (v > 0) {
           double mx = 0, md = 0;
           size_t bad = 0;
