@@ -38,6 +38,9 @@ SIGNATURES = {
                                                c_vp, c_vp, c_vp]),
     "expecto_beluga_forward_pairs": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_longlong, c_vp,
                                                     ctypes.c_int, c_vp, c_vp, ctypes.c_longlong, c_vp]),
+    "expecto_beluga_forward_segment_pairs": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_int,
+                                                            ctypes.c_longlong, ctypes.c_int, c_vp, c_vp, c_vp,
+                                                            ctypes.c_int, c_vp, c_vp, ctypes.c_longlong, c_vp]),
     "expecto_beluga_set_precision": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "expecto_beluga_get_precision": (ctypes.c_int, [c_vp]),
     "expecto_beluga_set_profiling": (ctypes.c_int, [c_vp, ctypes.c_int]),

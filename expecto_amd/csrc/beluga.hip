@@ -165,58 +165,220 @@ __global__ void seg_a_rows(const int* __restrict__ win_seg, const int* __restric
   a_rows[m] = (blk * s7 + off6) * 640;
 }
 
-// ---- alt-cone reuse for SNV ref/alt window pairs ---------------------------------------
-// A conv6 row t of a window depends on input positions [16t, 16t+309] (receptive field 310).
-// An SNV at window index p therefore changes only rows t in [ceil((p-309)/16), floor(p/16)]
-// (at most 20 of 106).  The alt window is computed as: the ref window's conv6 rows, with the
-// 20 rows starting at r0 replaced by the conv6 rows of a 616-bp "patch" sequence cut from the
-// alt window at 16*r0 (16-aligned, so pool1/pool2 groups coincide with the window's).  Every
-// row is produced by the same kernels from the same operands -> bit-identical alt outputs.
-constexpr int kPatchLen = 616;   // 16*19 + 310 rounded up to 4 -> 20 conv6 rows
-constexpr int kPatchRows = 20;
-constexpr int kPatchMaxRow0 = 106 - kPatchRows;
+// ---- alt-cone reuse for SNV ref/alt window pairs (per-layer deltas) ---------------------
+// An SNV at window index p changes only a few rows of each layer.  With the ref window's
+// layer l-1 activations at hand (the ping-pong buffer holds them while layer l is computed
+// for the ref windows) the alt window's layer l is obtained by recomputing a fixed-size run
+// of W_l rows starting at r_l, from an "assembled" input patch: the ref rows of layer l-1
+// with the alt's own recomputed rows of layer l-1 spliced in.  Rows outside [r_l, r_l+W_l)
+// are unchanged (they see only unchanged inputs), so the alt conv6 output is the ref's with
+// rows [r6, r6+20) replaced.  Every recomputed row uses the same operands, kernel and K order
+// as the full forward -> bit-identical alt outputs (tests/test_gpu_pipelines.py).
+//   layer    changed rows (from the previous run)          W     input rows (A patch)
+//   conv1    [p-7, p]                                      8     15 codes
+//   conv2+p  pooled [floor((r1-7)/4), floor((r1+7)/4)]     5     4*5+7 -> 28
+//   conv3    [r2-7, r2+4]                                  12    19
+//   conv4+p  pooled [floor((r3-7)/4), floor((r3+11)/4)]    6     4*6+7 -> 32
+//   conv5    [r4-7, r4+5]                                  13    20
+//   conv6    [r5-7, r5+12]                                 20    27
+// Each start is clamped to [0, T_l - W_l] (T_l = valid rows of layer l), which keeps the run
+// inside the layer and still covers every changed row.
+constexpr int kDW[7] = {0, 8, 5, 12, 6, 13, 20};         // W_l, l = 1..6
+constexpr int kDA[7] = {0, 15, 28, 19, 32, 20, 27};      // input rows of the layer-l patch
+constexpr int kDT[7] = {0, 1993, 496, 489, 120, 113, 106};
+constexpr int kDC[7] = {4, 320, 320, 480, 480, 640, 640};  // channels of layer l's output
 
-__device__ __forceinline__ int patch_row0(int p) {
-  const int t_lo = p >= 309 ? (p - 309 + 15) / 16 : 0;
-  return t_lo < kPatchMaxRow0 ? t_lo : kPatchMaxRow0;
+struct DeltaRows {
+  int r[7];    // r[l]: first recomputed row of layer l
+  int base[7]; // base[l]: first row of layer l-1 in layer l's input patch
+};
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+__device__ __forceinline__ int floor4(int v) { return v >= 0 ? v >> 2 : -((3 - v) >> 2); }
+
+__device__ __forceinline__ DeltaRows delta_rows(int p) {
+  DeltaRows d;
+  d.r[0] = p;
+  d.r[1] = clampi(p - 7, 0, kDT[1] - kDW[1]);
+  d.r[2] = clampi(floor4(d.r[1] - 7), 0, kDT[2] - kDW[2]);
+  d.r[3] = clampi(d.r[2] - 7, 0, kDT[3] - kDW[3]);
+  d.r[4] = clampi(floor4(d.r[3] - 7), 0, kDT[4] - kDW[4]);
+  d.r[5] = clampi(d.r[4] - 7, 0, kDT[5] - kDW[5]);
+  d.r[6] = clampi(d.r[5] - 7, 0, kDT[6] - kDW[6]);
+  d.base[0] = 0;
+  d.base[1] = d.r[1];
+  d.base[2] = 4 * d.r[2];
+  d.base[3] = d.r[3];
+  d.base[4] = 4 * d.r[4];
+  d.base[5] = d.r[5];
+  d.base[6] = d.r[6];
+  return d;
 }
 
-// m = strand*nv + (v - v0); strand 1 = reverse complement of the alt window.
-__global__ void pair_patch_codes(const uint8_t* __restrict__ alt, long long stride, int nv, int v0,
-                                 const int* __restrict__ var_pos, uint8_t* __restrict__ out) {
-  const int m = blockIdx.y;
+// window m = strand * nv + (v - v0); SNV index in that strand's window coordinates
+__device__ __forceinline__ int pair_pos(const int* var_pos, int m, int nv, int v0) {
   const int s = m / nv, v = v0 + m % nv;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= kPatchLen) return;
   const int pv = min(max(var_pos[v], 0), kLen - 1);
-  const int p = s ? kLen - 1 - pv : pv;
-  const int start = 16 * patch_row0(p);
+  return s ? kLen - 1 - pv : pv;
+}
+
+// conv1 input of the alt run: 16 codes starting at r1 of the alt window (15 used).
+__global__ void delta_codes(const uint8_t* __restrict__ alt, long long stride, int nv, int v0,
+                            const int* __restrict__ var_pos, uint8_t* __restrict__ out, int R) {
+  const int i = threadIdx.x & 15;
+  const int m = blockIdx.x * (blockDim.x >> 4) + (threadIdx.x >> 4);
+  if (m >= R) return;
+  const int s = m / nv, v = v0 + m % nv;
+  const int start = delta_rows(pair_pos(var_pos, m, nv, v0)).r[1];
   const uint8_t* a = alt + (long long)v * stride;
+  const int pos = min(start + i, kLen - 1);
   uint8_t c;
   if (s) {
-    const uint8_t f = a[kLen - 1 - (start + i)];
+    const uint8_t f = a[kLen - 1 - pos];
     c = f < 4 ? (uint8_t)(3 - f) : f;
   } else {
-    c = a[start + i];
+    c = a[pos];
   }
-  out[(long long)m * kPatchLen + i] = c;
+  out[(long long)m * 16 + i] = c;
 }
 
-// act6[m][r0 + r][:] = patch6[m][r][:] for r < 20: one conv6 row = row16 16-byte lanes
-// (640 fp32 = 160, or 640 channels of bf16 planes = 240)
-__global__ void pair_patch_apply(const float* __restrict__ patch6, float* __restrict__ act6, int nv, int v0,
+// Input patch of layer l (l = 2..6) for alt window m: rows base_l + i (i < kDA[l]) of the ref
+// layer l-1 (row stride ref_rows per window), except rows inside [r_{l-1}, r_{l-1}+W_{l-1})
+// which come from the alt run of layer l-1 (dprev, kDW[l-1] rows per window).  Rows are
+// row16 16-byte lanes (fp32 rows or bf16 planes of the same channels).
+__global__ void delta_assemble(const float* __restrict__ ref, int ref_rows, const float* __restrict__ dprev, int l,
+                               int row16, int nv, int v0, const int* __restrict__ var_pos,
+                               float* __restrict__ out) {
+  const int m = blockIdx.y;
+  const int i = blockIdx.x;
+  const DeltaRows d = delta_rows(pair_pos(var_pos, m, nv, v0));
+  const int src = d.base[l] + i, rp = d.r[l - 1];
+  const floatx4* from = (src >= rp && src < rp + kDW[l - 1])
+                            ? reinterpret_cast<const floatx4*>(dprev) + ((long long)m * kDW[l - 1] + src - rp) * row16
+                            : reinterpret_cast<const floatx4*>(ref) + ((long long)m * ref_rows + src) * row16;
+  floatx4* to = reinterpret_cast<floatx4*>(out) + ((long long)m * kDA[l] + i) * row16;
+  for (int c = threadIdx.x; c < row16; c += blockDim.x) to[c] = from[c];
+}
+
+// alt conv6 = ref conv6 (act6, 106 rows per window) with rows [r6, r6+20) from the alt run
+__global__ void pair_patch_apply(const float* __restrict__ d6, float* __restrict__ act6, int nv, int v0,
                                  const int* __restrict__ var_pos, int row16) {
   const int m = blockIdx.y;
   const int r = blockIdx.x;
-  const int c4 = threadIdx.x;
-  if (c4 >= row16) return;
-  const int s = m / nv, v = v0 + m % nv;
-  const int pv = min(max(var_pos[v], 0), kLen - 1);
-  const int p = s ? kLen - 1 - pv : pv;
-  const int r0 = patch_row0(p);
-  const floatx4* src = reinterpret_cast<const floatx4*>(patch6) + ((long long)m * kPatchRows + r) * row16;
-  floatx4* dst = reinterpret_cast<floatx4*>(act6) + ((long long)m * 106 + r0 + r) * row16;
-  dst[c4] = src[c4];
+  const int r6 = delta_rows(pair_pos(var_pos, m, nv, v0)).r[6];
+  const floatx4* src = reinterpret_cast<const floatx4*>(d6) + ((long long)m * kDW[6] + r) * row16;
+  floatx4* dst = reinterpret_cast<floatx4*>(act6) + ((long long)m * 106 + r6 + r) * row16;
+  for (int c = threadIdx.x; c < row16; c += blockDim.x) dst[c] = src[c];
+}
+
+// ---- alt deltas on the segment path (shift sweeps) -------------------------------------
+// Same idea as the pair path, in segment coordinates: the alt segment differs from the ref
+// segment at one base q (q' = L-1-q on the reverse-complement strand).  conv1..conv3 runs as
+// above; conv4 is unpooled on the segment path, so its run is the 19 rows [r4u, r4u+19); each
+// pool2 phase p then changes <= 6 pooled rows [r4p, r4p+6) and conv5 / conv6 runs follow per
+// (segment, phase) block.  Starts are clamped with the phase-0 (longest) geometry, like the
+// ref blocks; rows past a phase's valid length are never read by any window.
+// Per-segment table (kSegTab ints): q', r1, r2, r3, r4u, r4p[4], r5[4], r6[4].
+constexpr int kSegTab = 20;
+constexpr int kW4u = 19, kA4u = 26;
+struct SegDims {
+  int L, T1, P1, T3, T4, S5, T5, T6;
+};
+
+__global__ void seg_delta_table(const int* __restrict__ var_pos, int s0, int ns, int rc, SegDims g, int n_ph, int4 ph,
+                                int* __restrict__ tab) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= ns) return;
+  int q = min(max(var_pos[s0 + m], 0), g.L - 1);
+  if (rc) q = g.L - 1 - q;
+  int* t = tab + m * kSegTab;
+  const int r1 = clampi(q - 7, 0, g.T1 - kDW[1]);
+  const int r2 = clampi(floor4(r1 - 7), 0, g.P1 - kDW[2]);
+  const int r3 = clampi(r2 - 7, 0, g.T3 - kDW[3]);
+  const int r4 = clampi(r3 - 7, 0, g.T4 - kW4u);
+  t[0] = q;
+  t[1] = r1;
+  t[2] = r2;
+  t[3] = r3;
+  t[4] = r4;
+  for (int i = 0; i < n_ph; ++i) {
+    const int p = i == 0 ? ph.x : i == 1 ? ph.y : i == 2 ? ph.z : ph.w;
+    // pooled rows g of phase p read conv4 rows p+4g .. p+4g+3: the changed ones meet [r4, r4+19)
+    const int r4p = clampi(floor4(r4 - p), 0, g.S5 - kDW[4]);
+    const int r5 = clampi(r4p - 7, 0, g.T5 - kDW[5]);
+    t[5 + i] = r4p;
+    t[9 + i] = r5;
+    t[13 + i] = clampi(r5 - 7, 0, g.T6 - kDW[6]);
+  }
+}
+
+// 16 codes from r1 of the alt segment, in the strand's orientation (rc: mirrored, complemented)
+__global__ void seg_delta_codes(const uint8_t* __restrict__ codes, long long stride, const uint8_t* __restrict__ alt_code,
+                                int s0, int ns, int rc, int L, const int* __restrict__ tab, uint8_t* __restrict__ out) {
+  const int i = threadIdx.x & 15;
+  const int m = blockIdx.x * (blockDim.x >> 4) + (threadIdx.x >> 4);
+  if (m >= ns) return;
+  const int q = tab[m * kSegTab], x = min(tab[m * kSegTab + 1] + i, L - 1);
+  uint8_t c = x == q ? alt_code[s0 + m] : codes[(long long)(s0 + m) * stride + (rc ? L - 1 - x : x)];
+  if (rc && c < 4) c = (uint8_t)(3 - c);
+  out[(long long)m * 16 + i] = c;
+}
+
+// Input patch of one alt run: rows base + i (i < arows) of ref block m (ref_rows rows per
+// block), except rows inside [rp, rp + wprev), taken from the previous alt run.  Blocks are
+// segments (nb = 1) or (segment, phase) pairs (nb = n_ph, per-phase table entries).
+// base = mult * tab[ib (+ phase)], rp = tab[irp (+ phase)].
+__global__ void seg_delta_assemble(const float* __restrict__ ref, int ref_rows, const float* __restrict__ dprev,
+                                   int wprev, const int* __restrict__ tab, int nb, int ib, int mult, int irp,
+                                   int arows, int row16, float* __restrict__ out) {
+  const int m = blockIdx.y;
+  const int i = blockIdx.x;
+  const int seg = m / nb, off = nb > 1 ? m % nb : 0;
+  const int src = mult * tab[seg * kSegTab + ib + off] + i, rp = tab[seg * kSegTab + irp + off];
+  const floatx4* from = (src >= rp && src < rp + wprev)
+                            ? reinterpret_cast<const floatx4*>(dprev) + ((long long)m * wprev + src - rp) * row16
+                            : reinterpret_cast<const floatx4*>(ref) + ((long long)m * ref_rows + src) * row16;
+  floatx4* to = reinterpret_cast<floatx4*>(out) + ((long long)m * arows + i) * row16;
+  for (int c = threadIdx.x; c < row16; c += blockDim.x) to[c] = from[c];
+}
+
+// pool2 of the alt run for each phase: pooled rows [r4p, r4p+6) of block (seg, phase) from the
+// ref's unpooled conv4 rows and the alt conv4 run (exact max, as pool4_phases)
+__global__ void seg_delta_pool(const float* __restrict__ conv4, int t4, const float* __restrict__ d4, int n_ph,
+                               int4 ph, const int* __restrict__ tab, int x3, float* __restrict__ out) {
+  const int c = threadIdx.x;
+  if (c >= 480) return;
+  const int gi = blockIdx.x, m = blockIdx.y;
+  const int seg = m / n_ph, i = m % n_ph;
+  const int p = i == 0 ? ph.x : i == 1 ? ph.y : i == 2 ? ph.z : ph.w;
+  const int r4 = tab[seg * kSegTab + 4];
+  const int row0 = p + 4 * (tab[seg * kSegTab + 5 + i] + gi);
+  float mx = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = row0 + j;
+    const bool alt = row >= r4 && row < r4 + kW4u;
+    const float* b = alt ? d4 : conv4;
+    const long long r = alt ? (long long)seg * kW4u + row - r4 : (long long)seg * t4 + row;
+    const float v = x3 ? load_x3(b, r, 480, c) : b[r * 480 + c];
+    mx = j == 0 ? v : fmaxf(mx, v);
+  }
+  if (x3)
+    store_act<true>(out, (long long)m * kDW[4] + gi, 480, c, mx);
+  else
+    out[((long long)m * kDW[4] + gi) * 480 + c] = mx;
+}
+
+// alt conv6 phase blocks: the ref block (t6 rows) with rows [r6, r6+20) from the alt run
+__global__ void seg_alt_blocks(const float* __restrict__ ref6, const float* __restrict__ d6, int n_ph, int t6,
+                               const int* __restrict__ tab, int row16, float* __restrict__ out) {
+  const int t = blockIdx.x, m = blockIdx.y;
+  const int r6 = tab[(m / n_ph) * kSegTab + 13 + m % n_ph];
+  const floatx4* src = (t >= r6 && t < r6 + kDW[6])
+                           ? reinterpret_cast<const floatx4*>(d6) + ((long long)m * kDW[6] + t - r6) * row16
+                           : reinterpret_cast<const floatx4*>(ref6) + ((long long)m * t6 + t) * row16;
+  floatx4* dst = reinterpret_cast<floatx4*>(out) + ((long long)m * t6 + t) * row16;
+  for (int c = threadIdx.x; c < row16; c += blockDim.x) dst[c] = src[c];
 }
 
 __global__ void pair_rows(long long* __restrict__ c_rows, int M, int nv, int v0, long long strand_stride) {
@@ -278,7 +440,9 @@ constexpr ConvGeo kConv[5] = {
     {480, 640, 120, 113, 113, 0},  // conv5
     {640, 640, 113, 106, 106, 0},  // conv6 -> FC1 reads 106*640 = 67840 contiguous floats
 };
-constexpr int kFcSplits[] = {1, 2, 4, 5, 8, 10};  // divisors of 67840/32 = 2120
+// FC1 split-K: always 10 slabs of 6784 (a divisor of 67840/32 = 2120 blocks), whatever the
+// batch, so an FC1 output never depends on how many windows shared the launch.
+constexpr int kFcSplits = 10;
 }  // namespace
 
 struct expecto_beluga {
@@ -304,9 +468,11 @@ struct expecto_beluga {
   int* win_seg_d = nullptr;     // window tables of the current segment call
   int* win_off_d = nullptr;
   int* win_row_d = nullptr;
-  float* P2 = nullptr;           // patch trunk buffers (alt-cone path), lazily allocated
-  float* Q2 = nullptr;
-  uint8_t* patch_codes = nullptr;
+  float* DA = nullptr;           // alt-delta buffers (pair path), lazily allocated:
+  float* D0 = nullptr;           //   DA = assembled input patch, D0/D1 = alternating W_l-row runs
+  float* D1 = nullptr;
+  uint8_t* delta_codes = nullptr;
+  int* seg_tab = nullptr;        //   per-segment delta rows (segment pairs)
   int win_cap = 0;
   size_t bytes = 0;
   std::vector<void*> allocs;
@@ -464,11 +630,7 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
   int rc;
   const long long m_tiles = (nb + gemm_bm() - 1) / gemm_bm();
   const int n_tiles1 = npad_of(kFc1Out) / GBN;
-  int splits = kFcSplits[0];
-  for (int s : kFcSplits) {
-    splits = s;
-    if (m_tiles * n_tiles1 * s >= 1000) break;
-  }
+  const int splits = kFcSplits;
   {
     GemmArgs a{};
     a.A = act;
@@ -542,6 +704,23 @@ int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long 
   return run_fc(h, src, nullptr, nb, y, st);  // src = act5 (buffer Q), 106 x 640 rows per window
 }
 
+// Alt-run buffers, sized for max_batch blocks (a window, or a (segment, phase) block):
+// the largest input patch (27 x 640) and run (20 x 640), + Toeplitz over-read pad.
+int ensure_delta(expecto_beluga* h) {
+  if (h->DA) return EXPECTO_OK;
+  const size_t pad = 16 * 640;
+  const size_t da = (size_t)h->max_batch * kDA[6] * 640 + pad, dd = (size_t)h->max_batch * kDW[6] * 640 + pad;
+  float *pc = nullptr, *tb = nullptr;
+  int rc;
+  if ((rc = dalloc(h, &h->DA, act_alloc(da))) || (rc = dalloc(h, &h->D0, act_alloc(dd))) ||
+      (rc = dalloc(h, &h->D1, act_alloc(dd))) || (rc = dalloc(h, &pc, (size_t)h->max_batch * 4)) ||
+      (rc = dalloc(h, &tb, (size_t)h->max_batch * kSegTab)))
+    return rc;
+  h->delta_codes = reinterpret_cast<uint8_t*>(pc);
+  h->seg_tab = reinterpret_cast<int*>(tb);
+  return EXPECTO_OK;
+}
+
 // ---- segment path: windows that are slices of longer sequences share the trunk --------
 // A segment of L codes (L % 4 == 0); a window at offset o (o % 4 == 0, o + 2000 <= L).
 // conv1..conv4 run once over the segment; pool1 is fused into conv2 (phase 0 serves every
@@ -573,11 +752,22 @@ SegGeo seg_geo(int L, int n_ph) {
   return g;
 }
 
+// Segment pairs: the alt segment s is segment s with code alt_code[s] at var_pos[s] (DEVICE
+// arrays); its windows (the same offsets) go to y_alt, computed through per-layer alt runs.
+struct SegPairs {
+  const int* var_pos;
+  const uint8_t* alt_code;
+  float* y_alt;
+  long long strand_stride;
+};
+
 int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, long long code_stride, int mode,
                      const int* win_seg, const int* win_off, const int* win_row, int n_win, float* y,
-                     hipStream_t st) {
+                     hipStream_t st, const SegPairs* pr = nullptr) {
   EXPECTO_REQUIRE(L >= kLen && L % 4 == 0, "segment length must be >= 2000 and a multiple of 4");
   g_precision = h->precision;
+  int rc;
+  if (pr && (rc = ensure_delta(h))) return rc;
   // phases present (fwd and, for BOTH, the mirrored rc offsets)
   int present[4] = {0, 0, 0, 0};
   for (int w = 0; w < n_win; ++w) {
@@ -622,106 +812,130 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
   // the tables are caller-owned pageable host memory: finish the copies before returning
   EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
   const int strands = mode == EXPECTO_STRAND_BOTH ? 2 : 1;
-  int rc;
+  // alt runs: one block per segment (conv1..4) or per (segment, phase) (pool2, conv5, conv6)
+  const int blk_per_seg = pr ? std::max(n_ph, 1) : 0;
+  const long long strand_rows = pr ? pr->strand_stride : n_win;
+  const int eb = x3_act() ? 6 : 4;
+  const SegDims gd{L, g.T1, g.P1, g.T3, g.T4, g.S5, g.T5, g.T6};
+  const int4 ph4 = make_int4(ph[0], ph[1], ph[2], ph[3]);
   for (int sd = 0; sd < strands; ++sd) {
     const bool is_rc = (mode == EXPECTO_STRAND_RC) || sd == 1;
     for (int s0 = 0; s0 < n_seg;) {
-      // grow the chunk while the segment buffers and the FC workspace (<= max_batch windows) fit
+      // grow the chunk while the segment buffers, the FC workspace (<= max_batch windows) and
+      // the alt-run buffers (<= max_batch blocks) fit
       int s1 = s0 + 1;
-      while (s1 < n_seg && s1 - s0 < seg_cap && first[s1 + 1] - first[s0] <= h->max_batch) ++s1;
+      while (s1 < n_seg && s1 - s0 < seg_cap && first[s1 + 1] - first[s0] <= h->max_batch &&
+             (long long)(s1 + 1 - s0) * blk_per_seg <= h->max_batch)
+        ++s1;
       const int w0 = first[s0], nw = first[s1] - first[s0];
       EXPECTO_REQUIRE(nw <= h->max_batch, "more windows in one segment than max_batch");
       const int ns = s1 - s0;
+      const long long nb = (long long)ns * n_ph;
+      // alt input patch of a layer from the ref input `ref` (ref_rows per block) and the
+      // previous alt run, then the layer's GEMM on it (same kernel, K order and weights)
+      auto alt_layer = [&](int l, const float* ref, int ref_rows, const float* dprev, int wprev, int nbk, int ib,
+                           int mult, int irp, int arows, int w, bool pool, float* dnext) -> int {
+        const int row16 = kConv[l].cin * eb / 16;
+        seg_delta_assemble<<<dim3(arows, ns * nbk), dim3(64), 0, st>>>(ref, ref_rows, dprev, wprev, h->seg_tab, nbk,
+                                                                      ib, mult, irp, arows, row16, h->DA);
+        int r = check_launch("seg_delta_assemble");
+        return r ? r : run_conv(h, l, h->DA, dnext, (long long)ns * nbk, arows, w, w, pool, st);
+      };
       // conv1 from codes: virtual rows = segments; rc mode mirrors inside the kernel
       if ((rc = run_conv1(h, nullptr, codes + (long long)s0 * code_stride, code_stride, ns,
                           is_rc ? EXPECTO_STRAND_RC : EXPECTO_STRAND_FWD, 0, ns, L, g.S1, st)))
         return rc;
-      // conv2 + pool1 (P -> Q), conv3 (Q -> P), conv4 unpooled (P -> Q)
+      if (pr) {
+        seg_delta_table<<<dim3((ns + 255) / 256), dim3(256), 0, st>>>(pr->var_pos, s0, ns, is_rc ? 1 : 0, gd, n_ph,
+                                                                     ph4, h->seg_tab);
+        if ((rc = check_launch("seg_delta_table"))) return rc;
+        seg_delta_codes<<<dim3((ns + 15) / 16), dim3(256), 0, st>>>(codes, code_stride, pr->alt_code, s0, ns,
+                                                                   is_rc ? 1 : 0, L, h->seg_tab, h->delta_codes);
+        if ((rc = check_launch("seg_delta_codes"))) return rc;
+        if ((rc = run_conv1(h, nullptr, h->delta_codes, 16, ns, EXPECTO_STRAND_FWD, 0, ns, kDA[1], kDW[1], st,
+                            h->D0)))
+          return rc;
+      }
+      // conv2 + pool1 (P -> Q), conv3 (Q -> P), conv4 unpooled (P -> Q); alt runs D0 <-> D1
       if ((rc = run_conv(h, 0, h->P, h->Q, ns, g.S1, g.P1, g.P1, true, st))) return rc;
+      if (pr && (rc = alt_layer(0, h->P, g.S1, h->D0, kDW[1], 1, 2, 4, 1, kDA[2], kDW[2], true, h->D1))) return rc;
       if ((rc = run_conv(h, 1, h->Q, h->P, ns, g.P1, g.T3, g.T3, false, st))) return rc;
+      if (pr && (rc = alt_layer(1, h->Q, g.P1, h->D1, kDW[2], 1, 3, 1, 2, kDA[3], kDW[3], false, h->D0))) return rc;
       if ((rc = run_conv(h, 2, h->P, h->Q, ns, g.T3, g.T4, g.T4, false, st))) return rc;
+      if (pr && (rc = alt_layer(2, h->P, g.T3, h->D0, kDW[3], 1, 4, 1, 3, kA4u, kW4u, false, h->D1))) return rc;
       {  // pool2 phases (Q -> P)
         LayerTimer lt(h, 3, st);
         dim3 grid(g.S5, ns * n_ph);
-        pool4_phases<<<grid, dim3(480), 0, st>>>(h->Q, ns, g.T4, g.T4, 480, n_ph,
-                                               make_int4(ph[0], ph[1], ph[2], ph[3]), g.S5, h->P, x3_act());
+        pool4_phases<<<grid, dim3(480), 0, st>>>(h->Q, ns, g.T4, g.T4, 480, n_ph, ph4, g.S5, h->P, x3_act());
         if ((rc = check_launch("pool4_phases"))) return rc;
+        if (pr) {
+          seg_delta_pool<<<dim3(kDW[4], (unsigned)nb), dim3(480), 0, st>>>(h->Q, g.T4, h->D1, n_ph, ph4, h->seg_tab,
+                                                                           x3_act(), h->D0);
+          if ((rc = check_launch("seg_delta_pool"))) return rc;
+        }
       }
       // conv5 (P -> Q), conv6 (Q -> P) over (segment, phase) blocks
-      if ((rc = run_conv(h, 3, h->P, h->Q, (long long)ns * n_ph, g.S5, g.T5, g.T5, false, st))) return rc;
-      if ((rc = run_conv(h, 4, h->Q, h->P, (long long)ns * n_ph, g.T5, g.T6, g.T6, false, st))) return rc;
+      if ((rc = run_conv(h, 3, h->P, h->Q, nb, g.S5, g.T5, g.T5, false, st))) return rc;
+      if (pr && (rc = alt_layer(3, h->P, g.S5, h->D0, kDW[4], n_ph, 9, 1, 5, kDA[5], kDW[5], false, h->D1)))
+        return rc;
+      if ((rc = run_conv(h, 4, h->Q, h->P, nb, g.T5, g.T6, g.T6, false, st))) return rc;
+      if (pr && (rc = alt_layer(4, h->Q, g.T5, h->D1, kDW[5], n_ph, 13, 1, 9, kDA[6], kDW[6], false, h->D0)))
+        return rc;
       if (nw > 0) {
         seg_a_rows<<<dim3((nw + 255) / 256), dim3(256), 0, st>>>(
             h->win_seg_d, h->win_off_d, win_row ? h->win_row_d : nullptr, w0, nw, s0, is_rc ? 1 : 0, L, n_ph,
-            make_int4(ph_idx[0], ph_idx[1], ph_idx[2], ph_idx[3]), g.T6, (long long)sd * n_win, h->a_rows,
+            make_int4(ph_idx[0], ph_idx[1], ph_idx[2], ph_idx[3]), g.T6, (long long)sd * strand_rows, h->a_rows,
             h->c_rows);
         if ((rc = check_launch("seg_a_rows"))) return rc;
         if ((rc = run_fc(h, h->P, h->a_rows, nw, y, st, h->c_rows))) return rc;
+        if (pr) {  // alt conv6 blocks into Q (conv5 rows are dead), same row table
+          seg_alt_blocks<<<dim3(g.T6, (unsigned)nb), dim3(64), 0, st>>>(h->P, h->D0, n_ph, g.T6, h->seg_tab,
+                                                                       640 * eb / 16, h->Q);
+          if ((rc = check_launch("seg_alt_blocks"))) return rc;
+          if ((rc = run_fc(h, h->Q, h->a_rows, nw, pr->y_alt, st, h->c_rows))) return rc;
+        }
       }
       s0 = s1;
     }
   }
   return EXPECTO_OK;
 }
-// Trunk (conv1..conv6) of nseg segments of length L with pool2 phase 0 only (segment
-// starts 16-aligned relative to the windows they stand in for); conv6 rows end in `pbuf`.
-int run_trunk_phase0(expecto_beluga* h, const uint8_t* codes, long long stride, int nseg, int L, float* pbuf,
-                     float* qbuf, SegGeo& g, hipStream_t st) {
-  int rc;
-  g = seg_geo(L, 1);
-  if ((rc = run_conv1(h, nullptr, codes, stride, nseg, EXPECTO_STRAND_FWD, 0, nseg, L, g.S1, st, pbuf))) return rc;
-  if ((rc = run_conv(h, 0, pbuf, qbuf, nseg, g.S1, g.P1, g.P1, true, st))) return rc;
-  if ((rc = run_conv(h, 1, qbuf, pbuf, nseg, g.P1, g.T3, g.T3, false, st))) return rc;
-  if ((rc = run_conv(h, 2, pbuf, qbuf, nseg, g.T3, g.T4, g.T4, false, st))) return rc;
-  {
-    LayerTimer lt(h, 3, st);
-    pool4_phases<<<dim3(g.S5, nseg), dim3(480), 0, st>>>(qbuf, nseg, g.T4, g.T4, 480, 1, make_int4(0, 0, 0, 0),
-                                                         g.S5, pbuf, x3_act());
-    if ((rc = check_launch("pool4_phases"))) return rc;
-  }
-  if ((rc = run_conv(h, 3, pbuf, qbuf, nseg, g.S5, g.T5, g.T5, false, st))) return rc;
-  return run_conv(h, 4, qbuf, pbuf, nseg, g.T5, g.T6, g.T6, false, st);
-}
-
 int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int n, long long stride,
                   const int* var_pos, int mode, float* y_ref, float* y_alt, long long strand_stride, hipStream_t st) {
   g_precision = h->precision;
   const int strands = mode == EXPECTO_STRAND_BOTH ? 2 : 1;
-  if (!h->P2) {
-    const SegGeo g = seg_geo(kPatchLen, 1);
-    size_t pf = (size_t)h->max_batch * g.p_rows_floats + 16 * 640, qf = (size_t)h->max_batch * g.q_rows_floats + 16 * 640;
-    int rc;
-    if ((rc = dalloc(h, &h->P2, act_alloc(pf))) || (rc = dalloc(h, &h->Q2, act_alloc(qf)))) return rc;
-    float* pc = nullptr;
-    if ((rc = dalloc(h, &pc, ((size_t)h->max_batch * kPatchLen + 3) / 4))) return rc;
-    h->patch_codes = reinterpret_cast<uint8_t*>(pc);
-  }
-  const int nv_max = std::max(1, h->max_batch / strands);
   int rc;
+  if ((rc = ensure_delta(h))) return rc;
+  const int eb = x3_act() ? 6 : 4;   // bytes per activation element
+  const int nv_max = std::max(1, h->max_batch / strands);
   for (int v0 = 0; v0 < n; v0 += nv_max) {
     const int nv = std::min(nv_max, n - v0), R = strands * nv;
-    // ref windows: full per-window trunk, conv6 rows stay in Q
+    // conv1: ref windows (full) and the alt runs (15 codes -> 8 rows)
     if ((rc = run_conv1(h, nullptr, ref + (long long)v0 * stride, stride, nv, mode, 0, R, kLen, kS1, st))) return rc;
+    delta_codes<<<dim3((R + 15) / 16), dim3(256), 0, st>>>(alt, stride, nv, v0, var_pos, h->delta_codes, R);
+    if ((rc = check_launch("delta_codes"))) return rc;
+    if ((rc = run_conv1(h, nullptr, h->delta_codes, 16, R, EXPECTO_STRAND_FWD, 0, R, kDA[1], kDW[1], st, h->D0)))
+      return rc;
     float* src = h->P;
     float* dst = h->Q;
-    for (int l = 0; l < 5; ++l) {
+    float* dprev = h->D0;
+    float* dnext = h->D1;
+    for (int l = 0; l < 5; ++l) {   // conv2..conv6 (layer index l+2 in the delta tables)
       const ConvGeo& g = kConv[l];
+      const int L = l + 2;
       if ((rc = run_conv(h, l, src, dst, R, g.s_in, g.t_valid, g.s_out, g.pool != 0, st))) return rc;
+      const int row16 = g.cin * eb / 16;
+      delta_assemble<<<dim3(kDA[L], R), dim3(64), 0, st>>>(src, g.s_in, dprev, L, row16, nv, v0, var_pos, h->DA);
+      if ((rc = check_launch("delta_assemble"))) return rc;
+      if ((rc = run_conv(h, l, h->DA, dnext, R, kDA[L], kDW[L], kDW[L], g.pool != 0, st))) return rc;
       std::swap(src, dst);
+      std::swap(dprev, dnext);
     }
-    float* act6 = src;
+    float* act6 = src;   // ref conv6 rows; dprev = the alt runs' conv6 rows
     pair_rows<<<dim3((R + 255) / 256), dim3(256), 0, st>>>(h->c_rows, R, nv, v0, strand_stride);
     if ((rc = check_launch("pair_rows"))) return rc;
     if ((rc = run_fc(h, act6, nullptr, R, y_ref, st, h->c_rows))) return rc;
-    // alt windows: 600-bp patch trunk, patch rows spliced into the ref conv6 rows
-    pair_patch_codes<<<dim3((kPatchLen + 255) / 256, R), dim3(256), 0, st>>>(alt + 0, stride, nv, v0, var_pos,
-                                                                            h->patch_codes);
-    if ((rc = check_launch("pair_patch_codes"))) return rc;
-    SegGeo pg;
-    if ((rc = run_trunk_phase0(h, h->patch_codes, kPatchLen, R, kPatchLen, h->P2, h->Q2, pg, st))) return rc;
-    EXPECTO_REQUIRE(pg.T6 == kPatchRows, "patch geometry");
-    pair_patch_apply<<<dim3(kPatchRows, R), dim3(256), 0, st>>>(h->P2, act6, nv, v0, var_pos,
-                                                                x3_act() ? 240 : 160);
+    pair_patch_apply<<<dim3(kDW[6], R), dim3(64), 0, st>>>(dprev, act6, nv, v0, var_pos, 640 * eb / 16);
     if ((rc = check_launch("pair_patch_apply"))) return rc;
     if ((rc = run_fc(h, act6, nullptr, R, y_alt, st, h->c_rows))) return rc;
   }
@@ -777,7 +991,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   }
   if ((rc = check_launch("repack"))) return fail(rc);
   const size_t pf = p_floats(max_batch), qf = q_floats(max_batch);
-  const size_t partf = (size_t)kFcSplits[5] * max_batch * kHidLd;
+  const size_t partf = (size_t)kFcSplits * max_batch * kHidLd;
   if ((rc = dalloc(h, &h->P, act_alloc(pf))) || (rc = dalloc(h, &h->Q, act_alloc(qf))) ||
       (rc = dalloc(h, &h->part, partf)) || (rc = dalloc(h, &h->h1, act_alloc((size_t)max_batch * kHidLd))))
     return fail(rc);
@@ -852,6 +1066,24 @@ int expecto_beluga_forward_segments(expecto_beluga_t h, const uint8_t* codes, in
   EXPECTO_HIP_CHECK(hipSetDevice(h->device));
   return forward_segments(h, codes, n_seg, seg_len, code_stride, strand_mode, win_seg, win_off, win_row, n_win, y,
                           as_stream(stream));
+}
+
+int expecto_beluga_forward_segment_pairs(expecto_beluga_t h, const uint8_t* codes, const int* var_pos,
+                                         const uint8_t* alt_code, int n_seg, int seg_len, long long code_stride,
+                                         int strand_mode, const int* win_seg, const int* win_off, const int* win_row,
+                                         int n_win, float* y_ref, float* y_alt, long long strand_stride,
+                                         void* stream) {
+  EXPECTO_REQUIRE(h != nullptr, "null handle");
+  EXPECTO_REQUIRE(n_seg >= 0 && n_win >= 0, "negative count");
+  EXPECTO_REQUIRE(strand_mode >= 0 && strand_mode <= 2, "bad strand mode");
+  if (n_win == 0 || n_seg == 0) return EXPECTO_OK;
+  EXPECTO_REQUIRE(codes && var_pos && alt_code && y_ref && y_alt && win_seg && win_off, "null argument");
+  EXPECTO_REQUIRE(code_stride >= seg_len, "code_stride < seg_len");
+  EXPECTO_REQUIRE(strand_mode != EXPECTO_STRAND_BOTH || strand_stride >= n_win, "strand_stride < n_win");
+  EXPECTO_HIP_CHECK(hipSetDevice(h->device));
+  const SegPairs pr{var_pos, alt_code, y_alt, strand_stride};
+  return forward_segments(h, codes, n_seg, seg_len, code_stride, strand_mode, win_seg, win_off, win_row, n_win,
+                          y_ref, as_stream(stream), &pr);
 }
 
 int expecto_beluga_forward_pairs(expecto_beluga_t h, const uint8_t* ref_codes, const uint8_t* alt_codes, int n,

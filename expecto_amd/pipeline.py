@@ -88,9 +88,11 @@ def gather_segments(lib, dg, start: torch.Tensor, seg_len: int, splice_pos=None,
 class VariantPipeline:
     """Holds the device genome + model engine; computes shift sweeps for variant batches.
 
-    SNVs go through the segment path: per (allele, variant) ONE sequence covering every
-    shift's window (length 2000 + max_shift - min_shift), so the conv trunk is computed once
-    per sequence instead of once per shift (outputs bit-identical to the per-window path).
+    SNVs go through the segment path: per variant ONE ref sequence covering every shift's
+    window (length 2000 + max_shift - min_shift), so the conv trunk is computed once per
+    sequence instead of once per shift, and the alt allele recomputes only the rows the SNV
+    changes at each layer (use_pairs); single-shift runs use the per-window pair path.
+    Outputs are bit-identical to the per-window forward of every window.
     Indels/MNPs, whose windows are length-changing splices, use the per-window path with
     host-built codes; shift lists that are not 4-aligned use per-window device windows."""
 
@@ -124,17 +126,32 @@ class VariantPipeline:
         lo_s, hi_s = min(shifts), max(shifts)
         if ns and S > 1 and self.use_segments and all((x - lo_s) % 4 == 0 for x in shifts):
             L = 2000 + hi_s - lo_s
-            # segment a*ns + v; window (a, v, j) at offset shifts[j] - lo_s -> row (a*S + j)*ns + v
-            a_i, v_i, j_i = np.meshgrid(np.arange(2), np.arange(ns), np.arange(S), indexing="ij")
-            prep["seg"] = {
-                "L": L,
-                "start": torch.from_numpy(np.concatenate([off[snv_idx], off[snv_idx]]) + lo_s - 999).to(dev),
-                "splice_pos": torch.full((2 * ns,), 999 - lo_s, dtype=torch.int32, device=dev),
-                "splice_code": torch.from_numpy(np.concatenate([rc, ac])).to(dev),
-                "win_seg": (a_i * ns + v_i).ravel().astype(np.int32),
-                "win_off": (np.asarray(shifts)[j_i.ravel()] - lo_s).astype(np.int32),
-                "win_row": ((a_i * S + j_i) * ns + v_i).ravel().astype(np.int32),
-            }
+            if self.use_pairs:
+                # ref segment v; window (v, j) at offset shifts[j] - lo_s -> row j*ns + v of each
+                # allele block; the alt segment is the ref one with the alt base at 999 - lo_s
+                v_i, j_i = np.meshgrid(np.arange(ns), np.arange(S), indexing="ij")
+                prep["seg"] = {
+                    "L": L, "pairs": True,
+                    "start": torch.from_numpy(off[snv_idx] + lo_s - 999).to(dev),
+                    "splice_pos": torch.full((ns,), 999 - lo_s, dtype=torch.int32, device=dev),
+                    "splice_code": torch.from_numpy(rc).to(dev),
+                    "alt_code": torch.from_numpy(ac).to(dev),
+                    "win_seg": v_i.ravel().astype(np.int32),
+                    "win_off": (np.asarray(shifts)[j_i.ravel()] - lo_s).astype(np.int32),
+                    "win_row": (j_i * ns + v_i).ravel().astype(np.int32),
+                }
+            else:
+                # segment a*ns + v; window (a, v, j) at offset shifts[j] - lo_s -> row (a*S + j)*ns + v
+                a_i, v_i, j_i = np.meshgrid(np.arange(2), np.arange(ns), np.arange(S), indexing="ij")
+                prep["seg"] = {
+                    "L": L, "pairs": False,
+                    "start": torch.from_numpy(np.concatenate([off[snv_idx], off[snv_idx]]) + lo_s - 999).to(dev),
+                    "splice_pos": torch.full((2 * ns,), 999 - lo_s, dtype=torch.int32, device=dev),
+                    "splice_code": torch.from_numpy(np.concatenate([rc, ac])).to(dev),
+                    "win_seg": (a_i * ns + v_i).ravel().astype(np.int32),
+                    "win_off": (np.asarray(shifts)[j_i.ravel()] - lo_s).astype(np.int32),
+                    "win_row": ((a_i * S + j_i) * ns + v_i).ravel().astype(np.int32),
+                }
         elif ns:
             prep["win"] = {"off": torch.from_numpy(off[snv_idx]).to(dev), "rc": torch.from_numpy(rc).to(dev),
                            "ac": torch.from_numpy(ac).to(dev),
@@ -194,8 +211,14 @@ class VariantPipeline:
             if seg is not None:
                 scodes = gather_segments(self.lib, self.dg, seg["start"], seg["L"], seg["splice_pos"],
                                          seg["splice_code"])
-                self.engine.forward_segments(scodes, seg["L"], seg["win_seg"], seg["win_off"], seg["win_row"],
-                                             _lib.STRAND_BOTH, out=y.view(4 * S * ns, 2002))
+                if seg["pairs"]:
+                    yf = y.view(4 * S * ns, 2002)
+                    self.engine.forward_segment_pairs(scodes, seg["L"], seg["splice_pos"], seg["alt_code"],
+                                                      seg["win_seg"], seg["win_off"], seg["win_row"], yf[0:],
+                                                      yf[S * ns:], 2 * S * ns, _lib.STRAND_BOTH)
+                else:
+                    self.engine.forward_segments(scodes, seg["L"], seg["win_seg"], seg["win_off"], seg["win_row"],
+                                                 _lib.STRAND_BOTH, out=y.view(4 * S * ns, 2002))
             elif self.use_pairs:
                 # alt-cone reuse per shift: the alt window recomputes only the SNV's cone
                 codes = self._snv_window_codes(prep)

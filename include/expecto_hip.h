@@ -114,15 +114,31 @@ int expecto_gather_segments(const uint8_t* genome, long long genome_len, const l
 
 /* SNV ref/alt window pairs with alt-cone reuse: ref_codes/alt_codes are n windows each
  * (2000 codes at + v*code_stride) that differ at most at window index var_pos[v] (DEVICE array).
- * The ref windows run the full forward; each alt window reuses the ref conv6 rows outside the
- * SNV's receptive-field cone (<= 20 of 106 rows, recomputed from a 616-bp patch), so the alt
- * trunk costs ~30 % of a window -- outputs are bit-identical to the full alt forward.
+ * The ref windows run the full forward; each alt window recomputes, layer by layer, only the
+ * rows the SNV changes (conv1 8, pool1 5, conv3 12, pool2 6, conv5 13, conv6 20 rows) from
+ * input patches assembled out of the ref activations, so the alt trunk costs ~6 % of a window
+ * -- outputs are bit-identical to the full alt forward.
  * strand_mode FWD (rows: fwd) or BOTH (fwd and reverse complement).  Output row of (strand s,
  * variant v) is s*strand_stride + v in y_ref and in y_alt (chromatin.py:262-281 row order
  * when strand_stride = n). */
 int expecto_beluga_forward_pairs(expecto_beluga_t h, const uint8_t* ref_codes, const uint8_t* alt_codes, int n,
                                  long long code_stride, const int* var_pos, int strand_mode, float* y_ref,
                                  float* y_alt, long long strand_stride, void* stream);
+
+/* SNV shift sweeps on the segment path with alt reuse: segment i (as in
+ * expecto_beluga_forward_segments) is the REF sequence; its alt sequence has code
+ * alt_code[i] at index var_pos[i] (DEVICE arrays, one per segment).  Both alleles' windows are
+ * computed (same win_* tables): the ref trunk once per segment, and for the alt only the rows
+ * the SNV changes at each layer (conv1 8, pool1 5, conv3 12, conv4 19, pool2 6 per phase,
+ * conv5 13, conv6 20), assembled from the ref activations -- bit-identical to the full alt
+ * forward.  Window w of strand s lands in row s*strand_stride + win_row[w] of y_ref and of
+ * y_alt.  Replaces the ref/alt forwards of chromatin.py:243-281 for --maxshift sweeps (and
+ * the 200-shift eQTL variant scoring of geuvadis_sed_for_top_eqtls.py:61-98). */
+int expecto_beluga_forward_segment_pairs(expecto_beluga_t h, const uint8_t* codes, const int* var_pos,
+                                         const uint8_t* alt_code, int n_seg, int seg_len, long long code_stride,
+                                         int strand_mode, const int* win_seg, const int* win_off, const int* win_row,
+                                         int n_win, float* y_ref, float* y_alt, long long strand_stride,
+                                         void* stream);
 
 int expecto_beluga_set_precision(expecto_beluga_t h, int precision);
 int expecto_beluga_get_precision(expecto_beluga_t h);

@@ -115,14 +115,16 @@ def test_segment_path_is_bitwise_equal_to_per_window_variants(precision):
     vs = VariantSet([s[0] for s in snv], np.array([s[1] for s in snv]), [s[2] for s in snv], [s[3] for s in snv])
     eng = _engine(precision)
     dg = DeviceGenome(fa)
+    full = VariantPipeline(eng, fa, dg, use_segments=False, use_pairs=False)
     for shifts in (shift_order(800), shift_order(200), [0, 400, -400]):
-        seg = VariantPipeline(eng, fa, dg, use_segments=True)
-        win = VariantPipeline(eng, fa, dg, use_segments=False)
-        ps = seg.prepare(vs, shifts)
-        assert ps["seg"] is not None
-        a = seg.predict(ps)
-        b = win.predict(vs, shifts)
-        assert torch.equal(a, b), f"segment path differs for shifts {shifts}: {float((a - b).abs().max())}"
+        b = full.predict(vs, shifts)
+        for pairs in (True, False):
+            seg = VariantPipeline(eng, fa, dg, use_segments=True, use_pairs=pairs)
+            ps = seg.prepare(vs, shifts)
+            assert ps["seg"] is not None and ps["seg"]["pairs"] == pairs
+            a = seg.predict(ps)
+            assert torch.equal(a, b), f"segment path (pairs={pairs}) differs for shifts {shifts}: " \
+                                      f"{float((a - b).abs().max())}"
 
 
 def test_segment_path_mixed_snv_and_indel_batch():
@@ -142,7 +144,7 @@ def test_segment_path_mixed_snv_and_indel_batch():
     eng = _engine()
     dg = DeviceGenome(fa)
     a = VariantPipeline(eng, fa, dg, use_segments=True).predict(vs, shift_order(400))
-    b = VariantPipeline(eng, fa, dg, use_segments=False).predict(vs, shift_order(400))
+    b = VariantPipeline(eng, fa, dg, use_segments=False, use_pairs=False).predict(vs, shift_order(400))
     assert torch.equal(a, b)
 
 
@@ -198,3 +200,33 @@ def test_variant_pipeline_pairs_equal_per_window():
     a = VariantPipeline(eng, fa, dg, use_pairs=True).predict(vs, [0])
     b = VariantPipeline(eng, fa, dg, use_pairs=False).predict(vs, [0])
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("precision", ["bf16x6", "fp32"])
+def test_segment_pairs_alt_runs_are_bitwise_equal(precision):
+    """forward_segment_pairs == full forwards of every ref and alt window, for SNVs at the
+    segment edges and in the middle, windows at the first/last offsets, both strands."""
+    import torch
+    eng = _engine(precision)
+    rng = np.random.default_rng(11)
+    L = 2000 + 1600
+    q = np.array([0, 3, 7, 500, 1234, 1799, 1800, 2001, 3000, L - 9, L - 2, L - 1], np.int32)
+    n = q.size
+    ref = torch.from_numpy(rng.integers(0, 5, (n, L)).astype(np.uint8)).cuda()
+    alt_code = torch.from_numpy(((ref.cpu().numpy()[np.arange(n), q] + 1 + rng.integers(0, 3, n)) % 4)
+                                .astype(np.uint8)).cuda()
+    alt = ref.clone()
+    alt[torch.arange(n), torch.from_numpy(q).long()] = alt_code
+    offs = np.array([0, 4, 200, 796, 800, 1000, 1596, 1600], np.int32)
+    S = offs.size
+    v_i, j_i = np.meshgrid(np.arange(n), np.arange(S), indexing="ij")
+    win_seg, win_off, win_row = v_i.ravel().astype(np.int32), offs[j_i.ravel()], (j_i * n + v_i).ravel().astype(np.int32)
+    y = torch.full((2, 2, S * n, 2002), float("nan"), device="cuda")
+    yf = y.view(4 * S * n, 2002)
+    eng.forward_segment_pairs(ref, L, torch.from_numpy(q).cuda(), alt_code, win_seg, win_off, win_row, yf[0:],
+                              yf[S * n:], 2 * S * n)
+    for a, src in enumerate((ref, alt)):
+        wins = torch.stack([src[:, o:o + 2000] for o in offs], 0).reshape(S * n, 2000).contiguous()  # row j*n + v
+        want = eng.forward_codes(wins, 2).view(2, S * n, 2002)
+        d = (y[:, a] - want).abs().amax(-1).view(2, S, n).cpu().numpy()
+        assert (d == 0).all(), f"allele {a}: strand x offset x variant max|diff| {d} (q={q}, offsets={offs})"
