@@ -53,7 +53,7 @@ def kernel_name(layer: str, precision: str) -> str:
     if layer not in GEMM_LAYER_EPI:
         return {"conv1": "beluga_conv1", "fc1_reduce": "fc1_reduce"}[layer]
     l, e = GEMM_LAYER_EPI[layer]
-    return f"beluga_gemm_x6p<{l}, {e}, 0>" if precision == "bf16x6" else f"beluga_gemm<{l}, {e}, 4, 2, 32, 1>"
+    return f"beluga_gemm_x6q<{l}, {e}, 0>" if precision == "bf16x6" else f"beluga_gemm<{l}, {e}, 4, 2, 32, 1>"
 WINDOW_MACS = sum(LAYER_MACS.values())
 
 
@@ -215,6 +215,7 @@ def main():
         "executed_fp32_tflops": 2.0 * exec_macs * world / el / 1e12,
         "roofline": roof,
         "layer_ms_per_step": {k: ms / args.steps for k, (ms, c, m) in layers.items()},
+        "layer_tflops": {k: 2.0 * m / (ms * 1e-3) / 1e12 for k, (ms, c, m) in layers.items() if ms > 0},
         "profile_key": key,
         "reuse": "alt-cone (SNV alt windows recompute <=20 of 106 conv6 rows; bit-identical)" if S == 1 else
                  "segments (trunk shared across shifts; bit-identical)",
@@ -229,6 +230,8 @@ def main():
         extras["cfg3_shift_sweep_800"] = {
             "variants_per_s": 400 * 2 / el3, "windows_per_variant": 36, "dense_windows_per_s": 400 * 36 * 2 / el3,
             "executed_fp32_tflops": 2.0 * sum(m for _, _, m in l3.values()) / el3 / 1e12,
+            "layer_ms_per_step": {k: ms / 2 for k, (ms, c, m) in l3.items()},
+            "layer_tflops": {k: 2.0 * m / (ms * 1e-3) / 1e12 for k, (ms, c, m) in l3.items() if ms > 0},
             "roofline": roofline(l3, eng.precision)}
         # the metric's literal unit: a variant scored with 200 windows (+-20 kb, stride 200) x ref/alt x fwd/rc
         sh200 = list(range(-20000, 20000, 200))
@@ -238,6 +241,8 @@ def main():
         extras["variant_200_windows"] = {
             "variants_per_s": 24 * 2 / el2, "windows_per_variant": 800, "dense_windows_per_s": 24 * 800 * 2 / el2,
             "executed_fp32_tflops": 2.0 * sum(m for _, _, m in l2.values()) / el2 / 1e12,
+            "layer_ms_per_step": {k: ms / 2 for k, (ms, c, m) in l2.items()},
+            "layer_tflops": {k: 2.0 * m / (ms * 1e-3) / 1e12 for k, (ms, c, m) in l2.items() if ms > 0},
             "roofline": roofline(l2, eng.precision)}
         rec["extra_workloads"] = extras
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

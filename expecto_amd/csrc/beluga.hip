@@ -570,7 +570,7 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st) {
   EXPECTO_REQUIRE(a.m_tiles * gemm_bm() >= a.M, "gemm M tiles do not cover M");
   if (g_precision == EXPECTO_PRECISION_BF16X6) {
     EXPECTO_REQUIRE(a.Bp != nullptr && a.lda % GBK == 0 && a.ldb % GBK == 0, "bf16x6 GEMM needs planes, K % 32");
-    beluga_gemm_x6p<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
+    beluga_gemm_x6q<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
   } else
     beluga_gemm<LAYER, EPI, kWM, kMinBlocks, GBK, kPipe><<<dim3((unsigned)nblk), dim3(64 * kWM), 0, st>>>(a);
   return check_launch("beluga_gemm");

@@ -40,7 +40,7 @@ struct GemmArgs {
   long long split_stride;
   const long long* a_rows;  // optional: A row m starts at A + a_rows[m] (FC1 over segment windows)
   const long long* c_rows;  // optional: C row of M row m (non-pool epilogues; FC2 output order)
-  const void* Bp;           // x6p only: B as bf16 planes [Npad][K/32][3][32] (split_planes)
+  const void* Bp;           // bf16x6 GEMM: B as bf16 planes [Npad][K/32][3][32] (split_planes)
 };
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -418,26 +418,24 @@ __global__ __launch_bounds__(64 * WM, MINB * WM / 4) void beluga_gemm_x6(GemmArg
   gemm_epilogue<EPI>(p, acc, m0 + wave * 32, n0, ks, li, lh);
 }
 
-// ---- bf16x6 on pre-split planes with LDS-DMA staging ("x6p", the library's bf16x6 GEMM) ----
-// Same arithmetic and the same MFMA order per accumulator as beluga_gemm_x6 above, hence the
-// same bits (tools/gemm_bench checks it).  What changes is the data movement:
+// ---- bf16x6 on pre-split planes with LDS-DMA staging (the library's bf16x6 GEMM) ----------
+// The arithmetic of beluga_gemm_x6 above (exact 3-way split, the six products of combined
+// order <= 2 into one fp32 accumulator), with the data movement redesigned:
 //  * B (weights) is split once at handle creation into planes [n][k/32][3][32] (split_planes);
 //  * A (activations) is split once by the PRODUCING layer's epilogue into the same planes
-//    layout (store_act<true>); beluga_gemm_x6 re-split every Toeplitz element once per tap;
-//  * both tiles arrive by global_load_lds_dwordx4 (no VGPR round trip, no ds_write) into a
-//    double-buffered LDS ring, one raw barrier per 32-deep K block; each wave stages its own
-//    64 A rows, so it waits for them with its own counted vmcnt, not a barrier;
-//  * each wave owns 64 x 160 (2 x 5 accumulators, 160 AGPRs), four waves = 256 x 160, one
-//    workgroup per CU; B fragments are prefetched one 12-MFMA unit ahead and the LDS-DMA
-//    pieces are issued between units (sched_group_barrier-pinned).
+//    layout (store_act<true>); beluga_gemm_x6 re-splits every Toeplitz element once per tap;
+//  * both tiles arrive by LDS-DMA (buffer_load_dwordx4 ... lds: constant lane offsets in
+//    voffset, the stage offset in soffset) into a double-buffered LDS ring, one raw barrier
+//    per 32-deep K block; each wave stages its own 64 A rows, so it waits for them with its
+//    own counted vmcnt, not a barrier;
+//  * each wave owns 64 x 160 as 4 x 10 blocks of v_mfma_f32_16x16x32_bf16 (160 AGPRs), four
+//    waves = 256 x 160, one workgroup per CU; B fragments are prefetched one unit ahead and the
+//    LDS-DMA pieces are issued between units (sched_group_barrier-pinned).
 // Stage = A planes 48 KB + B planes 30 KB + 2 KB pad = 80 KB; two stages fill the CU's LDS.
 // Per wave and stage: 12 A pieces (its rows x 3 planes) + 8 B pieces (30 real + 2 dummies).
-// LDS-DMA writes lane-linear 1 KiB pieces (16 rows x 64 B), so conflict-free ds_read_b128
-// comes from an XOR swizzle on the per-lane SOURCE address, undone on the read:
-//   position = chunk ^ ((row >> 2) & 3)   (the 16 lanes of one ds_read_b128 lane group read
-//                                          16 distinct rows mod 16 at one chunk)
-// tools/gemm_bench, conv2 shape, 1000 windows: 228 fp32-equivalent TF/s vs 190 for
-// beluga_gemm_x6 and 140 for the fp32 MFMA kernel.
+// tools/gemm_bench, conv2 shape, 1000 windows (fp32-equivalent TF/s): 284 here, vs 234 for
+// the same data path on 32x32x16 MFMAs (the 16x16x32 form holds a higher clock under load,
+// MI355X_MICROARCH.md DVFS item 7), 197 for beluga_gemm_x6 and 140 for the fp32 kernel.
 constexpr int X6P_BM = 256;
 constexpr int X6P_B_PLANE = GBN * 64;                     // 10 KB
 constexpr int X6P_A_PLANE = X6P_BM * 64;                  // 16 KB
@@ -453,8 +451,58 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
 
 // TM: timing-only probes for tools/gemm_bench (wrong results): 2 = no LDS-DMA in the loop,
 // 4 = no barrier in the loop, 8 = LDS-DMA always from stage 0's (L2-hot) addresses.
+// 16x16x32 lane layout: A/B lane l holds row/col (l & 15), k = 8*(l >> 4)..+7; C lane l
+// holds col (l & 15), rows 4*(l >> 4)..+3.  The 16 lanes of one ds_read_b128 lane group then
+// read mixed chunks, so LDS-DMA pieces (lane-linear 1 KiB = 16 rows x 64 B) are placed with an
+// XOR swizzle on the SOURCE offset, undone on the read: position = chunk ^ (-(row >> 2) & 3).
+typedef float floatx4v __attribute__((ext_vector_type(4)));
+
+template <int EPI, bool X3>
+__device__ __forceinline__ void gemm_epilogue16(const GemmArgs& p, const floatx4v (&acc)[4][10], long long mw, int n0,
+                                                int ks, int lane) {
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int nb = 0; nb < 10; ++nb) {
+    const int n = n0 + nb * 16 + fr;
+    if (n >= p.n_store) continue;
+    const float bn = (EPI == EPI_PARTIAL) ? 0.f : p.bias[n];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      const long long m4 = mw + mb * 16 + 4 * fq;   // first of this lane's 4 rows (multiple of 4)
+      if (EPI == EPI_PARTIAL) {
+        float* cp = p.C + (long long)ks * p.split_stride + n;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (m4 + j < p.M) cp[(m4 + j) * p.ldc] = acc[mb][nb][j];
+      } else if (EPI == EPI_RELU_POOL4) {
+        if (m4 >= p.M) continue;
+        const long long w = m4 / p.s_in;
+        const int tp = (int)(m4 - w * p.s_in) >> 2;
+        if (tp >= p.t_valid) continue;
+        const float mx = fmaxf(fmaxf(acc[mb][nb][0], acc[mb][nb][1]), fmaxf(acc[mb][nb][2], acc[mb][nb][3]));
+        store_act<X3>(p.C, w * p.s_out + tp, p.ldc, n, fmaxf(mx + bn, 0.f));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const long long m = m4 + j;
+          if (m >= p.M) continue;
+          const long long w = m / p.s_in;
+          const int tpos = (int)(m - w * p.s_in);
+          if (tpos >= p.t_valid) continue;
+          const float v = acc[mb][nb][j] + bn;
+          const long long orow = p.c_rows ? p.c_rows[m] : (w * p.s_out + tpos);
+          if (EPI == EPI_SIGMOID)
+            p.C[orow * p.ldc + n] = 1.0f / (1.0f + expf(-v));
+          else
+            store_act<X3>(p.C, orow, p.ldc, n, fmaxf(v, 0.f));
+        }
+      }
+    }
+  }
+}
+
 template <int LAYER, int EPI, int TM = 0>
-__global__ __launch_bounds__(256, 1) void beluga_gemm_x6p(GemmArgs p) {
+__global__ __launch_bounds__(256, 1) void beluga_gemm_x6q(GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * X6P_STAGE];
 
   const unsigned nblk = gridDim.x, bid = blockIdx.x;
@@ -473,97 +521,120 @@ __global__ __launch_bounds__(256, 1) void beluga_gemm_x6p(GemmArgs p) {
     mt = rest % p.m_tiles;
     ks = (int)(rest / p.m_tiles);
   }
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: LDS bases stay scalar
   const long long m0 = mt * X6P_BM;
   const int n0 = nt * GBN;
   const int kb_total = (int)(p.ldb / GBK);
   const int gs0 = ks * (p.kper / GBK);
-  const long long lda_kb = p.lda / GBK;            // K blocks per A row
-
-  // A pieces: wave w stages its own rows 64w .. 64w+63: 4 pieces (16 rows x 64 B) per plane
-  const __bf16* Ap = (const __bf16*)p.A;
-  const __bf16* asrc[4];
+  const long long lda_kb = p.lda / GBK;
+  auto swz = [](int r) { return (-(r >> 2)) & 3; };
+  // Sources = uniform 64-bit base + constant 32-bit lane offset (global_load_lds saddr form:
+  // a stage only moves the scalar base).  FC1's row gather (a_rows) keeps 64-bit lane addresses.
+  constexpr bool kGather = (LAYER == 7);
+  const char* Ab = (const char*)p.A + (kGather ? 0 : m0 * lda_kb * 192);
+  unsigned aoff[4];
+  const char* aptr[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int r = wave * 64 + j * 16 + (lane >> 2);
     long long m = m0 + r;
     if (m > p.M - 1) m = p.M - 1;
-    const int c = (lane & 3) ^ ((r >> 2) & 3);
-    asrc[j] = Ap + (p.a_rows ? p.a_rows[m] / GBK : m * lda_kb) * 96 + 8 * c;
+    const int c = (lane & 3) ^ swz(r);
+    if (kGather) {
+      aptr[j] = (const char*)p.A + (p.a_rows ? p.a_rows[m] / GBK : m * lda_kb) * 192 + 16 * c;
+      aoff[j] = 0;
+    } else {
+      aptr[j] = nullptr;
+      aoff[j] = (unsigned)((m - m0) * lda_kb * 192 + 16 * c);
+    }
   }
-  const __bf16* bsrc[8];
-  const __bf16* Bp = (const __bf16*)p.Bp;
+  const char* Bb = (const char*)p.Bp + ((long long)n0 * kb_total + gs0) * 192;
+  unsigned boff[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int g = min(wave + 4 * j, 29);
     const int pl = g / 10, r = 16 * (g % 10) + (lane >> 2);
-    const int c = (lane & 3) ^ ((r >> 2) & 3);
-    bsrc[j] = Bp + ((long long)(n0 + r) * kb_total + gs0) * 96 + pl * 32 + 8 * c;
+    const int c = (lane & 3) ^ swz(r);
+    boff[j] = (unsigned)((long long)r * kb_total * 192 + pl * 64 + 16 * c);
   }
-  // A piece i (0..11) = plane i / 4, row group i % 4
+  // buffer_load ... lds: 128-bit resource from uniform values, the constant lane offset in
+  // voffset and the stage offset in soffset (no per-stage vector address arithmetic)
+  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, 0x7fffffff, 0x00020000);
   auto issue_a = [&](int s, int buf, int i0, int ni) {
     if constexpr ((TM & 8) != 0) s = 0;
     const int gs = gs0 + s;
     const int chunk = gs / p.taps, tap = gs - chunk * p.taps;
-    const long long ao = ((long long)tap * lda_kb + chunk) * 96;
+    const long long ao = ((long long)tap * lda_kb + chunk) * 192;
     char* base = smem + buf * X6P_STAGE;
-    for (int i = i0; i < i0 + ni; ++i)
-      glds16(asrc[i % 4] + ao + (i / 4) * 32, base + (i / 4) * X6P_A_PLANE + (wave * 4 + i % 4) * 1024);
+    for (int i = i0; i < i0 + ni; ++i) {
+      char* dst = base + (i / 4) * X6P_A_PLANE + (wave * 4 + i % 4) * 1024;
+      if (kGather)
+        glds16(aptr[i % 4] + ao + (i / 4) * 64, dst);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (lds_void*)dst, 16, aoff[i % 4] + (i / 4) * 64, (unsigned)ao, 0,
+                                                 0);
+    }
   };
   auto issue_b = [&](int s, int buf, int j0, int nj) {
     if constexpr ((TM & 8) != 0) s = 0;
     char* base = smem + buf * X6P_STAGE + X6P_A_BYTES;
-    for (int j = j0; j < j0 + nj; ++j) glds16(bsrc[j] + s * 96, base + (wave + 4 * j) * 1024);
+    for (int j = j0; j < j0 + nj; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + (wave + 4 * j) * 1024), 16, boff[j],
+                                               (unsigned)(s * 192), 0, 0);
   };
 
-  floatx16 acc[2][GTN];
+  floatx4v acc[4][10];
 #pragma unroll
-  for (int mb = 0; mb < 2; ++mb)
+  for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-    for (int t = 0; t < GTN; ++t)
+    for (int nb = 0; nb < 10; ++nb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[mb][t][r] = 0.f;
+      for (int r = 0; r < 4; ++r) acc[mb][nb][r] = 0.f;
 
-  const int sw = (li >> 2) & 3;                    // same 64-B-row swizzle for A and B planes
-  const int arow = (wave * 64 + li) * 64;
-  const int brow = X6P_A_BYTES + li * 64;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int coff = 16 * (fq ^ swz(fr));            // swizzled chunk of this lane (row & 15 = fr)
+  const int arow = (wave * 64 + fr) * 64 + coff;
+  const int brow = X6P_A_BYTES + fr * 64 + coff;
   const int nk = p.kper / GBK;
 
-  auto read_a = [&](const char* base, int kq, bf16x8 (&a)[2][3]) {
+  auto read_a = [&](const char* base, bf16x8 (&a)[4][3]) {
 #pragma unroll
-    for (int mb = 0; mb < 2; ++mb) {
-      const char* ar = base + arow + mb * 32 * 64 + 16 * ((2 * kq + lh) ^ sw);
+    for (int mb = 0; mb < 4; ++mb) {
+      const char* ar = base + arow + mb * 16 * 64;
       a[mb][0] = *(const bf16x8*)(ar);
       a[mb][1] = *(const bf16x8*)(ar + X6P_A_PLANE);
       a[mb][2] = *(const bf16x8*)(ar + 2 * X6P_A_PLANE);
     }
   };
-  auto read_b = [&](const char* base, int kq, int t, bf16x8 (&b)[3]) {
-    const char* br = base + brow + t * 32 * 64 + 16 * ((2 * kq + lh) ^ sw);
+  auto read_b = [&](const char* base, int nb, bf16x8 (&b)[3]) {
+    const char* br = base + brow + nb * 16 * 64;
     b[0] = *(const bf16x8*)(br);
     b[1] = *(const bf16x8*)(br + X6P_B_PLANE);
     b[2] = *(const bf16x8*)(br + 2 * X6P_B_PLANE);
   };
-  auto unit = [&](const bf16x8 (&a)[2][3], int t, const bf16x8 (&b)[3]) {
+  auto unit = [&](const bf16x8 (&a)[4][3], int nb, const bf16x8 (&b)[3]) {
 #pragma unroll
-    for (int mb = 0; mb < 2; ++mb) {
-      floatx16 c = acc[mb][t];
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][2], b[0], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][1], b[1], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][0], b[2], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][1], b[0], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][0], b[1], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mb][0], b[0], c, 0, 0, 0);
-      acc[mb][t] = c;
+    for (int mb = 0; mb < 4; ++mb) {
+      floatx4v c = acc[mb][nb];
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mb][2], b[0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mb][1], b[1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mb][0], b[2], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mb][1], b[0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mb][0], b[1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mb][0], b[0], c, 0, 0, 0);
+      acc[mb][nb] = c;
     }
   };
+  // 24 MFMAs (16 cycles each) per unit; up to 2 LDS-DMA pieces, 1 LDS read, 1 VALU per slot
   auto pin = [&](int nv) {
 #pragma unroll
-    for (int i = 0; i < 12; ++i) {
+    for (int i = 0; i < 24; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      if ((i & 1) == 0 && i < 2 * nv) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+      if ((i % 6) == 0 && i < 6 * nv) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      if ((i & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
     }
   };
 
@@ -572,8 +643,8 @@ __global__ __launch_bounds__(256, 1) void beluga_gemm_x6p(GemmArgs p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  bf16x8 as[2][2][3];  // [kq][mb][plane]
-  read_a(smem, 0, as[0]);
+  bf16x8 as[4][3];
+  read_a(smem, as);
   for (int s = 0; s < nk; ++s) {
     const int buf = s & 1;
     const int sn = (TM & 2) ? s : min(s + 1, nk - 1);
@@ -581,59 +652,31 @@ __global__ __launch_bounds__(256, 1) void beluga_gemm_x6p(GemmArgs p) {
     const char* nbase = smem + (buf ^ 1) * X6P_STAGE;
     const bool go = !(TM & 2);
     bf16x8 b0[3], b1[3];
-    read_b(base, 0, 0, b0);
-    read_a(base, 1, as[1]);
-    // kq = 0 on as[0]; stage s+1's 12 A pieces go out first, then its 8 B pieces
-    read_b(base, 0, 1, b1);
-    if (go) issue_a(sn, buf ^ 1, 0, 3);
-    unit(as[0], 0, b0);
-    pin(3);
-    read_b(base, 0, 2, b0);
-    if (go) issue_a(sn, buf ^ 1, 3, 3);
-    unit(as[0], 1, b1);
-    pin(3);
-    read_b(base, 0, 3, b1);
-    if (go) issue_a(sn, buf ^ 1, 6, 3);
-    unit(as[0], 2, b0);
-    pin(3);
-    read_b(base, 0, 4, b0);
-    if (go) issue_a(sn, buf ^ 1, 9, 3);
-    unit(as[0], 3, b1);
-    pin(3);
-    read_b(base, 1, 0, b1);
-    if (go) issue_b(sn, buf ^ 1, 0, 3);
-    unit(as[0], 4, b0);
-    pin(3);
-    read_b(base, 1, 1, b0);
-    if (go) issue_b(sn, buf ^ 1, 3, 3);
-    unit(as[1], 0, b1);
-    pin(3);
-    read_b(base, 1, 2, b1);
-    if (go) issue_b(sn, buf ^ 1, 6, 2);
-    unit(as[1], 1, b0);
-    pin(2);
-    // this wave's 12 A pieces of stage s+1 are older than its 8 B pieces: vmcnt(8)
+    read_b(base, 0, b0);
+#pragma unroll
+    for (int nb = 0; nb < 10; ++nb) {
+      // glds: 12 A pieces over units 0..5, 8 B pieces over units 6..9
+      if (go && nb < 6) issue_a(sn, buf ^ 1, 2 * nb, 2);
+      if (go && nb >= 6) issue_b(sn, buf ^ 1, 2 * (nb - 6), 2);
+      if (nb + 1 < 10) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
+      unit(as, nb, (nb & 1) ? b1 : b0);
+      pin(2);
+    }
+    // A of stage s+1 (this wave's 12 pieces, older than its 8 B pieces) replaces A(s) while
+    // the last unit's MFMAs drain
     if constexpr (!(TM & 2)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    read_b(base, 1, 3, b0);
-    unit(as[1], 2, b1);
-    pin(0);
-    read_a(nbase, 0, as[0]);
-    read_b(base, 1, 4, b1);
-    unit(as[1], 3, b0);
-    pin(0);
-    unit(as[1], 4, b1);
-    pin(0);
+    read_a(nbase, as);
     if constexpr (!(TM & 4)) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     }
     asm volatile("" ::: "memory");
   }
-#pragma unroll
-  for (int mb = 0; mb < 2; ++mb) gemm_epilogue<EPI, true>(p, acc[mb], m0 + wave * 64 + mb * 32, n0, ks, li, lh);
+  (void)fr;
+  gemm_epilogue16<EPI, true>(p, acc, m0 + wave * 64, n0, ks, lane);
 }
 
-// B planes for beluga_gemm_x6p from a K-contiguous fp32 B [rows][K] (K % 32 == 0).
+// B planes for beluga_gemm_x6q from a K-contiguous fp32 B [rows][K] (K % 32 == 0).
 __global__ void split_planes(const float* __restrict__ W, long long rows, int K, __bf16* __restrict__ Bp) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= rows * K / 4) return;

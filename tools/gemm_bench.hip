@@ -43,8 +43,8 @@ Variant mk6(const char* name) {
 }
 
 template <int L, int EPI, int TM = 0>
-Variant mk6p(const char* name) {
-  return {name, X6P_BM, [](const GemmArgs& a, unsigned nblk) { beluga_gemm_x6p<L, EPI, TM><<<nblk, 256>>>(a); }};
+Variant mk6q(const char* name) {
+  return {name, X6P_BM, [](const GemmArgs& a, unsigned nblk) { beluga_gemm_x6q<L, EPI, TM><<<nblk, 256>>>(a); }};
 }
 
 template <int L, int EPI, int WM, int MINB, int BK, int PIPE = 0>
@@ -83,7 +83,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&bias, npad * 4));
   const size_t csz = (size_t)nb * sh.s_out * sh.cout;
   CK(hipMalloc(&C0, csz * 4));
-  CK(hipMalloc(&C1, csz * 6));   // x6p writes bf16 planes (6 B per element)
+  CK(hipMalloc(&C1, csz * 6));   // x6q writes bf16 planes (6 B per element)
   fill(X, xa, 0.f, 1.f, 1);
   fill(W, (size_t)npad * K, -0.05f, 0.05f, 2);
   fill(bias, npad, -0.1f, 0.1f, 3);
@@ -99,12 +99,12 @@ int main(int argc, char** argv) {
   // variant 0 is the reference for the bitwise comparison: x6 and x6d must agree exactly
   if (sh.pool) {
     vs.push_back(mk6<2, EPI_RELU_POOL4, 4, 1>("x6_wm4_b1"));
-    vs.push_back(mk6p<2, EPI_RELU_POOL4>("x6p"));
-    vs.push_back(mk6p<2, EPI_RELU_POOL4, 2>("x6p_noglds"));
+    vs.push_back(mk6q<2, EPI_RELU_POOL4>("x6q"));
+    vs.push_back(mk6q<2, EPI_RELU_POOL4, 2>("x6q_noglds"));
     vs.push_back(mk<2, EPI_RELU_POOL4, 4, 2, 32, 1>("f32_pipe"));
   } else {
     vs.push_back(mk6<3, EPI_RELU, 4, 1>("x6_wm4_b1"));
-    vs.push_back(mk6p<3, EPI_RELU>("x6p"));
+    vs.push_back(mk6q<3, EPI_RELU>("x6q"));
     vs.push_back(mk<3, EPI_RELU, 4, 2, 32, 1>("f32_pipe"));
   }
   auto args_for = [&](int bm, float* C) {
@@ -125,7 +125,7 @@ int main(int argc, char** argv) {
       float* C = v == 0 ? C0 : C1;
       CK(hipMemset(C, 0, v == 0 ? csz * 4 : csz * 6));
       GemmArgs a = args_for(vs[v].bm, C);
-      if (vs[v].name.rfind("x6p", 0) == 0) a.A = (const float*)Xp;
+      if (vs[v].name.rfind("x6q", 0) == 0) a.A = (const float*)Xp;
       unsigned nblk = (unsigned)(a.m_tiles * a.n_tiles);
       vs[v].launch(a, nblk);  // warm
       CK(hipEventRecord(e0));
@@ -136,7 +136,7 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       times[v].push_back(ms);
       if (r == 0) {
-        if (vs[v].name.rfind("x6p", 0) == 0) {   // decode planes [row][cout/32][3][32]
+        if (vs[v].name.rfind("x6q", 0) == 0) {   // decode planes
           std::vector<uint16_t> pl(csz * 3);
           CK(hipMemcpy(pl.data(), C, csz * 6, hipMemcpyDeviceToHost));
           auto f = [](uint16_t b) { uint32_t u = (uint32_t)b << 16; float x; memcpy(&x, &u, 4); return x; };
