@@ -136,12 +136,13 @@ class BelugaEngine:
             _lib.stream_ptr(stream)), "forward_segments")
         return out
 
-    def forward_segment_pairs(self, codes: torch.Tensor, seg_len: int, var_pos: torch.Tensor, alt_code: torch.Tensor,
+    def forward_segment_pairs(self, codes: torch.Tensor, seg_len: int, var_pos, alt_code: torch.Tensor,
                               win_seg, win_off, win_row, y_ref: torch.Tensor, y_alt: torch.Tensor, strand_stride: int,
                               strand_mode: int = _lib.STRAND_BOTH, stream=None):
         """SNV sweeps on shared segments: ref windows from `codes` (uint8 [n_seg, >=seg_len]),
-        alt windows = the same offsets with alt_code[s] at var_pos[s] (int32 / uint8 device
-        tensors, one per segment); the alt trunk recomputes only the rows the SNV changes.
+        alt windows = the same offsets with alt_code[s] (uint8 device tensor) at var_pos[s]
+        (host ints, one per segment); the alt trunk recomputes only the rows the SNV changes
+        and alt windows not holding the SNV copy their ref row.
         Row (strand s, window w) is s*strand_stride + win_row[w] of y_ref / y_alt (device
         views starting at row 0; they may alias one larger tensor).  Bit-identical to full
         forwards of both alleles."""
@@ -150,15 +151,17 @@ class BelugaEngine:
         if codes.dtype != torch.uint8 or codes.dim() != 2 or codes.shape[1] < seg_len or codes.stride(1) != 1:
             raise RuntimeError("codes must be uint8 [n_seg, >=seg_len] with contiguous rows")
         n_seg = codes.shape[0]
-        if not (var_pos.is_cuda and alt_code.is_cuda) or var_pos.numel() != n_seg or alt_code.numel() != n_seg:
-            raise RuntimeError("var_pos / alt_code: one device entry per segment")
-        pos = var_pos.to(torch.int32).contiguous()
+        if isinstance(var_pos, torch.Tensor):
+            var_pos = var_pos.cpu().numpy()
+        pos = np.ascontiguousarray(var_pos, np.int32).reshape(-1)
+        if not alt_code.is_cuda or pos.size != n_seg or alt_code.numel() != n_seg:
+            raise RuntimeError("var_pos (host) / alt_code (device): one entry per segment")
         alt = alt_code.to(torch.uint8).contiguous()
         ws = np.ascontiguousarray(win_seg, np.int32)
         wo = np.ascontiguousarray(win_off, np.int32)
         wr = None if win_row is None else np.ascontiguousarray(win_row, np.int32)
         _lib.check(self.lib.expecto_beluga_forward_segment_pairs(
-            self.handle, _lib.dptr(codes), _lib.dptr(pos), _lib.dptr(alt), n_seg, int(seg_len), codes.stride(0),
+            self.handle, _lib.dptr(codes), pos.ctypes.data, _lib.dptr(alt), n_seg, int(seg_len), codes.stride(0),
             int(strand_mode), ws.ctypes.data, wo.ctypes.data, None if wr is None else wr.ctypes.data, int(ws.size),
             _lib.dptr(y_ref), _lib.dptr(y_alt), int(strand_stride), _lib.stream_ptr(stream)), "forward_segment_pairs")
 

@@ -150,13 +150,14 @@ __global__ void pool4_phases(const float* __restrict__ in, int n_seg, int s_in, 
 
 // FC1 row table of the windows of one segment chunk: window m of the chunk reads conv6
 // rows [off6, off6+106) of block (segment, pool2 phase).
+// (widx: optional list of window indices; row m then serves window widx[m].)
 __global__ void seg_a_rows(const int* __restrict__ win_seg, const int* __restrict__ win_off,
-                           const int* __restrict__ win_row, int w0, int m_count, int seg_base, int rc, int seg_len,
-                           int n_ph, int4 ph_idx, int s7, long long row_base, long long* __restrict__ a_rows,
-                           long long* __restrict__ c_rows) {
+                           const int* __restrict__ win_row, const int* __restrict__ widx, int w0, int m_count,
+                           int seg_base, int rc, int seg_len, int n_ph, int4 ph_idx, int s7, long long row_base,
+                           long long* __restrict__ a_rows, long long* __restrict__ c_rows) {
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= m_count) return;
-  const int w = w0 + m;
+  const int w = widx ? widx[m] : w0 + m;
   c_rows[m] = row_base + (win_row ? win_row[w] : w);
   const int o = rc ? seg_len - 2000 - win_off[w] : win_off[w];
   const int q = o >> 2, p = q & 3, off6 = (q - p) >> 2;
@@ -381,6 +382,14 @@ __global__ void seg_alt_blocks(const float* __restrict__ ref6, const float* __re
   for (int c = threadIdx.x; c < row16; c += blockDim.x) dst[c] = src[c];
 }
 
+// y_alt rows of windows whose alt sequence equals the ref one (the SNV lies outside them)
+__global__ void copy_rows(const float* __restrict__ src, float* __restrict__ dst, const int* __restrict__ widx,
+                          const int* __restrict__ win_row, long long row_base) {
+  const int w = widx[blockIdx.x];
+  const long long r = (row_base + (win_row ? win_row[w] : w)) * kNFeat;
+  for (int i = threadIdx.x; i < kNFeat; i += blockDim.x) dst[r + i] = src[r + i];
+}
+
 __global__ void pair_rows(long long* __restrict__ c_rows, int M, int nv, int v0, long long strand_stride) {
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m < M) c_rows[m] = (long long)(m / nv) * strand_stride + v0 + m % nv;
@@ -466,6 +475,10 @@ struct expecto_beluga {
   long long* a_rows = nullptr;  // FC1 row table (segment path), max_batch entries
   long long* c_rows = nullptr;  // FC2 output-row table (segment path), max_batch entries
   int* win_seg_d = nullptr;     // window tables of the current segment call
+  int* alt_w_d = nullptr;       //   segment pairs: windows holding the SNV / the others
+  int* copy_w_d = nullptr;
+  int* seg_var_d = nullptr;     //   segment pairs: SNV index per segment
+  int seg_var_cap = 0;
   int* win_off_d = nullptr;
   int* win_row_d = nullptr;
   float* DA = nullptr;           // alt-delta buffers (pair path), lazily allocated:
@@ -752,8 +765,10 @@ SegGeo seg_geo(int L, int n_ph) {
   return g;
 }
 
-// Segment pairs: the alt segment s is segment s with code alt_code[s] at var_pos[s] (DEVICE
-// arrays); its windows (the same offsets) go to y_alt, computed through per-layer alt runs.
+// Segment pairs: the alt segment s is segment s with code alt_code[s] (DEVICE) at var_pos[s]
+// (HOST); its windows (the same offsets) go to y_alt.  Windows that hold the SNV get their
+// alt trunk through per-layer alt runs and their own FC; the others equal their ref window
+// and their rows are copied.
 struct SegPairs {
   const int* var_pos;
   const uint8_t* alt_code;
@@ -793,15 +808,36 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
   for (int w = n_win - 1; w >= 0; --w) first[win_seg[w]] = w;
   for (int sg = n_seg - 1; sg >= 0; --sg) first[sg] = std::min(first[sg], first[sg + 1]);
   if (n_win > h->win_cap) {
-    if (h->win_seg_d) EXPECTO_HIP_CHECK(hipFree(h->win_seg_d));
-    if (h->win_off_d) EXPECTO_HIP_CHECK(hipFree(h->win_off_d));
-    if (h->win_row_d) EXPECTO_HIP_CHECK(hipFree(h->win_row_d));
-    h->win_seg_d = h->win_off_d = h->win_row_d = nullptr;
+    for (int** b : {&h->win_seg_d, &h->win_off_d, &h->win_row_d, &h->alt_w_d, &h->copy_w_d}) {
+      if (*b) EXPECTO_HIP_CHECK(hipFree(*b));
+      *b = nullptr;
+    }
     h->win_cap = 0;
-    EXPECTO_HIP_CHECK(hipMalloc(&h->win_seg_d, n_win * sizeof(int)));
-    EXPECTO_HIP_CHECK(hipMalloc(&h->win_off_d, n_win * sizeof(int)));
-    EXPECTO_HIP_CHECK(hipMalloc(&h->win_row_d, n_win * sizeof(int)));
+    for (int** b : {&h->win_seg_d, &h->win_off_d, &h->win_row_d, &h->alt_w_d, &h->copy_w_d})
+      EXPECTO_HIP_CHECK(hipMalloc(b, n_win * sizeof(int)));
     h->win_cap = n_win;
+  }
+  std::vector<int> alt_w, copy_w;
+  if (pr) {
+    for (int sg = 0; sg < n_seg; ++sg)
+      EXPECTO_REQUIRE(pr->var_pos[sg] >= 0 && pr->var_pos[sg] < L, "variant position outside its segment");
+    for (int w = 0; w < n_win; ++w) {
+      const int q = pr->var_pos[win_seg[w]];
+      (win_off[w] <= q && q < win_off[w] + kLen ? alt_w : copy_w).push_back(w);
+    }
+    if (n_seg > h->seg_var_cap) {
+      if (h->seg_var_d) EXPECTO_HIP_CHECK(hipFree(h->seg_var_d));
+      h->seg_var_d = nullptr;
+      h->seg_var_cap = 0;
+      EXPECTO_HIP_CHECK(hipMalloc(&h->seg_var_d, n_seg * sizeof(int)));
+      h->seg_var_cap = n_seg;
+    }
+    EXPECTO_HIP_CHECK(hipMemcpyAsync(h->seg_var_d, pr->var_pos, n_seg * sizeof(int), hipMemcpyHostToDevice, st));
+    if (!alt_w.empty())
+      EXPECTO_HIP_CHECK(hipMemcpyAsync(h->alt_w_d, alt_w.data(), alt_w.size() * sizeof(int), hipMemcpyHostToDevice, st));
+    if (!copy_w.empty())
+      EXPECTO_HIP_CHECK(
+          hipMemcpyAsync(h->copy_w_d, copy_w.data(), copy_w.size() * sizeof(int), hipMemcpyHostToDevice, st));
   }
   if (win_row) {
     for (int w = 0; w < n_win; ++w) EXPECTO_REQUIRE(win_row[w] >= 0 && win_row[w] < n_win, "window row out of range");
@@ -846,7 +882,7 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
                           is_rc ? EXPECTO_STRAND_RC : EXPECTO_STRAND_FWD, 0, ns, L, g.S1, st)))
         return rc;
       if (pr) {
-        seg_delta_table<<<dim3((ns + 255) / 256), dim3(256), 0, st>>>(pr->var_pos, s0, ns, is_rc ? 1 : 0, gd, n_ph,
+        seg_delta_table<<<dim3((ns + 255) / 256), dim3(256), 0, st>>>(h->seg_var_d, s0, ns, is_rc ? 1 : 0, gd, n_ph,
                                                                      ph4, h->seg_tab);
         if ((rc = check_launch("seg_delta_table"))) return rc;
         seg_delta_codes<<<dim3((ns + 15) / 16), dim3(256), 0, st>>>(codes, code_stride, pr->alt_code, s0, ns,
@@ -882,17 +918,35 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
       if (pr && (rc = alt_layer(4, h->Q, g.T5, h->D1, kDW[5], n_ph, 13, 1, 9, kDA[6], kDW[6], false, h->D0)))
         return rc;
       if (nw > 0) {
-        seg_a_rows<<<dim3((nw + 255) / 256), dim3(256), 0, st>>>(
-            h->win_seg_d, h->win_off_d, win_row ? h->win_row_d : nullptr, w0, nw, s0, is_rc ? 1 : 0, L, n_ph,
-            make_int4(ph_idx[0], ph_idx[1], ph_idx[2], ph_idx[3]), g.T6, (long long)sd * strand_rows, h->a_rows,
-            h->c_rows);
+        const int4 phi = make_int4(ph_idx[0], ph_idx[1], ph_idx[2], ph_idx[3]);
+        const long long row_base = (long long)sd * strand_rows;
+        seg_a_rows<<<dim3((nw + 255) / 256), dim3(256), 0, st>>>(h->win_seg_d, h->win_off_d,
+                                                                 win_row ? h->win_row_d : nullptr, nullptr, w0, nw, s0,
+                                                                 is_rc ? 1 : 0, L, n_ph, phi, g.T6, row_base,
+                                                                 h->a_rows, h->c_rows);
         if ((rc = check_launch("seg_a_rows"))) return rc;
         if ((rc = run_fc(h, h->P, h->a_rows, nw, y, st, h->c_rows))) return rc;
-        if (pr) {  // alt conv6 blocks into Q (conv5 rows are dead), same row table
-          seg_alt_blocks<<<dim3(g.T6, (unsigned)nb), dim3(64), 0, st>>>(h->P, h->D0, n_ph, g.T6, h->seg_tab,
-                                                                       640 * eb / 16, h->Q);
-          if ((rc = check_launch("seg_alt_blocks"))) return rc;
-          if ((rc = run_fc(h, h->Q, h->a_rows, nw, pr->y_alt, st, h->c_rows))) return rc;
+        if (pr) {
+          // windows of this chunk holding the SNV (alt FC) and the others (copies of the ref rows)
+          const int ia0 = (int)(std::lower_bound(alt_w.begin(), alt_w.end(), w0) - alt_w.begin());
+          const int ia1 = (int)(std::lower_bound(alt_w.begin(), alt_w.end(), w0 + nw) - alt_w.begin());
+          const int ic0 = (int)(std::lower_bound(copy_w.begin(), copy_w.end(), w0) - copy_w.begin());
+          const int ic1 = (int)(std::lower_bound(copy_w.begin(), copy_w.end(), w0 + nw) - copy_w.begin());
+          if (ia1 > ia0) {  // alt conv6 blocks into Q (conv5 rows are dead), then their FC
+            seg_alt_blocks<<<dim3(g.T6, (unsigned)nb), dim3(64), 0, st>>>(h->P, h->D0, n_ph, g.T6, h->seg_tab,
+                                                                         640 * eb / 16, h->Q);
+            if ((rc = check_launch("seg_alt_blocks"))) return rc;
+            seg_a_rows<<<dim3((ia1 - ia0 + 255) / 256), dim3(256), 0, st>>>(
+                h->win_seg_d, h->win_off_d, win_row ? h->win_row_d : nullptr, h->alt_w_d + ia0, 0, ia1 - ia0, s0,
+                is_rc ? 1 : 0, L, n_ph, phi, g.T6, row_base, h->a_rows, h->c_rows);
+            if ((rc = check_launch("seg_a_rows"))) return rc;
+            if ((rc = run_fc(h, h->Q, h->a_rows, ia1 - ia0, pr->y_alt, st, h->c_rows))) return rc;
+          }
+          if (ic1 > ic0) {
+            copy_rows<<<dim3(ic1 - ic0), dim3(256), 0, st>>>(y, pr->y_alt, h->copy_w_d + ic0,
+                                                             win_row ? h->win_row_d : nullptr, row_base);
+            if ((rc = check_launch("copy_rows"))) return rc;
+          }
         }
       }
       s0 = s1;
@@ -1011,6 +1065,9 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
 void expecto_beluga_destroy(expecto_beluga_t h) {
   if (!h) return;
   if (h->win_seg_d) (void)hipFree(h->win_seg_d);
+  if (h->alt_w_d) (void)hipFree(h->alt_w_d);
+  if (h->copy_w_d) (void)hipFree(h->copy_w_d);
+  if (h->seg_var_d) (void)hipFree(h->seg_var_d);
   if (h->win_off_d) (void)hipFree(h->win_off_d);
   if (h->win_row_d) (void)hipFree(h->win_row_d);
   for (void* p : h->allocs) (void)hipFree(p);

@@ -136,6 +136,7 @@ class VariantPipeline:
                     "splice_pos": torch.full((ns,), 999 - lo_s, dtype=torch.int32, device=dev),
                     "splice_code": torch.from_numpy(rc).to(dev),
                     "alt_code": torch.from_numpy(ac).to(dev),
+                    "var_pos": np.full(ns, 999 - lo_s, np.int32),
                     "win_seg": v_i.ravel().astype(np.int32),
                     "win_off": (np.asarray(shifts)[j_i.ravel()] - lo_s).astype(np.int32),
                     "win_row": (j_i * ns + v_i).ravel().astype(np.int32),
@@ -213,7 +214,7 @@ class VariantPipeline:
                                          seg["splice_code"])
                 if seg["pairs"]:
                     yf = y.view(4 * S * ns, 2002)
-                    self.engine.forward_segment_pairs(scodes, seg["L"], seg["splice_pos"], seg["alt_code"],
+                    self.engine.forward_segment_pairs(scodes, seg["L"], seg["var_pos"], seg["alt_code"],
                                                       seg["win_seg"], seg["win_off"], seg["win_row"], yf[0:],
                                                       yf[S * ns:], 2 * S * ns, _lib.STRAND_BOTH)
                 else:

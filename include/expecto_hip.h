@@ -127,11 +127,12 @@ int expecto_beluga_forward_pairs(expecto_beluga_t h, const uint8_t* ref_codes, c
 
 /* SNV shift sweeps on the segment path with alt reuse: segment i (as in
  * expecto_beluga_forward_segments) is the REF sequence; its alt sequence has code
- * alt_code[i] at index var_pos[i] (DEVICE arrays, one per segment).  Both alleles' windows are
- * computed (same win_* tables): the ref trunk once per segment, and for the alt only the rows
- * the SNV changes at each layer (conv1 8, pool1 5, conv3 12, conv4 19, pool2 6 per phase,
- * conv5 13, conv6 20), assembled from the ref activations -- bit-identical to the full alt
- * forward.  Window w of strand s lands in row s*strand_stride + win_row[w] of y_ref and of
+ * alt_code[i] (DEVICE array) at index var_pos[i] (HOST array, 0 <= var_pos[i] < seg_len).
+ * Both alleles' windows are computed (same win_* tables): the ref trunk once per segment, and
+ * for the alt only the rows the SNV changes at each layer (conv1 8, pool1 5, conv3 12, conv4
+ * 19, pool2 6 per phase, conv5 13, conv6 20), assembled from the ref activations; alt windows
+ * that do not hold the SNV equal their ref window and get a copy of its row -- bit-identical
+ * to the full alt forward.  Window w of strand s lands in row s*strand_stride + win_row[w] of y_ref and of
  * y_alt.  Replaces the ref/alt forwards of chromatin.py:243-281 for --maxshift sweeps (and
  * the 200-shift eQTL variant scoring of geuvadis_sed_for_top_eqtls.py:61-98). */
 int expecto_beluga_forward_segment_pairs(expecto_beluga_t h, const uint8_t* codes, const int* var_pos,

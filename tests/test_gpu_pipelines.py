@@ -217,13 +217,13 @@ def test_segment_pairs_alt_runs_are_bitwise_equal(precision):
                                 .astype(np.uint8)).cuda()
     alt = ref.clone()
     alt[torch.arange(n), torch.from_numpy(q).long()] = alt_code
-    offs = np.array([0, 4, 200, 796, 800, 1000, 1596, 1600], np.int32)
+    offs = np.array([0, 4, 200, 796, 800, 1000, 1596, 1600], np.int32)   # some windows miss some SNVs
     S = offs.size
     v_i, j_i = np.meshgrid(np.arange(n), np.arange(S), indexing="ij")
     win_seg, win_off, win_row = v_i.ravel().astype(np.int32), offs[j_i.ravel()], (j_i * n + v_i).ravel().astype(np.int32)
     y = torch.full((2, 2, S * n, 2002), float("nan"), device="cuda")
     yf = y.view(4 * S * n, 2002)
-    eng.forward_segment_pairs(ref, L, torch.from_numpy(q).cuda(), alt_code, win_seg, win_off, win_row, yf[0:],
+    eng.forward_segment_pairs(ref, L, q, alt_code, win_seg, win_off, win_row, yf[0:],
                               yf[S * n:], 2 * S * n)
     for a, src in enumerate((ref, alt)):
         wins = torch.stack([src[:, o:o + 2000] for o in offs], 0).reshape(S * n, 2000).contiguous()  # row j*n + v
