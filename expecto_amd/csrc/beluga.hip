@@ -662,6 +662,7 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     a.ldc = kHidLd;
     a.n_store = kHidLd;
     a.split_stride = (long long)nb * kHidLd;
+    a.linear_order = 1;
     LayerTimer lt(h, 6, st);
     if (h->profiling) h->macs[6] += (double)nb * kFc1Out * kFc1In;
     if ((rc = launch_gemm<7, EPI_PARTIAL>(a, splits, st))) return rc;

@@ -41,6 +41,8 @@ struct GemmArgs {
   const long long* a_rows;  // optional: A row m starts at A + a_rows[m] (FC1 over segment windows)
   const long long* c_rows;  // optional: C row of M row m (non-pool epilogues; FC2 output order)
   const void* Bp;           // bf16x6 GEMM: B as bf16 planes [Npad][K/32][3][32] (split_planes)
+  int linear_order;         // bf16x6 GEMM: blocks in dispatch order (no XCD grouping); FC1 sets it
+                            // so every XCD sweeps the same K slab at once (Infinity-Cache reuse)
 };
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -507,7 +509,8 @@ __global__ __launch_bounds__(256, 1) void beluga_gemm_x6q(GemmArgs p) {
 
   const unsigned nblk = gridDim.x, bid = blockIdx.x;
   const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
-  const unsigned lin = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const unsigned lin =
+      p.linear_order ? bid : (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
   long long mt;
   int nt, ks;
   if (p.m_fastest) {
