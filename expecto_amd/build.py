@@ -22,7 +22,7 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = SOURCES + [os.path.join(HERE, "csrc", "common.h"),
+    deps = SOURCES + [os.path.join(HERE, "csrc", h) for h in ("common.h", "gemm_kernel.h")] + [
                       os.path.join(os.path.dirname(HERE), "include", "expecto_hip.h")]
     return any(os.path.getmtime(d) > t for d in deps)
 
