@@ -37,6 +37,7 @@ FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 
 # per 32 cycles) x 2.4 GHz = 2516.6 TFLOP/s (MI355X_MICROARCH.md "~2.5 PF dense")
 BF16_MFMA_PEAK_TFLOPS = 256 * 4 * 1024 * 2.4e9 / 1e12
 BF16X6_PRODUCTS = 6               # bf16 MFMA products per fp32 multiply-add in the bf16x6 kernel
+F16X3_PRODUCTS = 3                # fp16 MFMA products per multiply-add in the f16x3 kernel (fp16 peak = bf16 peak)
 
 # per-window dense MACs of each layer, for the roofline of each kernel
 LAYER_MACS = {
@@ -48,12 +49,24 @@ GEMM_LAYER_EPI = {"conv2": (2, 1), "conv3": (3, 0), "conv4": (4, 1), "conv5": (5
                   "fc1": (7, 3), "fc2": (8, 2)}
 
 
+DTYPES = {
+    "bf16x6": "fp32 (bf16x6: exact 3-way bf16 split, 6 MFMA products, fp32 accumulate)",
+    "f16x3": "fp32 in/out (f16x3: power-of-2-scaled 2-way fp16 split = 22-bit operands, 3 MFMA products, "
+             "fp32 accumulate; bf16x6 recompute on fp16 overflow)",
+    "fp32": "fp32",
+}
+
+
 def kernel_name(layer: str, precision: str) -> str:
     """rocprofv3 kernel name of a layer's launch (per-window path)."""
     if layer not in GEMM_LAYER_EPI:
         return {"conv1": "beluga_conv1", "fc1_reduce": "fc1_reduce"}[layer]
     l, e = GEMM_LAYER_EPI[layer]
-    return f"beluga_gemm_x6q<{l}, {e}, 0>" if precision == "bf16x6" else f"beluga_gemm<{l}, {e}, 4, 2, 32, 1>"
+    if precision == "bf16x6":
+        return f"beluga_gemm_x6q<{l}, {e}, 0>"
+    if precision == "f16x3":
+        return f"beluga_gemm_h3q<{l}, {e}, 0, 3>" if l in (7, 8) else f"beluga_conv_h3q<{l}, {e}, 0>"
+    return f"beluga_gemm<{l}, {e}, 4, 2, 32, 1>"
 WINDOW_MACS = sum(LAYER_MACS.values())
 
 
@@ -129,6 +142,8 @@ def roofline(layers, precision):
     fp32_tflops = fp32_flops_launch / (ms / calls / 1e3) / 1e12
     if precision == "bf16x6":
         mult, peak = BF16X6_PRODUCTS, BF16_MFMA_PEAK_TFLOPS
+    elif precision == "f16x3":
+        mult, peak = F16X3_PRODUCTS, BF16_MFMA_PEAK_TFLOPS
     else:
         mult, peak = 1, FP32_MFMA_PEAK_TFLOPS
     achieved = mult * fp32_tflops
@@ -170,6 +185,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the cfg3 / 200-window extra workloads")
+    ap.add_argument("--precision", default=None, help="GEMM arithmetic (default: the engine default)")
     args = ap.parse_args()
 
     rank, world, local = edist.init("nccl")
@@ -187,6 +203,8 @@ def main():
     sd_cpu = {k: v.detach().clone() for k, v in model.state_dict().items()} if (rank == 0 and world == 1) else None
     model = model.cuda()
     eng = model.engine()
+    if args.precision:
+        eng.set_precision(args.precision)
     pipe = VariantPipeline(eng, fasta, DeviceGenome(fasta, device=dev))
     prep = pipe.prepare(vs, shifts)                          # variant table resident in HBM
 
@@ -204,8 +222,7 @@ def main():
         "metric": METRIC, "value": value, "unit": "variants/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32 (bf16x6: exact 3-way bf16 split, 6 MFMA products, fp32 accumulate)"
-                 if eng.precision == "bf16x6" else "fp32",
+        "dtype": DTYPES[eng.precision],
         "data": "synthetic: seeded genome (24 x 2 Mbp), seeded SNVs, seeded Beluga weights x sqrt(6)",
         "config": {"workload": f"configs[1]: {n} SNVs/GPU, shifts {shifts}, ref+alt x fwd+rc = "
                                f"{rows} Beluga windows/step/GPU (window gen + forward + diff)",
@@ -220,6 +237,9 @@ def main():
         "reuse": "alt-cone (SNV alt windows recompute <=20 of 106 conv6 rows; bit-identical)" if S == 1 else
                  "segments (trunk shared across shifts; bit-identical)",
     }
+    if eng.precision == "f16x3":
+        fb, sx = eng.f16_state()
+        rec["f16x3"] = {"fallback_calls": fb, "activation_scale_exp": sx}
     if world == 1 and not args.no_extras:
         extras = {}
         # configs[2]: the +-800 shift sweep (9 shifts) -- segment path (trunk shared across shifts)

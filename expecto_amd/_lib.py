@@ -43,6 +43,8 @@ SIGNATURES = {
                                                             ctypes.c_int, c_vp, c_vp, ctypes.c_longlong, c_vp]),
     "expecto_beluga_set_precision": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "expecto_beluga_get_precision": (ctypes.c_int, [c_vp]),
+    "expecto_beluga_set_f16_target": (ctypes.c_int, [c_vp, ctypes.c_int]),
+    "expecto_beluga_f16_fallbacks": (ctypes.c_longlong, [c_vp, c_i32p]),
     "expecto_beluga_set_profiling": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "expecto_beluga_layer_times": (ctypes.c_int, [c_vp, c_f64p, c_i64p, c_f64p, ctypes.c_int]),
     "expecto_variant_windows": (ctypes.c_int, [c_vp, ctypes.c_longlong, c_vp, c_vp, c_vp, ctypes.c_int, c_vp,
@@ -59,8 +61,8 @@ SIGNATURES = {
 }
 
 STRAND_FWD, STRAND_RC, STRAND_BOTH = 0, 1, 2
-PRECISION_FP32, PRECISION_BF16X6 = 0, 1
-PRECISIONS = {"fp32": PRECISION_FP32, "bf16x6": PRECISION_BF16X6}
+PRECISION_FP32, PRECISION_BF16X6, PRECISION_F16X3 = 0, 1, 2
+PRECISIONS = {"fp32": PRECISION_FP32, "bf16x6": PRECISION_BF16X6, "f16x3": PRECISION_F16X3}
 N_LAYERS = 9
 LAYER_NAMES = ("conv1", "conv2", "conv3", "conv4", "conv5", "conv6", "fc1", "fc1_reduce", "fc2")
 

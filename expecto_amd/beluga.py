@@ -60,11 +60,28 @@ class BelugaEngine:
         self.set_precision(os.environ.get("EXPECTO_PRECISION", "bf16x6"))
 
     def set_precision(self, precision: str):
-        """'bf16x6' (default, fp32-faithful split-bf16 MFMA) or 'fp32' (exact fp32 MFMA)."""
+        """GEMM arithmetic (include/expecto_hip.h): 'bf16x6' (fp32-faithful split-bf16 MFMA),
+        'f16x3' (scaled split-fp16, half the MFMA work, bf16x6 fallback on fp16 overflow) or
+        'fp32' (exact fp32 MFMA)."""
         if precision not in _lib.PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(_lib.PRECISIONS)}")
-        _lib.check(self.lib.expecto_beluga_set_precision(self.handle, _lib.PRECISIONS[precision]), "set_precision")
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.expecto_beluga_set_precision(self.handle, _lib.PRECISIONS[precision]),
+                       "set_precision")
         self.precision = precision
+
+    def set_f16_target(self, target_log2: int):
+        """f16x3 calibration target: the largest calibration activation maps to 2^target_log2."""
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.expecto_beluga_set_f16_target(self.handle, int(target_log2)), "set_f16_target")
+
+    def f16_state(self):
+        """(calls recomputed with bf16x6 after an fp16 overflow, activation scale exponents [7])."""
+        sx = (ctypes.c_int * 7)()
+        n = self.lib.expecto_beluga_f16_fallbacks(self.handle, sx)
+        if n < 0:
+            _lib.check(int(n), "f16_fallbacks")
+        return int(n), list(sx)
 
     def __del__(self):
         h = getattr(self, "handle", None)

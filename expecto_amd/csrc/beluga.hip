@@ -48,7 +48,8 @@ constexpr int C1_T = 128;
 __global__ __launch_bounds__(320) void beluga_conv1(const float* __restrict__ x, const uint8_t* __restrict__ codes,
                                                     long long code_stride, int n_src, int mode, long long row0,
                                                     const float* __restrict__ w1, const float* __restrict__ b1,
-                                                    float* __restrict__ out, int out_rows, int len, int x3) {
+                                                    float* __restrict__ out, int out_rows, int len, int fmt,
+                                                    float osc, int* __restrict__ ovf) {
   __shared__ floatx4 xs[C1_T + 8];
   const int t0 = blockIdx.x * C1_T;
   const long long win = blockIdx.y;
@@ -102,27 +103,22 @@ __global__ __launch_bounds__(320) void beluga_conv1(const float* __restrict__ x,
       s = fmaf(w[16 + k], v[2], s);
       s = fmaf(w[24 + k], v[3], s);
     }
-    const float v = fmaxf(s + bco, 0.f);
-    if (x3)
-      store_act<true>(out, orow + t, 320, co, v);
-    else
-      store_act<false>(out, orow + t, 320, co, v);
+    store_act_rt(fmt, out, orow + t, 320, co, fmaxf(s + bco, 0.f), osc, ovf);
   }
 }
 
 __global__ void fc1_reduce(const float* __restrict__ part, int splits, long long split_stride, long long count,
-                           const float* __restrict__ bias, float* __restrict__ h1, int x3) {
+                           const float* __restrict__ bias, float* __restrict__ h1, int fmt,
+                           const float* __restrict__ col_scale, float osc, int* __restrict__ ovf) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   const long long row = i / kHidLd;
   const int n = (int)(i - row * kHidLd);
   float s = 0.f;
   for (int k = 0; k < splits; ++k) s += part[k * split_stride + i];
+  if (col_scale) s *= col_scale[n];   // f16x3: exact power-of-2 unscaling of the split-K sum
   const float v = n < kFc1Out ? fmaxf(s + bias[n], 0.f) : 0.f;
-  if (x3)
-    store_act<true>(h1, row, kHidLd, n, v);
-  else
-    h1[i] = v;
+  store_act_rt(fmt, h1, row, kHidLd, n, v, osc, ovf);
 }
 
 // MaxPool(1,4) floor mode at pool phases p (segment path, SURVEY.md 5 "trunk sharing"):
@@ -131,7 +127,7 @@ __global__ void fc1_reduce(const float* __restrict__ part, int splits, long long
 // One thread per channel; on the bf16x6 path the values are recovered exactly from their
 // planes, pooled, and re-split (so the planes equal those of the pooled fp32 value).
 __global__ void pool4_phases(const float* __restrict__ in, int n_seg, int s_in, int t_in, int C,
-                             int n_ph, int4 ph, int s_out, float* __restrict__ out, int x3) {
+                             int n_ph, int4 ph, int s_out, float* __restrict__ out, int fmt) {
   const int c = threadIdx.x;
   const int g = blockIdx.x;
   const int i = blockIdx.y % n_ph;
@@ -139,13 +135,10 @@ __global__ void pool4_phases(const float* __restrict__ in, int n_seg, int s_in, 
   const int p = i == 0 ? ph.x : i == 1 ? ph.y : i == 2 ? ph.z : ph.w;
   if (c >= C || g >= (t_in - p) / 4) return;
   const long long r0 = seg * s_in + p + 4LL * g, orow = (seg * n_ph + i) * s_out + g;
-  float m = x3 ? load_x3(in, r0, C, c) : in[r0 * C + c];
+  float m = load_act_rt(fmt, in, r0, C, c);
 #pragma unroll
-  for (int j = 1; j < 4; ++j) m = fmaxf(m, x3 ? load_x3(in, r0 + j, C, c) : in[(r0 + j) * C + c]);
-  if (x3)
-    store_act<true>(out, orow, C, c, m);
-  else
-    out[orow * C + c] = m;
+  for (int j = 1; j < 4; ++j) m = fmaxf(m, load_act_rt(fmt, in, r0 + j, C, c));
+  store_act_rt(fmt, out, orow, C, c, m);   // fmt 2: values stay in the (shared) scaled domain
 }
 
 // FC1 row table of the windows of one segment chunk: window m of the chunk reads conv6
@@ -346,7 +339,7 @@ __global__ void seg_delta_assemble(const float* __restrict__ ref, int ref_rows, 
 // pool2 of the alt run for each phase: pooled rows [r4p, r4p+6) of block (seg, phase) from the
 // ref's unpooled conv4 rows and the alt conv4 run (exact max, as pool4_phases)
 __global__ void seg_delta_pool(const float* __restrict__ conv4, int t4, const float* __restrict__ d4, int n_ph,
-                               int4 ph, const int* __restrict__ tab, int x3, float* __restrict__ out) {
+                               int4 ph, const int* __restrict__ tab, int fmt, float* __restrict__ out) {
   const int c = threadIdx.x;
   if (c >= 480) return;
   const int gi = blockIdx.x, m = blockIdx.y;
@@ -361,13 +354,10 @@ __global__ void seg_delta_pool(const float* __restrict__ conv4, int t4, const fl
     const bool alt = row >= r4 && row < r4 + kW4u;
     const float* b = alt ? d4 : conv4;
     const long long r = alt ? (long long)seg * kW4u + row - r4 : (long long)seg * t4 + row;
-    const float v = x3 ? load_x3(b, r, 480, c) : b[r * 480 + c];
+    const float v = load_act_rt(fmt, b, r, 480, c);
     mx = j == 0 ? v : fmaxf(mx, v);
   }
-  if (x3)
-    store_act<true>(out, (long long)m * kDW[4] + gi, 480, c, mx);
-  else
-    out[((long long)m * kDW[4] + gi) * 480 + c] = mx;
+  store_act_rt(fmt, out, (long long)m * kDW[4] + gi, 480, c, mx);
 }
 
 // alt conv6 phase blocks: the ref block (t6 rows) with rows [r6, r6+20) from the alt run
@@ -428,6 +418,67 @@ __global__ void pad_copy(const float* __restrict__ src, int n, int npad, float* 
   if (i < npad) dst[i] = i < n ? src[i] : 0.f;
 }
 
+// ---- f16x3 scaling --------------------------------------------------------------------
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// s_w[n] = 15 - e with max_k |W[n][k]| = m * 2^e (m in [0.5, 1)): the row's largest weight
+// lands in [2^14, 2^15) after scaling.  All-zero (padding) rows get 0.
+__global__ void row_scale_exp(const float* __restrict__ W, int K, int* __restrict__ sw) {
+  __shared__ float red[4];
+  const long long n = blockIdx.x;
+  float m = 0.f;
+  for (int k = threadIdx.x; k < K; k += blockDim.x) m = fmaxf(m, fabsf(W[n * K + k]));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    int e = 0;
+    (void)frexpf(m, &e);
+    sw[n] = m > 0.f ? 15 - e : 0;
+  }
+}
+
+// col_scale[n] = 2^-(s_in + s_w[n]): undoes both operand scales of a GEMM column exactly
+__global__ void col_scales(const int* __restrict__ sw, int n, int s_in, float* __restrict__ cs) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) cs[i] = ldexpf(1.f, -(s_in + sw[i]));
+}
+
+// max over the valid rows (t_valid of every s_rows) and first C channels of a bf16x6-format
+// activation buffer (non-negative: every boundary follows a ReLU), as float bits
+__global__ void act_max(const float* __restrict__ A, long long groups, int s_rows, int t_valid, int ld, int C,
+                        unsigned* __restrict__ out) {
+  const long long rows = groups * t_valid;
+  float m = 0.f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < rows * C;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / C;
+    const int c = (int)(i - r * C);
+    const long long row = (r / t_valid) * s_rows + r % t_valid;
+    m = fmaxf(m, load_act<1>(A, row, ld, c));
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+// seeded random A/G/C/T codes (calibration windows)
+__global__ void random_codes(uint8_t* __restrict__ codes, long long n, unsigned seed) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  unsigned x = (unsigned)i * 2654435761u ^ seed;
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  codes[i] = (uint8_t)(x & 3u);
+}
+
 }  // namespace expecto
 
 using namespace expecto;
@@ -468,6 +519,19 @@ struct expecto_beluga {
   float* wp[5] = {};             // bf16x6: weight planes of conv2..6, FC1, FC2 (split_planes)
   float* fc1p = nullptr;
   float* fc2p = nullptr;
+  // f16x3 (built on the first switch to it): fp16 weight planes of the 7 GEMM layers (conv2..6,
+  // FC1, FC2), their per-channel scale exponents, per-column unscale factors, the calibrated
+  // activation scale exponents sx[g] of GEMM layer g's input (sx[0] = conv1 output), and the
+  // device overflow flag.
+  float* wh[7] = {};
+  int* swd[7] = {};
+  float* cs[7] = {};
+  int sx[7] = {};
+  int f16_target = 10;
+  bool f16_ready = false;
+  int* ovf = nullptr;
+  float* calib = nullptr;        // calibration windows' codes, outputs and maxima
+  long long fallbacks = 0;
   float* P = nullptr;
   float* Q = nullptr;
   float* part = nullptr;
@@ -565,13 +629,19 @@ struct LayerTimer {
   }
 };
 
-// Arithmetic of the MFMA GEMMs: exact fp32 (v_mfma_f32_32x32x2_f32) or the fp32-faithful
-// 3-way bf16 split (six v_mfma_f32_32x32x16_bf16 products per k-step, gemm_kernel.h).
+// Arithmetic of the MFMA GEMMs: exact fp32 (v_mfma_f32_32x32x2_f32), the fp32-faithful 3-way
+// bf16 split (bf16x6) or the scaled 2-way fp16 split (f16x3), gemm_kernel.h.
 thread_local int g_precision = EXPECTO_PRECISION_BF16X6;
 
-// activations stored as bf16 planes (bf16x6 path) or fp32 rows
-int x3_act() { return g_precision == EXPECTO_PRECISION_BF16X6 ? 1 : 0; }
-long long gemm_bm() { return g_precision == EXPECTO_PRECISION_BF16X6 ? X6P_BM : GBM; }
+// activation storage format (gemm_kernel.h): 1 bf16 planes (bf16x6), 2 scaled fp16 planes
+// (f16x3), 0 fp32 rows; bytes per element 6 / 4 / 4
+int act_fmt() {
+  return g_precision == EXPECTO_PRECISION_BF16X6 ? 1 : g_precision == EXPECTO_PRECISION_F16X3 ? 2 : 0;
+}
+int act_bytes() { return act_fmt() == 1 ? 6 : 4; }
+bool planes_gemm() { return g_precision != EXPECTO_PRECISION_FP32; }
+long long gemm_bm() { return planes_gemm() ? X6P_BM : GBM; }
+float exp2i(int e) { return std::ldexp(1.0f, e); }
 
 template <int LAYER, int EPI>
 int launch_gemm(const GemmArgs& a, int splits, hipStream_t st) {
@@ -584,6 +654,16 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st) {
   if (g_precision == EXPECTO_PRECISION_BF16X6) {
     EXPECTO_REQUIRE(a.Bp != nullptr && a.lda % GBK == 0 && a.ldb % GBK == 0, "bf16x6 GEMM needs planes, K % 32");
     beluga_gemm_x6q<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
+  } else if (g_precision == EXPECTO_PRECISION_F16X3) {
+    EXPECTO_REQUIRE(a.Bp != nullptr && a.lda % GBK == 0 && a.ldb % GBK == 0, "f16x3 GEMM needs planes, K % 32");
+    EXPECTO_REQUIRE(EPI == EPI_PARTIAL || a.col_scale != nullptr, "f16x3 GEMM needs column scales");
+    if (a.taps == 8) {   // conv: chunk-slab kernel (one Toeplitz A slab per 32-channel chunk)
+      EXPECTO_REQUIRE(splits == 1 && a.kper == a.ldb && a.ldb == 8 * a.lda && !a.m_fastest && !a.a_rows,
+                      "f16x3 conv GEMM: full K, no split, no row gather");
+      beluga_conv_h3q<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
+    } else {
+      beluga_gemm_h3q<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
+    }
   } else
     beluga_gemm<LAYER, EPI, kWM, kMinBlocks, GBK, kPipe><<<dim3((unsigned)nblk), dim3(64 * kWM), 0, st>>>(a);
   return check_launch("beluga_gemm");
@@ -595,7 +675,7 @@ int run_conv1(expecto_beluga* h, const float* x, const uint8_t* codes, long long
   if (h->profiling) h->macs[0] += (double)nb * (len - 7) * 320 * 32;
   dim3 grid((len - 7 + C1_T - 1) / C1_T, nb);
   beluga_conv1<<<grid, dim3(320), 0, st>>>(x, codes, code_stride, n_src, mode, row0, h->w1, h->b1,
-                                           dst ? dst : h->P, out_rows, len, x3_act());
+                                           dst ? dst : h->P, out_rows, len, act_fmt(), exp2i(h->sx[0]), h->ovf);
   return check_launch("beluga_conv1");
 }
 
@@ -608,7 +688,10 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
   a.lda = g.cin;
   a.M = groups * s_in;
   a.B = h->wt[l];
-  a.Bp = h->wp[l];
+  a.Bp = g_precision == EXPECTO_PRECISION_F16X3 ? h->wh[l] : h->wp[l];
+  a.col_scale = g_precision == EXPECTO_PRECISION_F16X3 ? h->cs[l] : nullptr;
+  a.out_scale = exp2i(h->sx[l + 1]);
+  a.ovf = h->ovf;
   a.ldb = 8LL * g.cin;
   a.kper = 8 * g.cin;
   a.taps = 8;
@@ -651,7 +734,7 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     a.lda = (long long)kFc1In;
     a.M = nb;
     a.B = h->fc1w;
-    a.Bp = h->fc1p;
+    a.Bp = g_precision == EXPECTO_PRECISION_F16X3 ? h->wh[5] : h->fc1p;
     a.ldb = kFc1In;
     a.kper = kFc1In / splits;
     a.taps = 1;
@@ -670,8 +753,9 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
   {
     LayerTimer lt(h, 7, st);
     const long long count = (long long)nb * kHidLd;
-    fc1_reduce<<<dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st>>>(h->part, splits, count, count, h->fc1b,
-                                                                            h->h1, x3_act());
+    const bool f16 = g_precision == EXPECTO_PRECISION_F16X3;
+    fc1_reduce<<<dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st>>>(
+        h->part, splits, count, count, h->fc1b, h->h1, act_fmt(), f16 ? h->cs[5] : nullptr, exp2i(h->sx[6]), h->ovf);
     if ((rc = check_launch("fc1_reduce"))) return rc;
   }
   {
@@ -680,7 +764,8 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     a.lda = kHidLd;
     a.M = nb;
     a.B = h->fc2w;
-    a.Bp = h->fc2p;
+    a.Bp = g_precision == EXPECTO_PRECISION_F16X3 ? h->wh[6] : h->fc2p;
+    a.col_scale = g_precision == EXPECTO_PRECISION_F16X3 ? h->cs[6] : nullptr;
     a.ldb = kHidLd;
     a.kper = kHidLd;
     a.taps = 1;
@@ -852,7 +937,7 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
   // alt runs: one block per segment (conv1..4) or per (segment, phase) (pool2, conv5, conv6)
   const int blk_per_seg = pr ? std::max(n_ph, 1) : 0;
   const long long strand_rows = pr ? pr->strand_stride : n_win;
-  const int eb = x3_act() ? 6 : 4;
+  const int eb = act_bytes();
   const SegDims gd{L, g.T1, g.P1, g.T3, g.T4, g.S5, g.T5, g.T6};
   const int4 ph4 = make_int4(ph[0], ph[1], ph[2], ph[3]);
   for (int sd = 0; sd < strands; ++sd) {
@@ -903,11 +988,11 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
       {  // pool2 phases (Q -> P)
         LayerTimer lt(h, 3, st);
         dim3 grid(g.S5, ns * n_ph);
-        pool4_phases<<<grid, dim3(480), 0, st>>>(h->Q, ns, g.T4, g.T4, 480, n_ph, ph4, g.S5, h->P, x3_act());
+        pool4_phases<<<grid, dim3(480), 0, st>>>(h->Q, ns, g.T4, g.T4, 480, n_ph, ph4, g.S5, h->P, act_fmt());
         if ((rc = check_launch("pool4_phases"))) return rc;
         if (pr) {
           seg_delta_pool<<<dim3(kDW[4], (unsigned)nb), dim3(480), 0, st>>>(h->Q, g.T4, h->D1, n_ph, ph4, h->seg_tab,
-                                                                           x3_act(), h->D0);
+                                                                           act_fmt(), h->D0);
           if ((rc = check_launch("seg_delta_pool"))) return rc;
         }
       }
@@ -961,7 +1046,7 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
   const int strands = mode == EXPECTO_STRAND_BOTH ? 2 : 1;
   int rc;
   if ((rc = ensure_delta(h))) return rc;
-  const int eb = x3_act() ? 6 : 4;   // bytes per activation element
+  const int eb = act_bytes();   // bytes per activation element
   const int nv_max = std::max(1, h->max_batch / strands);
   for (int v0 = 0; v0 < n; v0 += nv_max) {
     const int nv = std::min(nv_max, n - v0), R = strands * nv;
@@ -995,6 +1080,129 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
     if ((rc = run_fc(h, act6, nullptr, R, y_alt, st, h->c_rows))) return rc;
   }
   return EXPECTO_OK;
+}
+
+// ---- f16x3 set-up: fp16 weight planes + activation-scale calibration -----------------------
+constexpr int kCalibWindows = 256;
+
+// column scales of every GEMM layer from the current sx[] and the weight exponents
+int f16_col_scales(expecto_beluga* h, hipStream_t st) {
+  const int np[7] = {npad_of(320), npad_of(480), npad_of(480), npad_of(640), npad_of(640), npad_of(kFc1Out),
+                     npad_of(kNFeat)};
+  for (int g = 0; g < 7; ++g) {
+    col_scales<<<dim3((np[g] + 255) / 256), dim3(256), 0, st>>>(h->swd[g], np[g], h->sx[g], h->cs[g]);
+    int rc = check_launch("col_scales");
+    if (rc) return rc;
+  }
+  return EXPECTO_OK;
+}
+
+// sx[b] = target - e, with the calibration maximum of boundary b = m * 2^e (m in [0.5, 1)):
+// that maximum lands in (2^(target-1), 2^target] after scaling.
+int f16_calibrate(expecto_beluga* h, hipStream_t st) {
+  const int nb = std::min(kCalibWindows, h->max_batch);
+  int rc;
+  if (!h->calib && (rc = dalloc(h, &h->calib, (size_t)nb * kNFeat + (size_t)nb * kLen / 4 + 64))) return rc;
+  float* buf = h->calib;
+  float* y = buf;
+  uint8_t* codes = reinterpret_cast<uint8_t*>(buf + (size_t)nb * kNFeat);
+  unsigned* amax = reinterpret_cast<unsigned*>(buf + (size_t)nb * kNFeat + (size_t)nb * kLen / 4);
+  EXPECTO_HIP_CHECK(hipMemsetAsync(amax, 0, 8 * sizeof(unsigned), st));
+  const long long nc = (long long)nb * kLen;
+  random_codes<<<dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st>>>(codes, nc, 0x5eed1234u);
+  if ((rc = check_launch("random_codes"))) return rc;
+  const int saved = g_precision;
+  const bool prof = h->profiling;
+  h->profiling = false;
+  g_precision = EXPECTO_PRECISION_BF16X6;
+  auto amax_of = [&](const float* A, long long groups, int s_rows, int t_valid, int C, int b) {
+    act_max<<<dim3(1024), dim3(256), 0, st>>>(A, groups, s_rows, t_valid, C, C, amax + b);
+    return check_launch("act_max");
+  };
+  rc = run_conv1(h, nullptr, codes, kLen, nb, EXPECTO_STRAND_FWD, 0, nb, kLen, kS1, st);
+  if (!rc) rc = amax_of(h->P, nb, kS1, kLen - 7, 320, 0);
+  float* src = h->P;
+  float* dst = h->Q;
+  for (int l = 0; l < 5 && !rc; ++l) {
+    const ConvGeo& g = kConv[l];
+    rc = run_conv(h, l, src, dst, nb, g.s_in, g.t_valid, g.s_out, g.pool != 0, st);
+    if (!rc) rc = amax_of(dst, nb, g.s_out, g.t_valid, g.cout, l + 1);
+    std::swap(src, dst);
+  }
+  if (!rc) rc = run_fc(h, src, nullptr, nb, y, st);
+  if (!rc) {
+    act_max<<<dim3(1024), dim3(256), 0, st>>>(h->h1, nb, 1, 1, kHidLd, kFc1Out, amax + 6);
+    rc = check_launch("act_max");
+  }
+  g_precision = saved;
+  h->profiling = prof;
+  if (rc) return rc;
+  unsigned bits[7];
+  EXPECTO_HIP_CHECK(hipMemcpyAsync(bits, amax, sizeof(bits), hipMemcpyDeviceToHost, st));
+  EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
+  for (int b = 0; b < 7; ++b) {
+    float m;
+    std::memcpy(&m, &bits[b], sizeof(float));
+    int e = 0;
+    (void)std::frexp(m, &e);
+    h->sx[b] = (m > 0.f && std::isfinite(m)) ? std::min(40, std::max(-40, h->f16_target - e)) : 0;
+  }
+  return f16_col_scales(h, st);
+}
+
+int f16_prepare(expecto_beluga* h, hipStream_t st) {
+  if (h->f16_ready) return EXPECTO_OK;
+  int rc;
+  struct L {
+    const float* w;
+    int rows;
+    long long K;
+  } layers[7] = {{h->wt[0], npad_of(320), 8LL * 320}, {h->wt[1], npad_of(480), 8LL * 320},
+                 {h->wt[2], npad_of(480), 8LL * 480}, {h->wt[3], npad_of(640), 8LL * 480},
+                 {h->wt[4], npad_of(640), 8LL * 640}, {h->fc1w, npad_of(kFc1Out), kFc1In},
+                 {h->fc2w, npad_of(kNFeat), kHidLd}};
+  if (!h->ovf) {
+    float* f = nullptr;
+    if ((rc = dalloc(h, &f, 1))) return rc;
+    h->ovf = reinterpret_cast<int*>(f);
+    EXPECTO_HIP_CHECK(hipMemsetAsync(h->ovf, 0, sizeof(int), st));
+  }
+  for (int g = 0; g < 7; ++g) {
+    const L& y = layers[g];
+    float* swf = nullptr;
+    if ((rc = dalloc(h, &swf, y.rows)) || (rc = dalloc(h, &h->cs[g], y.rows)) ||
+        (rc = dalloc(h, &h->wh[g], (size_t)y.rows * y.K)))
+      return rc;
+    h->swd[g] = reinterpret_cast<int*>(swf);
+    row_scale_exp<<<dim3(y.rows), dim3(256), 0, st>>>(y.w, (int)y.K, h->swd[g]);
+    if ((rc = check_launch("row_scale_exp"))) return rc;
+    const long long n4 = (long long)y.rows * y.K / 4;
+    split_planes_h2<<<dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st>>>(
+        y.w, y.rows, (int)y.K, h->swd[g], reinterpret_cast<_Float16*>(h->wh[g]));
+    if ((rc = check_launch("split_planes_h2"))) return rc;
+  }
+  if ((rc = f16_calibrate(h, st))) return rc;
+  h->f16_ready = true;
+  return EXPECTO_OK;
+}
+
+// Run one public call; on the f16x3 path check the overflow flag afterwards and, if an
+// activation did not fit fp16, recompute the whole call with bf16x6.
+template <class F>
+int run_checked(expecto_beluga* h, hipStream_t st, F&& fn) {
+  if (h->precision != EXPECTO_PRECISION_F16X3) return fn();
+  int rc = fn();
+  if (rc) return rc;
+  int flag = 0;
+  EXPECTO_HIP_CHECK(hipMemcpyAsync(&flag, h->ovf, sizeof(int), hipMemcpyDeviceToHost, st));
+  EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
+  if (!flag) return EXPECTO_OK;
+  EXPECTO_HIP_CHECK(hipMemsetAsync(h->ovf, 0, sizeof(int), st));
+  h->fallbacks += 1;
+  h->precision = EXPECTO_PRECISION_BF16X6;
+  rc = fn();
+  h->precision = EXPECTO_PRECISION_F16X3;
+  return rc;
 }
 }  // namespace
 
@@ -1085,12 +1293,14 @@ int expecto_beluga_forward_onehot(expecto_beluga_t h, const float* x, int n, flo
   EXPECTO_REQUIRE(x != nullptr && y != nullptr, "null input/output");
   EXPECTO_HIP_CHECK(hipSetDevice(h->device));
   hipStream_t st = as_stream(stream);
-  for (long long r0 = 0; r0 < n; r0 += h->max_batch) {
-    const int nb = (int)std::min<long long>(h->max_batch, n - r0);
-    int rc = forward_chunk(h, x, nullptr, 0, 0, 0, r0, nb, y + r0 * kNFeat, st);
-    if (rc) return rc;
-  }
-  return EXPECTO_OK;
+  return run_checked(h, st, [&]() {
+    for (long long r0 = 0; r0 < n; r0 += h->max_batch) {
+      const int nb = (int)std::min<long long>(h->max_batch, n - r0);
+      int rc = forward_chunk(h, x, nullptr, 0, 0, 0, r0, nb, y + r0 * kNFeat, st);
+      if (rc) return rc;
+    }
+    return (int)EXPECTO_OK;
+  });
 }
 
 int expecto_beluga_forward_codes(expecto_beluga_t h, const uint8_t* codes, int n, long long code_stride,
@@ -1104,12 +1314,14 @@ int expecto_beluga_forward_codes(expecto_beluga_t h, const uint8_t* codes, int n
   EXPECTO_HIP_CHECK(hipSetDevice(h->device));
   hipStream_t st = as_stream(stream);
   const long long rows = strand_mode == EXPECTO_STRAND_BOTH ? 2LL * n : n;
-  for (long long r0 = 0; r0 < rows; r0 += h->max_batch) {
-    const int nb = (int)std::min<long long>(h->max_batch, rows - r0);
-    int rc = forward_chunk(h, nullptr, codes, code_stride, n, strand_mode, r0, nb, y + r0 * kNFeat, st);
-    if (rc) return rc;
-  }
-  return EXPECTO_OK;
+  return run_checked(h, st, [&]() {
+    for (long long r0 = 0; r0 < rows; r0 += h->max_batch) {
+      const int nb = (int)std::min<long long>(h->max_batch, rows - r0);
+      int rc = forward_chunk(h, nullptr, codes, code_stride, n, strand_mode, r0, nb, y + r0 * kNFeat, st);
+      if (rc) return rc;
+    }
+    return (int)EXPECTO_OK;
+  });
 }
 
 int expecto_beluga_forward_segments(expecto_beluga_t h, const uint8_t* codes, int n_seg, int seg_len,
@@ -1122,8 +1334,11 @@ int expecto_beluga_forward_segments(expecto_beluga_t h, const uint8_t* codes, in
   EXPECTO_REQUIRE(codes && y && win_seg && win_off, "null argument");
   EXPECTO_REQUIRE(code_stride >= seg_len, "code_stride < seg_len");
   EXPECTO_HIP_CHECK(hipSetDevice(h->device));
-  return forward_segments(h, codes, n_seg, seg_len, code_stride, strand_mode, win_seg, win_off, win_row, n_win, y,
-                          as_stream(stream));
+  hipStream_t st = as_stream(stream);
+  return run_checked(h, st, [&]() {
+    return forward_segments(h, codes, n_seg, seg_len, code_stride, strand_mode, win_seg, win_off, win_row, n_win, y,
+                            st);
+  });
 }
 
 int expecto_beluga_forward_segment_pairs(expecto_beluga_t h, const uint8_t* codes, const int* var_pos,
@@ -1140,8 +1355,11 @@ int expecto_beluga_forward_segment_pairs(expecto_beluga_t h, const uint8_t* code
   EXPECTO_REQUIRE(strand_mode != EXPECTO_STRAND_BOTH || strand_stride >= n_win, "strand_stride < n_win");
   EXPECTO_HIP_CHECK(hipSetDevice(h->device));
   const SegPairs pr{var_pos, alt_code, y_alt, strand_stride};
-  return forward_segments(h, codes, n_seg, seg_len, code_stride, strand_mode, win_seg, win_off, win_row, n_win,
-                          y_ref, as_stream(stream), &pr);
+  hipStream_t st = as_stream(stream);
+  return run_checked(h, st, [&]() {
+    return forward_segments(h, codes, n_seg, seg_len, code_stride, strand_mode, win_seg, win_off, win_row, n_win,
+                            y_ref, st, &pr);
+  });
 }
 
 int expecto_beluga_forward_pairs(expecto_beluga_t h, const uint8_t* ref_codes, const uint8_t* alt_codes, int n,
@@ -1154,15 +1372,47 @@ int expecto_beluga_forward_pairs(expecto_beluga_t h, const uint8_t* ref_codes, c
   EXPECTO_REQUIRE(ref_codes && alt_codes && var_pos && y_ref && y_alt, "null argument");
   EXPECTO_REQUIRE(code_stride >= kLen, "code_stride < 2000");
   EXPECTO_HIP_CHECK(hipSetDevice(h->device));
-  return forward_pairs(h, ref_codes, alt_codes, n, code_stride, var_pos, strand_mode, y_ref, y_alt, strand_stride,
-                       as_stream(stream));
+  hipStream_t st = as_stream(stream);
+  return run_checked(h, st, [&]() {
+    return forward_pairs(h, ref_codes, alt_codes, n, code_stride, var_pos, strand_mode, y_ref, y_alt, strand_stride,
+                         st);
+  });
 }
 
 int expecto_beluga_set_precision(expecto_beluga_t h, int precision) {
   EXPECTO_REQUIRE(h != nullptr, "null handle");
-  EXPECTO_REQUIRE(precision == EXPECTO_PRECISION_FP32 || precision == EXPECTO_PRECISION_BF16X6, "bad precision");
+  EXPECTO_REQUIRE(precision == EXPECTO_PRECISION_FP32 || precision == EXPECTO_PRECISION_BF16X6 ||
+                      precision == EXPECTO_PRECISION_F16X3,
+                  "bad precision");
+  if (precision == EXPECTO_PRECISION_F16X3) {
+    EXPECTO_HIP_CHECK(hipSetDevice(h->device));
+    int rc = f16_prepare(h, nullptr);
+    if (rc) return rc;
+    EXPECTO_HIP_CHECK(hipStreamSynchronize(nullptr));
+  }
   h->precision = precision;
   return EXPECTO_OK;
+}
+
+int expecto_beluga_set_f16_target(expecto_beluga_t h, int target_log2) {
+  EXPECTO_REQUIRE(h != nullptr, "null handle");
+  EXPECTO_REQUIRE(target_log2 >= 0 && target_log2 <= 20, "target_log2 out of range");
+  EXPECTO_HIP_CHECK(hipSetDevice(h->device));
+  h->f16_target = target_log2;
+  if (!h->f16_ready) return EXPECTO_OK;   // applied by the first f16_prepare
+  const int saved = g_precision;
+  int rc = f16_calibrate(h, nullptr);
+  g_precision = saved;
+  if (rc) return rc;
+  EXPECTO_HIP_CHECK(hipStreamSynchronize(nullptr));
+  return EXPECTO_OK;
+}
+
+long long expecto_beluga_f16_fallbacks(expecto_beluga_t h, int* sx) {
+  if (!h) return EXPECTO_EINVAL;
+  if (sx)
+    for (int b = 0; b < 7; ++b) sx[b] = h->sx[b];
+  return h->fallbacks;
 }
 
 int expecto_beluga_get_precision(expecto_beluga_t h) { return h ? h->precision : EXPECTO_EINVAL; }

@@ -43,6 +43,9 @@ struct GemmArgs {
   const void* Bp;           // bf16x6 GEMM: B as bf16 planes [Npad][K/32][3][32] (split_planes)
   int linear_order;         // bf16x6 GEMM: blocks in dispatch order (no XCD grouping); FC1 sets it
                             // so every XCD sweeps the same K slab at once (Infinity-Cache reuse)
+  const float* col_scale;   // f16x3: per-column 2^-(s_in + s_w[n]) undoing the operand scales (else null)
+  float out_scale;          // f16x3: 2^s_out applied to stored activations (next layer's input scale)
+  int* ovf;                 // f16x3: set to 1 when a stored activation does not fit fp16
 };
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -69,26 +72,83 @@ __device__ __forceinline__ void split3(const floatx4 x, bf16x4& h, bf16x4& m, bf
   }
 }
 
-// Activation storage.  fp32 path: row-major [rows][ld] floats.  bf16x6 path ("x3"): bf16
-// planes [rows][ld/32][3][32] -- each 32-channel block of a row holds its x0, x1, x2 planes
-// back to back (192 B), so a consumer's 32-deep K block is one contiguous 192-B run per row.
-__device__ __forceinline__ long long x3_index(long long row, long long ld, int n) {
-  return ((row * (ld >> 5) + (n >> 5)) * 3) * 32 + (n & 31);
+// Activation storage formats (FMT):
+//   0  fp32 rows [rows][ld];
+//   1  bf16x6 path: bf16 planes [rows][ld/32][3][32] -- each 32-channel block of a row holds its
+//      x0, x1, x2 planes back to back (192 B), so a consumer's 32-deep K block is one contiguous
+//      192-B run per row;
+//   2  f16x3 path: fp16 planes [rows][ld/32][2][32] of the SCALED value x * 2^s (x = hi + lo,
+//      128 B per 32-channel block).  s is the consumer layer's input scale (calibrated per
+//      handle so that activations sit well inside fp16's exponent range); a value that does not
+//      fit (|x * 2^s| >= 65504) raises the handle's overflow flag and the call is recomputed
+//      on the bf16x6 path.
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+typedef _Float16 halfx4 __attribute__((ext_vector_type(4)));
+
+template <int PL>
+__device__ __forceinline__ long long act_index(long long row, long long ld, int n) {
+  return ((row * (ld >> 5) + (n >> 5)) * PL) * 32 + (n & 31);
+}
+__device__ __forceinline__ long long x3_index(long long row, long long ld, int n) { return act_index<3>(row, ld, n); }
+
+// 2-way fp16 split of an (already scaled) fp32 value.  r = RNE16(x) + RNE16(x - RNE16(x)) is x
+// rounded to >= 22 significant bits and is exact in fp32; the stored pair is the CANONICAL
+// split of r, hi = RNE16(r), lo = r - hi (exact in fp16).  The pair then depends on r alone, so
+// re-splitting a recovered value (max pooling of stored rows on the segment path) reproduces
+// the pair the per-window path stores for the same value -- bit-identical paths.  (Without the
+// second step a tie |lo| = ulp(hi)/2 re-splits to (hi +- ulp, -lo): same value, other products.)
+__device__ __forceinline__ void split_h2(const float x, _Float16& hi, _Float16& lo) {
+  const _Float16 h0 = (_Float16)x;
+  const float r = (float)h0 + (float)(_Float16)(x - (float)h0);
+  hi = (_Float16)r;
+  lo = (_Float16)(r - (float)hi);
 }
 
-template <bool X3>
-__device__ __forceinline__ void store_act(float* C, long long row, long long ld, int n, float v) {
-  if constexpr (X3) {
-    __bf16* d = reinterpret_cast<__bf16*>(C) + x3_index(row, ld, n);
+template <int FMT>
+__device__ __forceinline__ void store_act(float* C, long long row, long long ld, int n, float v, float osc = 1.f,
+                                          int* ovf = nullptr) {
+  if constexpr (FMT == 1) {
+    __bf16* d = reinterpret_cast<__bf16*>(C) + act_index<3>(row, ld, n);
     split1(v, d[0], d[32], d[64]);
+  } else if constexpr (FMT == 2) {
+    const float x = v * osc;
+    if (!(fabsf(x) < 65504.f) && ovf) *ovf = 1;
+    _Float16* d = reinterpret_cast<_Float16*>(C) + act_index<2>(row, ld, n);
+    split_h2(x, d[0], d[32]);
   } else {
     C[row * ld + n] = v;
   }
 }
 
+// value as stored (fmt 2: still scaled -- max pooling commutes with the power-of-2 scale)
+template <int FMT>
+__device__ __forceinline__ float load_act(const float* A, long long row, long long ld, int n) {
+  if constexpr (FMT == 1) {
+    const __bf16* s = reinterpret_cast<const __bf16*>(A) + act_index<3>(row, ld, n);
+    return (float)s[0] + ((float)s[32] + (float)s[64]);   // exact: recovers the split value
+  } else if constexpr (FMT == 2) {
+    const _Float16* s = reinterpret_cast<const _Float16*>(A) + act_index<2>(row, ld, n);
+    return (float)s[0] + (float)s[32];                      // exact (22 significant bits)
+  } else {
+    return A[row * ld + n];
+  }
+}
 __device__ __forceinline__ float load_x3(const float* A, long long row, long long ld, int n) {
-  const __bf16* s = reinterpret_cast<const __bf16*>(A) + x3_index(row, ld, n);
-  return (float)s[0] + ((float)s[32] + (float)s[64]);   // exact: recovers the split value
+  return load_act<1>(A, row, ld, n);
+}
+
+// runtime-format helpers for the small kernels (conv1, pooling, FC1 reduce)
+__device__ __forceinline__ void store_act_rt(int fmt, float* C, long long row, long long ld, int n, float v,
+                                             float osc = 1.f, int* ovf = nullptr) {
+  if (fmt == 1)
+    store_act<1>(C, row, ld, n, v);
+  else if (fmt == 2)
+    store_act<2>(C, row, ld, n, v, osc, ovf);
+  else
+    store_act<0>(C, row, ld, n, v);
+}
+__device__ __forceinline__ float load_act_rt(int fmt, const float* A, long long row, long long ld, int n) {
+  return fmt == 1 ? load_act<1>(A, row, ld, n) : fmt == 2 ? load_act<2>(A, row, ld, n) : load_act<0>(A, row, ld, n);
 }
 
 // Epilogue shared by both GEMM kernels. C/D layout of 32x32 MFMA (every dtype on gfx950):
@@ -441,8 +501,18 @@ __global__ __launch_bounds__(64 * WM, MINB * WM / 4) void beluga_gemm_x6(GemmArg
 constexpr int X6P_BM = 256;
 constexpr int X6P_B_PLANE = GBN * 64;                     // 10 KB
 constexpr int X6P_A_PLANE = X6P_BM * 64;                  // 16 KB
-constexpr int X6P_A_BYTES = 3 * X6P_A_PLANE;
-constexpr int X6P_STAGE = X6P_A_BYTES + 3 * X6P_B_PLANE + 2048;   // 81,920 B
+
+// Stage bytes for PL operand planes: A planes + B planes (+ room for the B pieces' dummy tail).
+template <int PL>
+struct PlaneGeo {
+  static constexpr int A_BYTES = PL * X6P_A_PLANE;
+  static constexpr int B_GROUPS = PL * 10;                  // 1 KiB B pieces (16 rows x 64 B)
+  static constexpr int B_PER_WAVE = (B_GROUPS + 3) / 4;     // 8 (PL 3: 30 real + 2 dummies) / 5
+  static constexpr int STAGE = A_BYTES + 4 * B_PER_WAVE * 1024;   // 81,920 / 53,248 B
+  static constexpr int A_PIECES = 4 * PL;                   // per wave and stage
+  static constexpr int ROW_KB = 64 * PL;                    // global bytes per row and 32-deep K block
+};
+constexpr int X6P_STAGE = PlaneGeo<3>::STAGE;
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
@@ -459,7 +529,7 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
 // XOR swizzle on the SOURCE offset, undone on the read: position = chunk ^ (-(row >> 2) & 3).
 typedef float floatx4v __attribute__((ext_vector_type(4)));
 
-template <int EPI, bool X3>
+template <int EPI, int FMT>
 __device__ __forceinline__ void gemm_epilogue16(const GemmArgs& p, const floatx4v (&acc)[4][10], long long mw, int n0,
                                                 int ks, int lane) {
   const int fr = lane & 15, fq = lane >> 4;
@@ -468,6 +538,8 @@ __device__ __forceinline__ void gemm_epilogue16(const GemmArgs& p, const floatx4
     const int n = n0 + nb * 16 + fr;
     if (n >= p.n_store) continue;
     const float bn = (EPI == EPI_PARTIAL) ? 0.f : p.bias[n];
+    // f16x3: acc * 2^-(s_in + s_w[n]) is exact (power of 2), so the value equals the unscaled sum
+    const float cs = (FMT == 2 && EPI != EPI_PARTIAL) ? p.col_scale[n] : 1.f;
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb) {
       const long long m4 = mw + mb * 16 + 4 * fq;   // first of this lane's 4 rows (multiple of 4)
@@ -481,8 +553,9 @@ __device__ __forceinline__ void gemm_epilogue16(const GemmArgs& p, const floatx4
         const long long w = m4 / p.s_in;
         const int tp = (int)(m4 - w * p.s_in) >> 2;
         if (tp >= p.t_valid) continue;
-        const float mx = fmaxf(fmaxf(acc[mb][nb][0], acc[mb][nb][1]), fmaxf(acc[mb][nb][2], acc[mb][nb][3]));
-        store_act<X3>(p.C, w * p.s_out + tp, p.ldc, n, fmaxf(mx + bn, 0.f));
+        float mx = fmaxf(fmaxf(acc[mb][nb][0], acc[mb][nb][1]), fmaxf(acc[mb][nb][2], acc[mb][nb][3]));
+        if (FMT == 2) mx *= cs;
+        store_act<FMT>(p.C, w * p.s_out + tp, p.ldc, n, fmaxf(mx + bn, 0.f), p.out_scale, p.ovf);
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -491,22 +564,50 @@ __device__ __forceinline__ void gemm_epilogue16(const GemmArgs& p, const floatx4
           const long long w = m / p.s_in;
           const int tpos = (int)(m - w * p.s_in);
           if (tpos >= p.t_valid) continue;
-          const float v = acc[mb][nb][j] + bn;
+          const float a = FMT == 2 ? acc[mb][nb][j] * cs : acc[mb][nb][j];
+          const float v = a + bn;
           const long long orow = p.c_rows ? p.c_rows[m] : (w * p.s_out + tpos);
           if (EPI == EPI_SIGMOID)
             p.C[orow * p.ldc + n] = 1.0f / (1.0f + expf(-v));
           else
-            store_act<X3>(p.C, orow, p.ldc, n, fmaxf(v, 0.f));
+            store_act<FMT>(p.C, orow, p.ldc, n, fmaxf(v, 0.f), p.out_scale, p.ovf);
         }
       }
     }
   }
 }
 
-template <int LAYER, int EPI, int TM = 0>
-__global__ __launch_bounds__(256, 1) void beluga_gemm_x6q(GemmArgs p) {
-  __shared__ __attribute__((aligned(1024))) char smem[2 * X6P_STAGE];
+// Products of one (16-row, 16-col, 32-deep) unit, smallest terms first, into one fp32 accumulator.
+//   PL 3 (bf16x6): x = x0 + x1 + x2 (bf16), the six products of combined order <= 2;
+//   PL 2 (f16x3):  x = hi + lo (fp16, operands pre-scaled), hi*hi + hi*lo + lo*hi (lo*lo, at
+//                  2^-22 relative, dropped).  Every product is exact in fp32 in both forms.
+template <int PL>
+__device__ __forceinline__ floatx4v planes_mfma(floatx4v c, const bf16x8 (&a)[3], const bf16x8 (&b)[3]) {
+  if constexpr (PL == 3) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
+  } else {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8, a[1]), __builtin_bit_cast(halfx8, b[0]), c,
+                                               0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8, a[0]), __builtin_bit_cast(halfx8, b[1]), c,
+                                               0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8, a[0]), __builtin_bit_cast(halfx8, b[0]), c,
+                                               0, 0, 0);
+  }
+  return c;
+}
 
+// Body of the planes GEMM (PL operand planes per value; see beluga_gemm_x6q / beluga_gemm_h3q),
+// NS-stage LDS ring: the loads of stage s + NS - 1 are in flight while stage s computes.
+template <int LAYER, int EPI, int TM, int PL, int NS>
+__device__ __forceinline__ void gemm_planes_body(const GemmArgs& p, char* smem) {
+  static_assert(NS == 2 || (NS == 3 && PL == 2), "3-stage ring only fits the 2-plane stage in LDS");
+  using G = PlaneGeo<PL>;
+  constexpr int FMT = PL == 3 ? 1 : 2;
   const unsigned nblk = gridDim.x, bid = blockIdx.x;
   const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
   const unsigned lin =
@@ -535,7 +636,7 @@ __global__ __launch_bounds__(256, 1) void beluga_gemm_x6q(GemmArgs p) {
   // Sources = uniform 64-bit base + constant 32-bit lane offset (global_load_lds saddr form:
   // a stage only moves the scalar base).  FC1's row gather (a_rows) keeps 64-bit lane addresses.
   constexpr bool kGather = (LAYER == 7);
-  const char* Ab = (const char*)p.A + (kGather ? 0 : m0 * lda_kb * 192);
+  const char* Ab = (const char*)p.A + (kGather ? 0 : m0 * lda_kb * G::ROW_KB);
   unsigned aoff[4];
   const char* aptr[4];
 #pragma unroll
@@ -545,21 +646,21 @@ __global__ __launch_bounds__(256, 1) void beluga_gemm_x6q(GemmArgs p) {
     if (m > p.M - 1) m = p.M - 1;
     const int c = (lane & 3) ^ swz(r);
     if (kGather) {
-      aptr[j] = (const char*)p.A + (p.a_rows ? p.a_rows[m] / GBK : m * lda_kb) * 192 + 16 * c;
+      aptr[j] = (const char*)p.A + (p.a_rows ? p.a_rows[m] / GBK : m * lda_kb) * G::ROW_KB + 16 * c;
       aoff[j] = 0;
     } else {
       aptr[j] = nullptr;
-      aoff[j] = (unsigned)((m - m0) * lda_kb * 192 + 16 * c);
+      aoff[j] = (unsigned)((m - m0) * lda_kb * G::ROW_KB + 16 * c);
     }
   }
-  const char* Bb = (const char*)p.Bp + ((long long)n0 * kb_total + gs0) * 192;
-  unsigned boff[8];
+  const char* Bb = (const char*)p.Bp + ((long long)n0 * kb_total + gs0) * G::ROW_KB;
+  unsigned boff[G::B_PER_WAVE];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int g = min(wave + 4 * j, 29);
+  for (int j = 0; j < G::B_PER_WAVE; ++j) {
+    const int g = min(wave + 4 * j, G::B_GROUPS - 1);
     const int pl = g / 10, r = 16 * (g % 10) + (lane >> 2);
     const int c = (lane & 3) ^ swz(r);
-    boff[j] = (unsigned)((long long)r * kb_total * 192 + pl * 64 + 16 * c);
+    boff[j] = (unsigned)((long long)r * kb_total * G::ROW_KB + pl * 64 + 16 * c);
   }
   // buffer_load ... lds: 128-bit resource from uniform values, the constant lane offset in
   // voffset and the stage offset in soffset (no per-stage vector address arithmetic)
@@ -569,8 +670,8 @@ __global__ __launch_bounds__(256, 1) void beluga_gemm_x6q(GemmArgs p) {
     if constexpr ((TM & 8) != 0) s = 0;
     const int gs = gs0 + s;
     const int chunk = gs / p.taps, tap = gs - chunk * p.taps;
-    const long long ao = ((long long)tap * lda_kb + chunk) * 192;
-    char* base = smem + buf * X6P_STAGE;
+    const long long ao = ((long long)tap * lda_kb + chunk) * G::ROW_KB;
+    char* base = smem + buf * G::STAGE;
     for (int i = i0; i < i0 + ni; ++i) {
       char* dst = base + (i / 4) * X6P_A_PLANE + (wave * 4 + i % 4) * 1024;
       if (kGather)
@@ -582,10 +683,10 @@ __global__ __launch_bounds__(256, 1) void beluga_gemm_x6q(GemmArgs p) {
   };
   auto issue_b = [&](int s, int buf, int j0, int nj) {
     if constexpr ((TM & 8) != 0) s = 0;
-    char* base = smem + buf * X6P_STAGE + X6P_A_BYTES;
+    char* base = smem + buf * G::STAGE + G::A_BYTES;
     for (int j = j0; j < j0 + nj; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + (wave + 4 * j) * 1024), 16, boff[j],
-                                               (unsigned)(s * 192), 0, 0);
+                                               (unsigned)(s * G::ROW_KB), 0, 0);
   };
 
   floatx4v acc[4][10];
@@ -599,41 +700,213 @@ __global__ __launch_bounds__(256, 1) void beluga_gemm_x6q(GemmArgs p) {
   const int fr = lane & 15, fq = lane >> 4;
   const int coff = 16 * (fq ^ swz(fr));            // swizzled chunk of this lane (row & 15 = fr)
   const int arow = (wave * 64 + fr) * 64 + coff;
-  const int brow = X6P_A_BYTES + fr * 64 + coff;
+  const int brow = G::A_BYTES + fr * 64 + coff;
   const int nk = p.kper / GBK;
 
   auto read_a = [&](const char* base, bf16x8 (&a)[4][3]) {
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb) {
       const char* ar = base + arow + mb * 16 * 64;
-      a[mb][0] = *(const bf16x8*)(ar);
-      a[mb][1] = *(const bf16x8*)(ar + X6P_A_PLANE);
-      a[mb][2] = *(const bf16x8*)(ar + 2 * X6P_A_PLANE);
+#pragma unroll
+      for (int pl = 0; pl < PL; ++pl) a[mb][pl] = *(const bf16x8*)(ar + pl * X6P_A_PLANE);
     }
   };
   auto read_b = [&](const char* base, int nb, bf16x8 (&b)[3]) {
     const char* br = base + brow + nb * 16 * 64;
-    b[0] = *(const bf16x8*)(br);
-    b[1] = *(const bf16x8*)(br + X6P_B_PLANE);
-    b[2] = *(const bf16x8*)(br + 2 * X6P_B_PLANE);
+#pragma unroll
+    for (int pl = 0; pl < PL; ++pl) b[pl] = *(const bf16x8*)(br + pl * X6P_B_PLANE);
   };
   auto unit = [&](const bf16x8 (&a)[4][3], int nb, const bf16x8 (&b)[3]) {
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) {
-      floatx4v c = acc[mb][nb];
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mb][2], b[0], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mb][1], b[1], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mb][0], b[2], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mb][1], b[0], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mb][0], b[1], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mb][0], b[0], c, 0, 0, 0);
-      acc[mb][nb] = c;
-    }
+    for (int mb = 0; mb < 4; ++mb) acc[mb][nb] = planes_mfma<PL>(acc[mb][nb], a[mb], b);
   };
-  // 24 MFMAs (16 cycles each) per unit; up to 2 LDS-DMA pieces, 1 LDS read, 1 VALU per slot
+  // NM MFMAs (16 cycles each) per unit; up to 2 LDS-DMA pieces, 1 LDS read, 1 VALU per slot
+  constexpr int NM = PL == 3 ? 24 : 12;
   auto pin = [&](int nv) {
 #pragma unroll
-    for (int i = 0; i < 24; ++i) {
+    for (int i = 0; i < NM; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if ((i % 6) == 0 && i < 6 * nv) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      if ((i & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+    }
+  };
+  // per stage and wave: A_PIECES A pieces over the first units, then B_PER_WAVE B pieces
+  constexpr int A_UNITS = G::A_PIECES / 2;          // 2 A pieces per unit: units 0 .. A_UNITS-1
+  constexpr int B_PER_UNIT = (G::B_PER_WAVE + (10 - A_UNITS) - 1) / (10 - A_UNITS);
+
+  issue_a(0, 0, 0, G::A_PIECES);
+  issue_b(0, 0, 0, G::B_PER_WAVE);
+  if constexpr (NS == 3) {
+    issue_a(min(1, nk - 1), 1, 0, G::A_PIECES);
+    issue_b(min(1, nk - 1), 1, 0, G::B_PER_WAVE);
+    asm volatile("s_waitcnt vmcnt(13)" ::: "memory");   // stage 0 landed (13 = pieces per stage)
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  bf16x8 as[4][3];
+  read_a(smem, as);
+  int buf = 0;
+  for (int s = 0; s < nk; ++s) {
+    const int nbuf = buf + 1 == NS ? 0 : buf + 1;             // stage s + 1
+    const int lbuf = NS == 2 ? nbuf : (nbuf + 1 == NS ? 0 : nbuf + 1);   // stage s + NS - 1
+    const int sn = (TM & 2) ? s : min(s + NS - 1, nk - 1);
+    const char* base = smem + buf * G::STAGE;
+    const char* nbase = smem + nbuf * G::STAGE;
+    const bool go = !(TM & 2);
+    bf16x8 b0[3], b1[3];
+    read_b(base, 0, b0);
+#pragma unroll
+    for (int nb = 0; nb < 10; ++nb) {
+      int nv = 0;
+      if (go && nb < A_UNITS) {
+        issue_a(sn, lbuf, 2 * nb, 2);
+        nv = 2;
+      }
+      if (go && nb >= A_UNITS) {
+        const int j0 = (nb - A_UNITS) * B_PER_UNIT;
+        const int nj = min(B_PER_UNIT, G::B_PER_WAVE - j0);
+        if (nj > 0) {
+          issue_b(sn, lbuf, j0, nj);
+          nv = nj;
+        }
+      }
+      if (nb + 1 < 10) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
+      unit(as, nb, (nb & 1) ? b1 : b0);
+      pin(nv);
+    }
+    // A of stage s+1 (this wave's A pieces, older than its B pieces) replaces A(s) while the
+    // last unit's MFMAs drain
+    if constexpr (!(TM & 2)) {
+      if constexpr (NS == 3)
+        asm volatile("s_waitcnt vmcnt(13)" ::: "memory");   // all of stage s+1 (s+2 in flight)
+      else if constexpr (G::B_PER_WAVE == 8)
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    }
+    read_a(nbase, as);
+    if constexpr (!(TM & 4)) {
+      if constexpr (NS == 3)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    asm volatile("" ::: "memory");
+    buf = nbuf;
+  }
+  gemm_epilogue16<EPI, FMT>(p, acc, m0 + wave * 64, n0, ks, lane);
+}
+
+// ---- f16x3 conv GEMM with the Toeplitz A tile staged once per channel chunk -------------
+// For a k=8 conv the 8 taps of one 32-channel chunk read A rows m0+tap .. m0+tap+255: the same
+// 263 rows shifted by one.  gemm_planes_body re-stages them for every tap (8x the A traffic);
+// here the chunk's 288-row A slab (2 planes, 36 KB) is staged ONCE into a double-buffered slab
+// and the 8 tap stages read it at row offset +tap, while B (the weights of one (chunk, tap)
+// K-block, 20 KB) streams through a 3-deep ring.  A of chunk c+1 is fetched during chunk c
+// (9 pieces per wave, one or two per tap, issued before that stage's B pieces so a uniform
+// vmcnt(5) at every stage end covers it).  Same operands, products and k order as
+// gemm_planes_body<PL=2>: results are bitwise identical.
+// LDS: 2 x 36,864 (A slabs) + 3 x 20,480 (B ring) = 135,168 B.
+constexpr int H3C_AROWS = 288;                         // 256 + 7 rows needed, 18 groups of 16
+constexpr int H3C_APLANE = H3C_AROWS * 64;             // 18,432 B
+constexpr int H3C_ASLAB = 2 * H3C_APLANE;              // 36,864 B
+constexpr int H3C_BSTAGE = 2 * X6P_B_PLANE;            // 20,480 B
+constexpr int H3C_LDS = 2 * H3C_ASLAB + 3 * H3C_BSTAGE;
+
+template <int LAYER, int EPI, int TM>
+__device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem) {
+  constexpr int ROW_KB = 128;                         // global bytes per row and 32-channel block
+  const unsigned nblk = gridDim.x, bid = blockIdx.x;
+  const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
+  const unsigned lin = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int nt = (int)(lin % (unsigned)p.n_tiles);
+  const long long mt = (long long)(lin / (unsigned)p.n_tiles) % p.m_tiles;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const long long m0 = mt * X6P_BM;
+  const int n0 = nt * GBN;
+  const int kb_total = (int)(p.ldb / GBK);
+  const long long lda_kb = p.lda / GBK;
+  const int nchunk = (int)lda_kb;                     // Cin / 32
+  const int nk = nchunk * 8;
+  auto swz = [](int r) { return (-(r >> 2)) & 3; };
+  // A slab pieces: P = wave + 4*i (i < 9) of 36 = 18 row groups x 2 planes
+  const char* Ab = (const char*)p.A + m0 * lda_kb * ROW_KB;
+  const long long last_row = p.M - 1 + 7;             // Toeplitz rows read by the last output row
+  unsigned aoff[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int P = wave + 4 * i, g = P >> 1, pl = P & 1;
+    const int r = 16 * g + (lane >> 2);
+    const long long m = min(m0 + r, last_row);
+    const int c = (lane & 3) ^ swz(r);
+    aoff[i] = (unsigned)((m - m0) * lda_kb * ROW_KB + pl * 64 + 16 * c);
+  }
+  const char* Bb = (const char*)p.Bp + (long long)n0 * kb_total * ROW_KB;
+  unsigned boff[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int g = wave + 4 * j;                        // 20 pieces: plane g / 10, cols 16*(g % 10)
+    const int pl = g / 10, r = 16 * (g % 10) + (lane >> 2);
+    const int c = (lane & 3) ^ swz(r);
+    boff[j] = (unsigned)((long long)r * kb_total * ROW_KB + pl * 64 + 16 * c);
+  }
+  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, 0x7fffffff, 0x00020000);
+  char* const aslab = smem;
+  char* const bring = smem + 2 * H3C_ASLAB;
+  auto issue_a = [&](int chunk, int i0, int ni) {      // pieces i0.. of chunk's slab
+    char* base = aslab + (chunk & 1) * H3C_ASLAB;
+    for (int i = i0; i < i0 + ni; ++i) {
+      const int P = wave + 4 * i;
+      char* dst = base + (P & 1) * H3C_APLANE + (P >> 1) * 1024;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (lds_void*)dst, 16, aoff[i], (unsigned)(chunk * ROW_KB), 0, 0);
+    }
+  };
+  auto issue_b = [&](int s, int slot) {
+    if constexpr ((TM & 8) != 0) s = 0;
+    char* base = bring + slot * H3C_BSTAGE;
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + (wave + 4 * j) * 1024), 16, boff[j],
+                                               (unsigned)(s * ROW_KB), 0, 0);
+  };
+
+  floatx4v acc[4][10];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 10; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[mb][nb][r] = 0.f;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int brow = fr * 64 + 16 * (fq ^ swz(fr));
+  // A fragment of (row group mb, tap t): slab row wave*64 + mb*16 + fr + t
+  auto read_a = [&](const char* slab, int t, bf16x8 (&a)[4][3]) {
+    const int rr2 = fr + t;
+    const int off = (wave * 64 + rr2) * 64 + 16 * (fq ^ swz(rr2));
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      a[mb][0] = *(const bf16x8*)(slab + off + mb * 1024);
+      a[mb][1] = *(const bf16x8*)(slab + off + mb * 1024 + H3C_APLANE);
+    }
+  };
+  auto read_b = [&](const char* base, int nb, bf16x8 (&b)[3]) {
+    const char* br = base + brow + nb * 1024;
+    b[0] = *(const bf16x8*)(br);
+    b[1] = *(const bf16x8*)(br + X6P_B_PLANE);
+  };
+  auto unit = [&](const bf16x8 (&a)[4][3], int nb, const bf16x8 (&b)[3]) {
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) acc[mb][nb] = planes_mfma<2>(acc[mb][nb], a[mb], b);
+  };
+  auto pin = [&](int nv) {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       if ((i % 6) == 0 && i < 6 * nv) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
       if ((i & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
@@ -641,42 +914,75 @@ __global__ __launch_bounds__(256, 1) void beluga_gemm_x6q(GemmArgs p) {
     }
   };
 
-  issue_a(0, 0, 0, 12);
-  issue_b(0, 0, 0, 8);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // prologue: slab 0, B stages 0 and 1
+  issue_a(0, 0, 9);
+  issue_b(0, 0);
+  issue_b(min(1, nk - 1), 1);
+  asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   bf16x8 as[4][3];
-  read_a(smem, as);
-  for (int s = 0; s < nk; ++s) {
-    const int buf = s & 1;
-    const int sn = (TM & 2) ? s : min(s + 1, nk - 1);
-    const char* base = smem + buf * X6P_STAGE;
-    const char* nbase = smem + (buf ^ 1) * X6P_STAGE;
-    const bool go = !(TM & 2);
-    bf16x8 b0[3], b1[3];
-    read_b(base, 0, b0);
+  read_a(aslab, 0, as);
+  int slot = 0;
+  for (int c = 0; c < nchunk; ++c) {
+    const char* slab = aslab + (c & 1) * H3C_ASLAB;
+    const bool more_a = (c + 1 < nchunk) && !(TM & 2);
+    for (int t = 0; t < 8; ++t) {
+      const int s = c * 8 + t;
+      const int nslot = slot + 1 == 3 ? 0 : slot + 1;
+      const int lslot = nslot + 1 == 3 ? 0 : nslot + 1;     // stage s + 2
+      const char* base = bring + slot * H3C_BSTAGE;
+      bf16x8 b0[3], b1[3];
+      read_b(base, 0, b0);
 #pragma unroll
-    for (int nb = 0; nb < 10; ++nb) {
-      // glds: 12 A pieces over units 0..5, 8 B pieces over units 6..9
-      if (go && nb < 6) issue_a(sn, buf ^ 1, 2 * nb, 2);
-      if (go && nb >= 6) issue_b(sn, buf ^ 1, 2 * (nb - 6), 2);
-      if (nb + 1 < 10) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
-      unit(as, nb, (nb & 1) ? b1 : b0);
-      pin(2);
+      for (int nb = 0; nb < 10; ++nb) {
+        int nv = 0;
+        if (nb == 0 && more_a) {               // slab c+1: pieces 0,1 at tap 0, piece t+1 at taps 1..7
+          issue_a(c + 1, t == 0 ? 0 : t + 1, t == 0 ? 2 : 1);
+          nv = t == 0 ? 2 : 1;
+        }
+        if (nb == 2 && !(TM & 2)) {
+          issue_b(min(s + 2, nk - 1), lslot);
+          nv = 2;
+        }
+        if (nb + 1 < 10) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
+        unit(as, nb, (nb & 1) ? b1 : b0);
+        pin(nv);
+      }
+      if (t < 7) read_a(slab, t + 1, as);     // same slab: already resident
+      if constexpr (!(TM & 4)) {
+        asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");   // all but B(s+2): B(s+1), slab c+1
+        __builtin_amdgcn_s_barrier();
+      }
+      asm volatile("" ::: "memory");
+      slot = nslot;
     }
-    // A of stage s+1 (this wave's 12 pieces, older than its 8 B pieces) replaces A(s) while
-    // the last unit's MFMAs drain
-    if constexpr (!(TM & 2)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    read_a(nbase, as);
-    if constexpr (!(TM & 4)) {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-    asm volatile("" ::: "memory");
+    if (c + 1 < nchunk) read_a(aslab + ((c + 1) & 1) * H3C_ASLAB, 0, as);
   }
-  (void)fr;
-  gemm_epilogue16<EPI, true>(p, acc, m0 + wave * 64, n0, ks, lane);
+  gemm_epilogue16<EPI, 2>(p, acc, m0 + wave * 64, n0, 0, lane);
+}
+
+// ---- the library's split-operand GEMMs (both on 16x16x32 MFMAs, LDS-DMA staged) ---------
+// beluga_gemm_x6q: bf16x6 (3 bf16 planes, 6 products): fp32-faithful over fp32's whole range.
+// beluga_gemm_h3q: f16x3 (2 fp16 planes of pre-scaled operands, 3 products): 22-bit operands,
+//                  half the MFMA work; needs the calibrated scales (col_scale / out_scale).
+template <int LAYER, int EPI, int TM = 0>
+__global__ __launch_bounds__(256, 1) void beluga_gemm_x6q(GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * PlaneGeo<3>::STAGE];
+  gemm_planes_body<LAYER, EPI, TM, 3, 2>(p, smem);
+}
+
+template <int LAYER, int EPI, int TM = 0, int NS = 3>
+__global__ __launch_bounds__(256, 1) void beluga_gemm_h3q(GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[NS * PlaneGeo<2>::STAGE];
+  gemm_planes_body<LAYER, EPI, TM, 2, NS>(p, smem);
+}
+
+// f16x3 conv layers (taps == 8, no split-K): the chunk-slab kernel above
+template <int LAYER, int EPI, int TM = 0>
+__global__ __launch_bounds__(256, 1) void beluga_conv_h3q(GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[H3C_LDS];
+  gemm_conv_h3_body<LAYER, EPI, TM>(p, smem);
 }
 
 // B planes for beluga_gemm_x6q from a K-contiguous fp32 B [rows][K] (K % 32 == 0).
@@ -691,6 +997,20 @@ __global__ void split_planes(const float* __restrict__ W, long long rows, int K,
   *(bf16x4*)d = h;
   *(bf16x4*)(d + GBK) = m;
   *(bf16x4*)(d + 2 * GBK) = l;
+}
+
+// f16x3 B planes: row n scaled by 2^s_w[n] (s_w from row_scale_exp), then split into fp16
+// hi/lo planes [n][K/32][2][32].
+__global__ void split_planes_h2(const float* __restrict__ W, long long rows, int K, const int* __restrict__ sw,
+                                _Float16* __restrict__ Bp) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * K / 4) return;
+  const long long e = 4 * i, n = e / K;
+  const int k = (int)(e - n * K), kb = k / GBK, j = k % GBK;
+  const floatx4 x = *(const floatx4*)(W + e);
+  _Float16* d = Bp + ((n * (K / GBK) + kb) * 2) * GBK + j;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) split_h2(ldexpf(x[t], sw[n]), d[t], d[GBK + t]);
 }
 
 }  // namespace expecto

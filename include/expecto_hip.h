@@ -54,14 +54,21 @@ enum {
                                (encodeSeqs row order, chromatin.py:170-171)             */
 };
 
-/* GEMM arithmetic (expecto_beluga_set_precision).  Both are fp32-accurate:
+/* GEMM arithmetic (expecto_beluga_set_precision).  All accumulate in fp32:
  *  FP32   exact fp32 products and accumulation (v_mfma_f32_32x32x2_f32);
  *  BF16X6 every fp32 operand split exactly into three bf16 terms, the six products of
- *         combined order <= 2 accumulated in fp32 (v_mfma_f32_32x32x16_bf16); representation
- *         error < 2^-24 relative, products exact -- default, ~1.4x faster. */
+ *         combined order <= 2 accumulated in fp32 (v_mfma_f32_16x16x32_bf16); representation
+ *         error < 2^-24 relative, products exact, over fp32's whole exponent range;
+ *  F16X3  operands scaled by powers of 2 (weights per output channel; activations per layer,
+ *         calibrated once per handle on a seeded batch) and split into two fp16 terms
+ *         (22 significant bits), three products per k (v_mfma_f32_16x16x32_f16) -- half the
+ *         MFMA work of BF16X6.  An activation that does not fit fp16 after scaling raises an
+ *         overflow flag and the whole call is recomputed with BF16X6 (counted by
+ *         expecto_beluga_f16_fallbacks), so F16X3 never returns a saturated result. */
 enum {
   EXPECTO_PRECISION_FP32 = 0,
   EXPECTO_PRECISION_BF16X6 = 1,
+  EXPECTO_PRECISION_F16X3 = 2,
 };
 
 /* Number of parameter tensors and their order (the reference state-dict keys,
@@ -141,8 +148,18 @@ int expecto_beluga_forward_segment_pairs(expecto_beluga_t h, const uint8_t* code
                                          int n_win, float* y_ref, float* y_alt, long long strand_stride,
                                          void* stream);
 
+/* Select the GEMM arithmetic for later calls.  The first switch to F16X3 builds the fp16
+ * weight planes and calibrates the activation scales (a BF16X6 forward of 256 seeded random
+ * windows; each layer's scale puts its largest calibration activation at 2^target_log2,
+ * default 10, leaving >= 2^5 of headroom below fp16's 65504 before the fallback). */
 int expecto_beluga_set_precision(expecto_beluga_t h, int precision);
 int expecto_beluga_get_precision(expecto_beluga_t h);
+/* F16X3 calibration target (log2 of the scaled calibration maximum, 0..20); re-derives the
+ * scales.  Tests use a large target to force the overflow fallback. */
+int expecto_beluga_set_f16_target(expecto_beluga_t h, int target_log2);
+/* F16X3 state: activation scale exponents of the 7 layer inputs (conv2..fc2) into sx[7];
+ * returns the number of calls recomputed with BF16X6 after an overflow (or < 0 on error). */
+long long expecto_beluga_f16_fallbacks(expecto_beluga_t h, int* sx);
 
 /* Per-layer device time accumulated over forward calls while profiling is on (ms), launches
  * (`calls`) and executed multiply-adds (`macs`: GEMM M x N x K actually run, including the

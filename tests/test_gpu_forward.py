@@ -10,7 +10,7 @@ from conftest import GOLDEN, assert_close
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["bf16x6", "fp32"])
+@pytest.fixture(scope="module", params=["bf16x6", "f16x3", "fp32"])
 def model(request):
     import torch
     from expecto_amd import beluga
@@ -80,7 +80,7 @@ def test_forward_dense_float_input_vs_cpu_oracle(model, cpu_sd):
 
 
 def test_accuracy_vs_float64(model, cpu_sd):
-    """Both GEMM precisions are fp32-accurate: error vs a float64 forward within 3x the
+    """Every GEMM precision is fp32-accurate: error vs a float64 forward within 3x the
     reference's own fp32 (oneDNN) error, on 9 random windows."""
     import torch
     from oracle.beluga_np import forward_torch_cpu
@@ -121,3 +121,53 @@ def test_load_state_dict_rebuilds_engine(model):
     c = model.forward(x)
     assert not torch.allclose(a, b)
     assert torch.allclose(b, c, atol=1e-6)
+
+
+def _f16_pair():
+    """An f16x3 engine and a bf16x6 engine on the same seeded weights."""
+    from expecto_amd import beluga
+    a = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=64).cuda()
+    b = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=64).cuda()
+    a.engine().set_precision("f16x3")
+    b.engine().set_precision("bf16x6")
+    return a, b
+
+
+def test_f16x3_calibration_and_no_fallback_on_genomic_windows():
+    """Calibrated scales keep ordinary windows inside fp16 (no fallback), and the f16x3 result
+    stays within the parity bar of the bf16x6 one."""
+    import torch
+    a, b = _f16_pair()
+    n0, sx = a.engine().f16_state()
+    assert len(sx) == 7 and all(-40 <= s <= 40 for s in sx), sx
+    rng = np.random.default_rng(5)
+    codes = torch.from_numpy(rng.integers(0, 5, (40, 2000)).astype(np.uint8)).cuda()
+    ya = a.forward_codes(codes, 2).cpu().numpy()
+    yb = b.forward_codes(codes, 2).cpu().numpy()
+    assert a.engine().f16_state()[0] == n0
+    assert_close(ya, yb, what="f16x3 vs bf16x6")
+
+
+def test_f16x3_overflow_recomputes_with_bf16x6():
+    """An activation that does not fit fp16 after scaling (here: inputs x 3e4 on the dense
+    one-hot path, then a calibration target that puts every layer at the edge) makes the call
+    fall back to bf16x6: the output equals the bf16x6 engine's bit for bit."""
+    import torch
+    a, b = _f16_pair()
+    rng = np.random.default_rng(6)
+    x = torch.from_numpy(rng.uniform(0, 3e4, (5, 4, 1, 2000)).astype(np.float32)).cuda()
+    n0 = a.engine().f16_state()[0]
+    ya = a.forward(x).cpu()
+    yb = b.forward(x).cpu()
+    assert a.engine().f16_state()[0] == n0 + 1
+    assert torch.equal(ya, yb)
+    a.engine().set_f16_target(20)
+    codes = torch.from_numpy(rng.integers(0, 4, (8, 2000)).astype(np.uint8)).cuda()
+    ya = a.forward_codes(codes, 0).cpu()
+    yb = b.forward_codes(codes, 0).cpu()
+    assert a.engine().f16_state()[0] == n0 + 2
+    assert torch.equal(ya, yb)
+    a.engine().set_f16_target(10)
+    ya = a.forward_codes(codes, 0).cpu()
+    assert a.engine().f16_state()[0] == n0 + 2
+    assert_close(ya.numpy(), yb.numpy(), what="f16x3 after re-calibration")

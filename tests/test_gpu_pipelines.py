@@ -102,7 +102,7 @@ def _engine(precision="bf16x6"):
     return eng
 
 
-@pytest.mark.parametrize("precision", ["bf16x6", "fp32"])
+@pytest.mark.parametrize("precision", ["bf16x6", "f16x3", "fp32"])
 def test_segment_path_is_bitwise_equal_to_per_window_variants(precision):
     """Trunk sharing across shifts (segment path) reproduces the per-window forward exactly."""
     import torch
@@ -161,7 +161,7 @@ def test_segment_path_is_bitwise_equal_to_per_window_tss():
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("precision", ["bf16x6", "fp32"])
+@pytest.mark.parametrize("precision", ["bf16x6", "f16x3", "fp32"])
 def test_pair_path_alt_cone_is_bitwise_equal(precision):
     """Alt-cone reuse (only the SNV's receptive-field rows recomputed) == full alt forward,
     for SNVs anywhere in the window, both strands."""
@@ -202,7 +202,7 @@ def test_variant_pipeline_pairs_equal_per_window():
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("precision", ["bf16x6", "fp32"])
+@pytest.mark.parametrize("precision", ["bf16x6", "f16x3", "fp32"])
 def test_segment_pairs_alt_runs_are_bitwise_equal(precision):
     """forward_segment_pairs == full forwards of every ref and alt window, for SNVs at the
     segment edges and in the middle, windows at the first/last offsets, both strands."""

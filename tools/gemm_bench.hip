@@ -47,6 +47,16 @@ Variant mk6q(const char* name) {
   return {name, X6P_BM, [](const GemmArgs& a, unsigned nblk) { beluga_gemm_x6q<L, EPI, TM><<<nblk, 256>>>(a); }};
 }
 
+template <int L, int EPI, int TM = 0, int NS = 3>
+Variant mkh3q(const char* name) {
+  return {name, X6P_BM, [](const GemmArgs& a, unsigned nblk) { beluga_gemm_h3q<L, EPI, TM, NS><<<nblk, 256>>>(a); }};
+}
+
+template <int L, int EPI, int TM = 0>
+Variant mkc3(const char* name) {
+  return {name, X6P_BM, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3q<L, EPI, TM><<<nblk, 256>>>(a); }};
+}
+
 template <int L, int EPI, int WM, int MINB, int BK, int PIPE = 0>
 Variant mk(const char* name) {
   return {name, 32 * WM, [](const GemmArgs& a, unsigned nblk) {
@@ -95,16 +105,45 @@ int main(int argc, char** argv) {
   __bf16* Xp;
   CK(hipMalloc(&Xp, xa * 6));
   split_planes<<<(unsigned)((xa / 4 + 255) / 256), 256>>>(X, (long long)(M + 64), sh.cin, Xp);
+  // f16x3 operands: unit scales (timing; weights' lo planes go subnormal, numerics are not the point)
+  int* zs;
+  const long long zrows = std::max<long long>(npad, M + 64);
+  CK(hipMalloc(&zs, zrows * 4));
+  CK(hipMemset(zs, 0, zrows * 4));
+  float* ones;
+  CK(hipMalloc(&ones, npad * 4));
+  {
+    std::vector<float> o(npad, 1.f);
+    CK(hipMemcpy(ones, o.data(), npad * 4, hipMemcpyHostToDevice));
+  }
+  _Float16 *Bh, *Xh;
+  CK(hipMalloc(&Bh, (size_t)npad * K * 4));
+  CK(hipMalloc(&Xh, xa * 4));
+  split_planes_h2<<<(unsigned)(((long long)npad * K / 4 + 255) / 256), 256>>>(W, npad, K, zs, Bh);
+  split_planes_h2<<<(unsigned)((xa / 4 + 255) / 256), 256>>>(X, (long long)(M + 64), sh.cin, zs, Xh);
+  int* ovf;
+  CK(hipMalloc(&ovf, 4));
+  CK(hipMemset(ovf, 0, 4));
   CK(hipDeviceSynchronize());
   // variant 0 is the reference for the bitwise comparison: x6 and x6d must agree exactly
   if (sh.pool) {
     vs.push_back(mk6<2, EPI_RELU_POOL4, 4, 1>("x6_wm4_b1"));
     vs.push_back(mk6q<2, EPI_RELU_POOL4>("x6q"));
+    vs.push_back(mkh3q<2, EPI_RELU_POOL4>("h3q"));
+    vs.push_back(mkc3<2, EPI_RELU_POOL4>("h3c"));
+    vs.push_back(mkc3<2, EPI_RELU_POOL4, 2>("h3c_noglds"));
+    vs.push_back(mkh3q<2, EPI_RELU_POOL4, 0, 2>("h3q_ns2"));
+    vs.push_back(mkh3q<2, EPI_RELU_POOL4, 2>("h3q_noglds"));
+    vs.push_back(mkh3q<2, EPI_RELU_POOL4, 4>("h3q_nobar"));
     vs.push_back(mk6q<2, EPI_RELU_POOL4, 2>("x6q_noglds"));
     vs.push_back(mk<2, EPI_RELU_POOL4, 4, 2, 32, 1>("f32_pipe"));
   } else {
     vs.push_back(mk6<3, EPI_RELU, 4, 1>("x6_wm4_b1"));
     vs.push_back(mk6q<3, EPI_RELU>("x6q"));
+    vs.push_back(mkh3q<3, EPI_RELU>("h3q"));
+    vs.push_back(mkc3<3, EPI_RELU>("h3c"));
+    vs.push_back(mkh3q<3, EPI_RELU, 0, 2>("h3q_ns2"));
+    vs.push_back(mkh3q<3, EPI_RELU, 2>("h3q_noglds"));
     vs.push_back(mk<3, EPI_RELU, 4, 2, 32, 1>("f32_pipe"));
   }
   auto args_for = [&](int bm, float* C) {
@@ -126,6 +165,13 @@ int main(int argc, char** argv) {
       CK(hipMemset(C, 0, v == 0 ? csz * 4 : csz * 6));
       GemmArgs a = args_for(vs[v].bm, C);
       if (vs[v].name.rfind("x6q", 0) == 0) a.A = (const float*)Xp;
+      if (vs[v].name.rfind("h3", 0) == 0) {
+        a.A = (const float*)Xh;
+        a.Bp = Bh;
+        a.col_scale = ones;
+        a.out_scale = 1.f;
+        a.ovf = ovf;
+      }
       unsigned nblk = (unsigned)(a.m_tiles * a.n_tiles);
       vs[v].launch(a, nblk);  // warm
       CK(hipEventRecord(e0));
@@ -136,7 +182,15 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       times[v].push_back(ms);
       if (r == 0) {
-        if (vs[v].name.rfind("x6q", 0) == 0) {   // decode planes
+        if (vs[v].name.rfind("h3", 0) == 0) {   // decode fp16 planes
+          std::vector<_Float16> pl(csz * 2);
+          CK(hipMemcpy(pl.data(), C, csz * 4, hipMemcpyDeviceToHost));
+          for (size_t i = 0; i < csz; ++i) {
+            const size_t row = i / sh.cout, n = i % sh.cout;
+            const size_t k = ((row * (sh.cout / 32) + n / 32) * 2) * 32 + n % 32;
+            out[i] = (float)pl[k] + (float)pl[k + 32];
+          }
+        } else if (vs[v].name.rfind("x6q", 0) == 0) {   // decode planes
           std::vector<uint16_t> pl(csz * 3);
           CK(hipMemcpy(pl.data(), C, csz * 6, hipMemcpyDeviceToHost));
           auto f = [](uint16_t b) { uint32_t u = (uint32_t)b << 16; float x; memcpy(&x, &u, 4); return x; };
