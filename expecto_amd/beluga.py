@@ -57,12 +57,13 @@ class BelugaEngine:
         self.device = device
         self.max_batch = max_batch
         import os
-        self.set_precision(os.environ.get("EXPECTO_PRECISION", "bf16x6"))
+        self.set_precision(os.environ.get("EXPECTO_PRECISION", "f16x3"))
 
     def set_precision(self, precision: str):
-        """GEMM arithmetic (include/expecto_hip.h): 'bf16x6' (fp32-faithful split-bf16 MFMA),
-        'f16x3' (scaled split-fp16, half the MFMA work, bf16x6 fallback on fp16 overflow) or
-        'fp32' (exact fp32 MFMA)."""
+        """GEMM arithmetic (include/expecto_hip.h): 'f16x3' (default: scaled split-fp16, half the
+        MFMA work of bf16x6, bf16x6 recompute on fp16 overflow), 'bf16x6' (split-bf16 over fp32's
+        whole range) or 'fp32' (exact fp32 MFMA).  All three are within the parity bar of the
+        float64 forward with the same margin as the exact-fp32 kernel (tools/accuracy_gpu.py)."""
         if precision not in _lib.PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(_lib.PRECISIONS)}")
         with torch.cuda.device(self.device):

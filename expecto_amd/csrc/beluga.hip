@@ -1266,6 +1266,9 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   }
   EXPECTO_HIP_CHECK(hipMemsetAsync(h->P, 0, act_alloc(pf) * sizeof(float), st));
   EXPECTO_HIP_CHECK(hipMemsetAsync(h->Q, 0, act_alloc(qf) * sizeof(float), st));
+  // default arithmetic: f16x3 (fp16 weight planes + activation-scale calibration now)
+  if ((rc = f16_prepare(h, st))) return fail(rc);
+  h->precision = EXPECTO_PRECISION_F16X3;
   EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
   *out = h;
   return EXPECTO_OK;

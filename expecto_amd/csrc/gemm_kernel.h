@@ -817,6 +817,59 @@ constexpr int H3C_ASLAB = 2 * H3C_APLANE;              // 36,864 B
 constexpr int H3C_BSTAGE = 2 * X6P_B_PLANE;            // 20,480 B
 constexpr int H3C_LDS = 2 * H3C_ASLAB + 3 * H3C_BSTAGE;
 
+// ReLU epilogue of the f16x3 conv kernel through LDS.  A wave's 64 x 160 tile is, per output
+// row, ONE contiguous 640-B run of the planes layout (5 blocks x [hi 64 B | lo 64 B]); the
+// accumulator layout scatters it over 2-byte pieces.  Each half of the tile (32 rows) is split
+// into the wave's private LDS area (row stride 656 B: the 4 row groups of a ds_write_b16 land
+// on distinct banks), then written out as 16-B chunks (20 per lane), each row fully coalesced.
+constexpr int H3E_ROW = 656;
+constexpr int H3E_WAVE = 32 * H3E_ROW;                 // 20,992 B per wave
+
+__device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const floatx4v (&acc)[4][10], long long mw,
+                                                     int n0, int lane, char* lds) {
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+#pragma unroll
+    for (int nb = 0; nb < 10; ++nb) {
+      const int n = n0 + nb * 16 + fr;
+      const float bn = n < p.n_store ? p.bias[n] : 0.f;
+      const float cs = n < p.n_store ? p.col_scale[n] : 0.f;
+#pragma unroll
+      for (int mh = 0; mh < 2; ++mh) {
+        const int mb = 2 * half + mh;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float x = fmaxf(acc[mb][nb][j] * cs + bn, 0.f) * p.out_scale;
+          if (!(fabsf(x) < 65504.f)) *p.ovf = 1;   // NaN/overflow: the call is recomputed
+          _Float16 hi, lo;
+          split_h2(x, hi, lo);
+          char* d = lds + (mh * 16 + 4 * fq + j) * H3E_ROW + (nb >> 1) * 128 + ((nb & 1) * 16 + fr) * 2;
+          *(_Float16*)d = hi;
+          *(_Float16*)(d + 64) = lo;
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const long long ldb = p.ldc >> 5;
+#pragma unroll 4
+    for (int i = 0; i < 20; ++i) {
+      const int k = i * 64 + lane, row = k / 40, ch = k - row * 40;
+      const long long m = mw + half * 32 + row;
+      if (m < p.M) {
+        const long long w = m / p.s_in;
+        const int tpos = (int)(m - w * p.s_in);
+        if (tpos < p.t_valid && n0 + (ch >> 3) * 32 < p.n_store) {
+          const long long orow = w * p.s_out + tpos;
+          char* g = (char*)p.C + (orow * ldb + (n0 >> 5)) * 128 + ch * 16;
+          *(floatx4v*)g = *(const floatx4v*)(lds + row * H3E_ROW + ch * 16);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
 template <int LAYER, int EPI, int TM>
 __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem) {
   constexpr int ROW_KB = 128;                         // global bytes per row and 32-channel block
@@ -959,7 +1012,14 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
     }
     if (c + 1 < nchunk) read_a(aslab + ((c + 1) & 1) * H3C_ASLAB, 0, as);
   }
-  gemm_epilogue16<EPI, 2>(p, acc, m0 + wave * 64, n0, 0, lane);
+  if constexpr (EPI == EPI_RELU) {
+    // the ring's last (duplicate) B pieces may still be landing: drain before reusing LDS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    epilogue_relu_h2_lds(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
+  } else {
+    gemm_epilogue16<EPI, 2>(p, acc, m0 + wave * 64, n0, 0, lane);
+  }
 }
 
 // ---- the library's split-operand GEMMs (both on 16x16x32 MFMAs, LDS-DMA staged) ---------

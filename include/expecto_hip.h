@@ -148,10 +148,11 @@ int expecto_beluga_forward_segment_pairs(expecto_beluga_t h, const uint8_t* code
                                          int n_win, float* y_ref, float* y_alt, long long strand_stride,
                                          void* stream);
 
-/* Select the GEMM arithmetic for later calls.  The first switch to F16X3 builds the fp16
- * weight planes and calibrates the activation scales (a BF16X6 forward of 256 seeded random
- * windows; each layer's scale puts its largest calibration activation at 2^target_log2,
- * default 10, leaving >= 2^5 of headroom below fp16's 65504 before the fallback). */
+/* Select the GEMM arithmetic for later calls (a new handle starts in F16X3).  F16X3's fp16
+ * weight planes and activation scales are built at handle creation: a BF16X6 forward of 256
+ * seeded random windows; each layer's scale puts its largest calibration activation at
+ * 2^target_log2, default 10, leaving >= 2^5 of headroom below fp16's 65504 before the
+ * fallback. */
 int expecto_beluga_set_precision(expecto_beluga_t h, int precision);
 int expecto_beluga_get_precision(expecto_beluga_t h);
 /* F16X3 calibration target (log2 of the scaled calibration maximum, 0..20); re-derives the

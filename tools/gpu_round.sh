@@ -6,7 +6,7 @@ REPO=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$REPO/gpurun_out
 mkdir -p $OUT
 TAG=${1:-r01}
-STEPS=${STEPS:-tests,smoke,bench,prof,pmc}
+STEPS=${STEPS:-tests,smoke,bench,accuracy,prof,pmc}
 run() {  # name timeout cmd...
   local name=$1 to=$2; shift 2
   echo "=== $name: $*" >> $OUT/steps.log
@@ -20,6 +20,7 @@ cd $REPO
 [[ $STEPS == *tests* ]] && run gpu_tests 900 python -m pytest tests -m gpu -x -q
 [[ $STEPS == *smoke* ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *bench* ]] && run bench 600 python bench.py --steps 10 --warmup 3
+[[ $STEPS == *accuracy* ]] && run accuracy 300 python tools/accuracy_gpu.py 24
 export TMPDIR=/tmp
 if [[ $STEPS == *prof* ]]; then
   run prof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python3 $REPO/bench.py --steps 5 --warmup 2 --no-cpu-baseline
