@@ -815,7 +815,8 @@ constexpr int H3C_AROWS = 288;                         // 256 + 7 rows needed, 1
 constexpr int H3C_APLANE = H3C_AROWS * 64;             // 18,432 B
 constexpr int H3C_ASLAB = 2 * H3C_APLANE;              // 36,864 B
 constexpr int H3C_BSTAGE = 2 * X6P_B_PLANE;            // 20,480 B
-constexpr int H3C_LDS = 2 * H3C_ASLAB + 3 * H3C_BSTAGE;
+template <int NSB>
+constexpr int h3c_lds() { return 2 * H3C_ASLAB + NSB * H3C_BSTAGE; }
 
 // ReLU epilogue of the f16x3 conv kernel through LDS.  A wave's 64 x 160 tile is, per output
 // row, ONE contiguous 640-B run of the planes layout (5 blocks x [hi 64 B | lo 64 B]); the
@@ -870,8 +871,11 @@ __device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const fl
   }
 }
 
-template <int LAYER, int EPI, int TM>
+// NSB: depth of the B ring (3: loads of stage s+2 in flight during stage s; 4: s+3).
+// TM 16 (timing probe, wrong results): no vmcnt wait at stage ends.
+template <int LAYER, int EPI, int TM, int NSB>
 __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem) {
+  static_assert(NSB == 3 || NSB == 4, "B ring depth");
   constexpr int ROW_KB = 128;                         // global bytes per row and 32-channel block
   const unsigned nblk = gridDim.x, bid = blockIdx.x;
   const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
@@ -967,11 +971,16 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
     }
   };
 
-  // prologue: slab 0, B stages 0 and 1
+  // prologue: slab 0, B stages 0 .. NSB-2
   issue_a(0, 0, 9);
   issue_b(0, 0);
   issue_b(min(1, nk - 1), 1);
-  asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  if constexpr (NSB == 4) {
+    issue_b(min(2, nk - 1), 2);
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  }
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   bf16x8 as[4][3];
@@ -982,20 +991,24 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
     const bool more_a = (c + 1 < nchunk) && !(TM & 2);
     for (int t = 0; t < 8; ++t) {
       const int s = c * 8 + t;
-      const int nslot = slot + 1 == 3 ? 0 : slot + 1;
-      const int lslot = nslot + 1 == 3 ? 0 : nslot + 1;     // stage s + 2
+      const int nslot = slot + 1 == NSB ? 0 : slot + 1;
+      const int lslot = slot == 0 ? NSB - 1 : slot - 1;     // stage s + NSB - 1 (the slot read at s - 1)
       const char* base = bring + slot * H3C_BSTAGE;
       bf16x8 b0[3], b1[3];
       read_b(base, 0, b0);
 #pragma unroll
       for (int nb = 0; nb < 10; ++nb) {
         int nv = 0;
-        if (nb == 0 && more_a) {               // slab c+1: pieces 0,1 at tap 0, piece t+1 at taps 1..7
-          issue_a(c + 1, t == 0 ? 0 : t + 1, t == 0 ? 2 : 1);
-          nv = t == 0 ? 2 : 1;
+        if (nb == 0 && more_a) {
+          // slab c+1, 9 pieces: NSB 3 -> taps 0..7 as 2,1,1,1,1,1,1,1; NSB 4 -> taps 0..5 as
+          // 2,2,2,1,1,1 (the last two taps issue B only, so vmcnt(10) at tap 7 covers the slab)
+          const int i0 = NSB == 3 ? (t == 0 ? 0 : t + 1) : (t < 3 ? 2 * t : t + 3);
+          const int ni = NSB == 3 ? (t == 0 ? 2 : 1) : (t < 3 ? 2 : (t < 6 ? 1 : 0));
+          if (ni > 0) issue_a(c + 1, i0, ni);
+          nv = ni;
         }
         if (nb == 2 && !(TM & 2)) {
-          issue_b(min(s + 2, nk - 1), lslot);
+          issue_b(min(s + NSB - 1, nk - 1), lslot);
           nv = 2;
         }
         if (nb + 1 < 10) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
@@ -1004,7 +1017,13 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
       }
       if (t < 7) read_a(slab, t + 1, as);     // same slab: already resident
       if constexpr (!(TM & 4)) {
-        asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");   // all but B(s+2): B(s+1), slab c+1
+        // all but the B pieces of the last NSB-2 stages: B(s+1), and slab c+1 by its last tap
+        if constexpr ((TM & 16) != 0)
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        else if constexpr (NSB == 4)
+          asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
       }
       asm volatile("" ::: "memory");
@@ -1039,10 +1058,10 @@ __global__ __launch_bounds__(256, 1) void beluga_gemm_h3q(GemmArgs p) {
 }
 
 // f16x3 conv layers (taps == 8, no split-K): the chunk-slab kernel above
-template <int LAYER, int EPI, int TM = 0>
+template <int LAYER, int EPI, int TM = 0, int NSB = 3>
 __global__ __launch_bounds__(256, 1) void beluga_conv_h3q(GemmArgs p) {
-  __shared__ __attribute__((aligned(1024))) char smem[H3C_LDS];
-  gemm_conv_h3_body<LAYER, EPI, TM>(p, smem);
+  __shared__ __attribute__((aligned(1024))) char smem[h3c_lds<NSB>()];
+  gemm_conv_h3_body<LAYER, EPI, TM, NSB>(p, smem);
 }
 
 // B planes for beluga_gemm_x6q from a K-contiguous fp32 B [rows][K] (K % 32 == 0).

@@ -52,9 +52,9 @@ Variant mkh3q(const char* name) {
   return {name, X6P_BM, [](const GemmArgs& a, unsigned nblk) { beluga_gemm_h3q<L, EPI, TM, NS><<<nblk, 256>>>(a); }};
 }
 
-template <int L, int EPI, int TM = 0>
+template <int L, int EPI, int TM = 0, int NSB = 3>
 Variant mkc3(const char* name) {
-  return {name, X6P_BM, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3q<L, EPI, TM><<<nblk, 256>>>(a); }};
+  return {name, X6P_BM, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3q<L, EPI, TM, NSB><<<nblk, 256>>>(a); }};
 }
 
 template <int L, int EPI, int WM, int MINB, int BK, int PIPE = 0>
