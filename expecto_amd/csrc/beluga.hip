@@ -254,6 +254,22 @@ __global__ void delta_assemble(const float* __restrict__ ref, int ref_rows, cons
   for (int c = threadIdx.x; c < row16; c += blockDim.x) to[c] = from[c];
 }
 
+// FC1 split-K slabs the alt run changes: alt window m differs from its ref window only in conv6
+// rows [r6, r6+20), i.e. FC1 K range [640*r6, 640*(r6+20)); bit ks of mask[m / tile_rows] is
+// set for every slab (slab_k wide) that range touches.  Slabs outside it have the same A rows
+// as the ref windows, so their split-K partials (still in the partial buffer after the ref
+// FC1 of the same rows and tiling) are already the alt ones, bit for bit.
+__global__ void fc1_slab_mask(const int* __restrict__ var_pos, int nv, int v0, int R, int tile_rows, int slab_k,
+                              unsigned* __restrict__ mask) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= R) return;
+  const int r6 = delta_rows(pair_pos(var_pos, m, nv, v0)).r[6];
+  const int k0 = r6 * 640, k1 = (r6 + kDW[6]) * 640 - 1;
+  unsigned bits = 0;
+  for (int ks = k0 / slab_k; ks <= k1 / slab_k; ++ks) bits |= 1u << ks;
+  atomicOr(mask + m / tile_rows, bits);
+}
+
 // alt conv6 = ref conv6 (act6, 106 rows per window) with rows [r6, r6+20) from the alt run
 __global__ void pair_patch_apply(const float* __restrict__ d6, float* __restrict__ act6, int nv, int v0,
                                  const int* __restrict__ var_pos, int row16) {
@@ -550,6 +566,7 @@ struct expecto_beluga {
   float* D1 = nullptr;
   uint8_t* delta_codes = nullptr;
   int* seg_tab = nullptr;        //   per-segment delta rows (segment pairs)
+  float* slab_mask = nullptr;    //   alt FC1 split-K slab mask per M tile (pair path)
   int win_cap = 0;
   size_t bytes = 0;
   std::vector<void*> allocs;
@@ -722,7 +739,7 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
 // FC1 (split-K) + reduce + FC2/sigmoid for nb windows whose conv6 rows are at act
 // (+ a_rows[m] when given, else m*67840).
 int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb, float* y, hipStream_t st,
-           const long long* c_rows = nullptr) {
+           const long long* c_rows = nullptr, const unsigned* ks_mask = nullptr, double slab_frac = 1.0) {
   int rc;
   const long long m_tiles = (nb + gemm_bm() - 1) / gemm_bm();
   const int n_tiles1 = npad_of(kFc1Out) / GBN;
@@ -746,8 +763,10 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     a.n_store = kHidLd;
     a.split_stride = (long long)nb * kHidLd;
     a.linear_order = 1;
+    a.ks_mask = ks_mask;
+    EXPECTO_REQUIRE(!ks_mask || planes_gemm(), "slab mask needs the planes GEMM");
     LayerTimer lt(h, 6, st);
-    if (h->profiling) h->macs[6] += (double)nb * kFc1Out * kFc1In;
+    if (h->profiling) h->macs[6] += (double)nb * kFc1Out * kFc1In * slab_frac;
     if ((rc = launch_gemm<7, EPI_PARTIAL>(a, splits, st))) return rc;
   }
   {
@@ -813,7 +832,8 @@ int ensure_delta(expecto_beluga* h) {
   int rc;
   if ((rc = dalloc(h, &h->DA, act_alloc(da))) || (rc = dalloc(h, &h->D0, act_alloc(dd))) ||
       (rc = dalloc(h, &h->D1, act_alloc(dd))) || (rc = dalloc(h, &pc, (size_t)h->max_batch * 4)) ||
-      (rc = dalloc(h, &tb, (size_t)h->max_batch * kSegTab)))
+      (rc = dalloc(h, &tb, (size_t)h->max_batch * kSegTab)) ||
+      (rc = dalloc(h, &h->slab_mask, (size_t)h->max_batch / 64 + 64)))
     return rc;
   h->delta_codes = reinterpret_cast<uint8_t*>(pc);
   h->seg_tab = reinterpret_cast<int*>(tb);
@@ -1077,7 +1097,27 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
     if ((rc = run_fc(h, act6, nullptr, R, y_ref, st, h->c_rows))) return rc;
     pair_patch_apply<<<dim3(kDW[6], R), dim3(64), 0, st>>>(dprev, act6, nv, v0, var_pos, 640 * eb / 16);
     if ((rc = check_launch("pair_patch_apply"))) return rc;
-    if ((rc = run_fc(h, act6, nullptr, R, y_alt, st, h->c_rows))) return rc;
+    // alt FC1: only the split-K slabs the 20 changed conv6 rows touch (planes GEMMs)
+    const unsigned* mask = nullptr;
+    double frac = 1.0;
+    if (planes_gemm()) {
+      const int tiles = (int)((R + gemm_bm() - 1) / gemm_bm());
+      unsigned* md = reinterpret_cast<unsigned*>(h->slab_mask);
+      EXPECTO_HIP_CHECK(hipMemsetAsync(md, 0, tiles * sizeof(unsigned), st));
+      fc1_slab_mask<<<dim3((R + 255) / 256), dim3(256), 0, st>>>(var_pos, nv, v0, R, (int)gemm_bm(),
+                                                                  kFc1In / kFcSplits, md);
+      if ((rc = check_launch("fc1_slab_mask"))) return rc;
+      mask = md;
+      if (h->profiling) {   // executed share of the slabs, for the MAC count
+        std::vector<unsigned> hm(tiles);
+        EXPECTO_HIP_CHECK(hipMemcpyAsync(hm.data(), md, tiles * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+        EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
+        int bits = 0;
+        for (unsigned x : hm) bits += __builtin_popcount(x);
+        frac = (double)bits / (tiles * kFcSplits);
+      }
+    }
+    if ((rc = run_fc(h, act6, nullptr, R, y_alt, st, h->c_rows, mask, frac))) return rc;
   }
   return EXPECTO_OK;
 }

@@ -46,6 +46,8 @@ struct GemmArgs {
   const float* col_scale;   // f16x3: per-column 2^-(s_in + s_w[n]) undoing the operand scales (else null)
   float out_scale;          // f16x3: 2^s_out applied to stored activations (next layer's input scale)
   int* ovf;                 // f16x3: set to 1 when a stored activation does not fit fp16
+  const unsigned* ks_mask;  // split-K planes GEMM: bit ks of ks_mask[m_tile] = compute that slab
+                            // (others keep the partials already in C: alt FC1 of SNV pairs)
 };
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -625,6 +627,7 @@ __device__ __forceinline__ void gemm_planes_body(const GemmArgs& p, char* smem) 
     mt = rest % p.m_tiles;
     ks = (int)(rest / p.m_tiles);
   }
+  if (p.ks_mask && !((p.ks_mask[mt] >> ks) & 1u)) return;   // slab unchanged: partials already in C
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: LDS bases stay scalar
   const long long m0 = mt * X6P_BM;
