@@ -173,6 +173,36 @@ __global__ void variant_reduce_kernel(const float* __restrict__ eff, const long 
 
 using namespace expecto;
 
+// ---- gblinear scoring (predict.py:150-166, xgboost 0.7 GBLinear::Pred) ---------------------
+// out[m] = init + sum_j float32(X[m][cols[j]]) * w[j], accumulated in float32 in column order
+// with separate rounding of every product and sum (no FMA) -- the reference's CPU loop.  One
+// thread per row (64 rows per block); each 64-column slab of the 64 rows is staged through LDS
+// with row-contiguous (coalesced) loads.
+__global__ __launch_bounds__(64) void gblinear_kernel(const double* __restrict__ X, long long n, long long ld,
+                                                      const int* __restrict__ cols, int ncols,
+                                                      const float* __restrict__ w, float init,
+                                                      float* __restrict__ out) {
+  __shared__ float tile[64][65];
+  __shared__ float ws[64];
+  const long long r0 = (long long)blockIdx.x * 64;
+  const int t = threadIdx.x;
+  float psum = init;
+  for (int j0 = 0; j0 < ncols; j0 += 64) {
+    const int j = j0 + t;
+    const int c = j < ncols ? cols[j] : 0;
+    ws[t] = j < ncols ? w[j] : 0.f;
+    for (int rr = 0; rr < 64; ++rr) {
+      const long long m = r0 + rr;
+      tile[rr][t] = (m < n && j < ncols) ? (float)X[m * ld + c] : 0.f;
+    }
+    __syncthreads();
+    const int jn = min(64, ncols - j0);
+    for (int jj = 0; jj < jn; ++jj) psum = __fadd_rn(psum, __fmul_rn(tile[t][jj], ws[jj]));
+    __syncthreads();
+  }
+  if (r0 + t < n) out[r0 + t] = psum;
+}
+
 extern "C" {
 
 const char* expecto_last_error(void) { return g_last_error.c_str(); }
@@ -267,6 +297,17 @@ int expecto_variant_reduce(const float* effects, const long long* dist, const ui
   variant_reduce_kernel<<<grid, dim3(256), 0, as_stream(stream)>>>(effects, dist, strand_plus, shifts, n_shift, n,
                                                                    nfeat, out);
   return check_launch("variant_reduce");
+}
+
+int expecto_gblinear_predict(const double* X, long long n, long long ld, const int* cols, int ncols, const float* w,
+                             float init, float* out, void* stream) {
+  EXPECTO_REQUIRE(n >= 0 && ncols >= 0 && ld >= 0, "negative shape");
+  if (n == 0) return EXPECTO_OK;
+  EXPECTO_REQUIRE(X && out && (ncols == 0 || (cols && w)), "null argument");
+  EXPECTO_REQUIRE((n + 63) / 64 < (1LL << 31), "too many rows");
+  gblinear_kernel<<<dim3((unsigned)((n + 63) / 64)), dim3(64), 0, as_stream(stream)>>>(X, n, ld, cols, ncols, w, init,
+                                                                                      out);
+  return check_launch("gblinear_predict");
 }
 
 }  // extern "C"

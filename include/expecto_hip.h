@@ -25,6 +25,7 @@
  *                                   0.5*(fwd+rc) of compute_expecto_features.py:123)
  *   expecto_tss_reduce             pos_weights x pred_fwd_rc (compute_expecto_features.py:91-124)
  *   expecto_variant_reduce         exp-decay shift weights x effects (predict.py:87-136)
+ *   expecto_gblinear_predict       xgboost gblinear scoring of feature rows (predict.py:150-166)
  *   expecto_beluga_destroy         (model teardown)
  */
 #ifndef EXPECTO_HIP_H
@@ -202,6 +203,14 @@ int expecto_tss_reduce(const float* fwd, const float* rc, const double* weights,
  * shifts[n_shift]; out [n, 10*nfeat] fp64 (predict.py:87-124 feature layout). */
 int expecto_variant_reduce(const float* effects, const long long* dist, const uint8_t* strand_plus,
                            const int* shifts, int n_shift, int n, int nfeat, double* out, void* stream);
+
+/* ExPecto expression scoring with an xgboost gblinear model (predict.py:150-166;
+ * xgboost 0.7 GBLinear::Pred): out[m] = init + sum_j float32(X[m*ld + cols[j]]) * w[j],
+ * summed in float32 in column order with every product and sum rounded separately;
+ * init = float32(bias + base_score).  X: float64 feature rows (DEVICE), cols: int32[ncols]
+ * (the keep-mask column map of predict.py:137-145), w: float32[ncols]. */
+int expecto_gblinear_predict(const double* X, long long n, long long ld, const int* cols, int ncols, const float* w,
+                             float init, float* out, void* stream);
 
 const char* expecto_last_error(void);
 const char* expecto_version(void);

@@ -10,6 +10,7 @@ SURVEY.md section 8(a):
 * ``reduce_np``   -- the TSS spatial-transform reduction
                      (``compute_expecto_features.py:88-124``) and the variant-side
                      reduction (``predict.py:87-147,183-194``).
+* ``gblinear_np`` -- the xgboost gblinear expression scoring of ``predict.py:150-166``.
 * ``weights``     -- the seeded synthetic Beluga weights the golden vectors use.
 
 Pinning: the restatement is checked against golden vectors produced by running

@@ -1,0 +1,72 @@
+"""CPU: expression-scoring host logic (predict.py drop-in) against the reference's outputs.
+
+The golden TSVs come from running the reference predict.py (tests/golden/make_golden_predict.py)
+on the reference chromatin.py outputs, with xgboost's gblinear restated in the stub."""
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from conftest import GOLDEN
+
+PRED = os.path.join(GOLDEN, "predict_sed")
+FEATURES_TSV = os.path.join(PRED, "deepsea_beluga_2002_features.tsv")
+
+
+def test_legacy_model_reader_and_writer_roundtrip(tmp_path):
+    from expecto_amd.xgblinear import GBLinear
+    path = os.path.join(PRED, "all", "model.save")
+    m = GBLinear.load(path)
+    assert m.num_feature == 20020 and m.groups == 1
+    assert m.base_score == 2.0 and np.float32(m.bias[0]) == np.float32(0.37)
+    assert m.objective == "reg:linear"
+    out = tmp_path / "m.save"
+    m.save_legacy(str(out))
+    assert open(out, "rb").read() == open(path, "rb").read()
+
+
+def test_json_and_dump_readers_agree(tmp_path):
+    import json
+    from expecto_amd.xgblinear import GBLinear
+    m = GBLinear.load(os.path.join(PRED, "notf", "model.save"))
+    w = np.concatenate([m.weights[:, 0], m.bias])
+    js = {"learner": {"gradient_booster": {"name": "gblinear", "model": {"weights": [float(x) for x in w]}},
+                      "learner_model_param": {"base_score": "2E0", "num_feature": str(m.num_feature), "num_class": "0"},
+                      "objective": {"name": "reg:squarederror"}}}
+    (tmp_path / "m.json").write_text(json.dumps(js))
+    mj = GBLinear.load(str(tmp_path / "m.json"))
+    assert np.array_equal(mj.weights, m.weights) and np.array_equal(mj.bias, m.bias) and mj.base_score == 2.0
+    dump = "bias:\n%r\nweight:\n" % float(m.bias[0]) + "".join("%r\n" % float(x) for x in m.weights[:, 0])
+    (tmp_path / "m.dump").write_text(dump)
+    with pytest.raises(ValueError):
+        GBLinear.load(str(tmp_path / "m.dump"))
+    md = GBLinear.load(str(tmp_path / "m.dump"), base_score=2.0)
+    assert np.array_equal(md.weights, m.weights) and md.base_score == 2.0
+    (tmp_path / "bad.save").write_bytes(b"binf" + b"\0" * 40)
+    with pytest.raises(ValueError):
+        GBLinear.load(str(tmp_path / "bad.save"))
+
+
+def test_oracle_gblinear_reproduces_reference_predictions():
+    """Oracle scoring of the feature matrices the reference predict.py built == its REF/ALT."""
+    from expecto_amd.xgblinear import GBLinear
+    from oracle import gblinear_np
+    feats = np.load(os.path.join(GOLDEN, "predict_features.npz"))
+    m = GBLinear.load(os.path.join(PRED, "all", "model.save"))
+    sed = pd.read_csv(os.path.join(PRED, "all", "sed.tsv"), sep="\t", float_precision="round_trip")
+    for k, col in (("ref", "REF"), ("alt", "ALT")):
+        got = gblinear_np.predict(feats[k], m.weights[:, 0], m.bias[0], m.base_score)
+        assert np.array_equal(got.astype(np.float64), sed[col].to_numpy()), k
+
+
+def test_keep_mask_and_repeats_match_reference():
+    from expecto_amd import predict
+    df = pd.read_csv(FEATURES_TSV, sep="\t", index_col=0)
+    m = predict.get_keep_mask(df, True, False, False, False, True)
+    assert m.sum() == 1312
+    assert predict.get_keep_mask(df, False, False, False, False, False).sum() == 2002
+    genes = pd.DataFrame([[1, 5, 6, "A", "G", 0], [1, 5, 6, "A", "G", 1], [2, 7, 8, "C", "T", 2],
+                          [1, 5, 6, "A", "G", 3]])
+    assert predict.get_num_repeats(genes) == [2, 1, 1]
+    assert predict.get_num_repeats(genes.iloc[:0]) == [0]
