@@ -182,6 +182,7 @@ __global__ __launch_bounds__(64) void gblinear_kernel(const double* __restrict__
                                                       const int* __restrict__ cols, int ncols,
                                                       const float* __restrict__ w, float init,
                                                       float* __restrict__ out) {
+#pragma clang fp contract(off)   // products and sums rounded separately (HIP's __fmul_rn is a plain *)
   __shared__ float tile[64][65];
   __shared__ float ws[64];
   const long long r0 = (long long)blockIdx.x * 64;
@@ -197,7 +198,7 @@ __global__ __launch_bounds__(64) void gblinear_kernel(const double* __restrict__
     }
     __syncthreads();
     const int jn = min(64, ncols - j0);
-    for (int jj = 0; jj < jn; ++jj) psum = __fadd_rn(psum, __fmul_rn(tile[t][jj], ws[jj]));
+    for (int jj = 0; jj < jn; ++jj) psum = psum + tile[t][jj] * ws[jj];
     __syncthreads();
   }
   if (r0 + t < n) out[r0 + t] = psum;
