@@ -58,6 +58,8 @@ SIGNATURES = {
                                               c_vp, c_vp]),
     "expecto_gblinear_predict": (ctypes.c_int, [c_vp, ctypes.c_longlong, ctypes.c_longlong, c_vp, ctypes.c_int,
                                                 c_vp, ctypes.c_float, c_vp, c_vp]),
+    "expecto_shift_reduce": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            c_vp, c_vp]),
     "expecto_last_error": (ctypes.c_char_p, []),
     "expecto_version": (ctypes.c_char_p, []),
 }

@@ -108,6 +108,39 @@ __global__ void fwd_rc_avg_kernel(const float* __restrict__ x, int rows, int col
     out[i] = (x[i] + x[i + half]) / 2.0f;
 }
 
+// Generalised shift reduction (geuvadis_sed_for_top_eqtls.py:95-121,
+// geuvadis_predict_consensus.py:110-128): F64AVG averages fwd/rc in float64
+// ((double)a + (double)b) / 2 like numpy on float64 prediction arrays; LEGACY writes the
+// "backwards compatibility" layout 10 x [0, f_0 .. f_{nfeat-1}] (a zero column ahead of each
+// decay block: 10 * (nfeat + 1) = 20030 features).  Shifts are summed sequentially in order.
+template <bool F64AVG, bool LEGACY>
+__global__ void shift_reduce_kernel(const float* __restrict__ fwd, const float* __restrict__ rc,
+                                    const double* __restrict__ weights, int n_shift, int nfeat,
+                                    double* __restrict__ out) {
+  extern __shared__ double wsx[];  // [10][n_shift]
+  for (int i = threadIdx.x; i < 10 * n_shift; i += blockDim.x) wsx[i] = weights[i];
+  __syncthreads();
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  const long long g = blockIdx.y;
+  constexpr int kStride = LEGACY ? 1 : 0;
+  double* o = out + g * 10LL * (nfeat + kStride);
+  if (LEGACY && f < 10) o[(long long)f * (nfeat + 1)] = 0.0;
+  if (f >= nfeat) return;
+  double acc[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) acc[k] = 0.0;
+  const float* pf = fwd + g * n_shift * nfeat + f;
+  const float* pr = rc + g * n_shift * nfeat + f;
+  for (int s = 0; s < n_shift; ++s) {
+    const float a = pf[(long long)s * nfeat], b = pr[(long long)s * nfeat];
+    const double pd = F64AVG ? ((double)a + (double)b) / 2.0 : (double)(0.5f * (a + b));
+#pragma unroll
+    for (int k = 0; k < 10; ++k) acc[k] += wsx[k * n_shift + s] * pd;
+  }
+#pragma unroll
+  for (int k = 0; k < 10; ++k) o[(long long)k * (nfeat + kStride) + kStride + f] = acc[k];
+}
+
 // grid: (ceil(nfeat/256), n_genes); thread = feature f; loops over the shifts in order.
 __global__ void tss_reduce_kernel(const float* __restrict__ fwd, const float* __restrict__ rc,
                                   const double* __restrict__ weights, int n_shift, int nfeat,
@@ -309,6 +342,25 @@ int expecto_gblinear_predict(const double* X, long long n, long long ld, const i
   gblinear_kernel<<<dim3((unsigned)((n + 63) / 64)), dim3(64), 0, as_stream(stream)>>>(X, n, ld, cols, ncols, w, init,
                                                                                       out);
   return check_launch("gblinear_predict");
+}
+
+int expecto_shift_reduce(const float* fwd, const float* rc, const double* weights, int n_genes, int n_shift, int nfeat,
+                         int flags, double* out, void* stream) {
+  EXPECTO_REQUIRE(n_genes >= 0 && n_shift > 0 && n_shift <= 4096 && nfeat >= 10, "bad shape");
+  EXPECTO_REQUIRE((flags & ~3) == 0, "bad flags");
+  if (n_genes == 0) return EXPECTO_OK;
+  EXPECTO_REQUIRE(n_genes <= 65535, "at most 65535 sequences per call");
+  EXPECTO_REQUIRE(fwd && rc && weights && out, "null argument");
+  dim3 grid((nfeat + 255) / 256, n_genes);
+  const size_t shm = 10 * n_shift * sizeof(double);
+  hipStream_t st = as_stream(stream);
+  switch (flags) {
+    case 0: shift_reduce_kernel<false, false><<<grid, dim3(256), shm, st>>>(fwd, rc, weights, n_shift, nfeat, out); break;
+    case 1: shift_reduce_kernel<true, false><<<grid, dim3(256), shm, st>>>(fwd, rc, weights, n_shift, nfeat, out); break;
+    case 2: shift_reduce_kernel<false, true><<<grid, dim3(256), shm, st>>>(fwd, rc, weights, n_shift, nfeat, out); break;
+    default: shift_reduce_kernel<true, true><<<grid, dim3(256), shm, st>>>(fwd, rc, weights, n_shift, nfeat, out); break;
+  }
+  return check_launch("shift_reduce");
 }
 
 }  // extern "C"

@@ -38,7 +38,9 @@ def _datatype(dt: np.dtype) -> bytes:
         return struct.pack("<BBBBI", 0x11, 0x20, 31, 0, 4) + struct.pack("<HHBBBBI", 0, 32, 23, 8, 0, 23, 127)
     if dt == np.float64:
         return struct.pack("<BBBBI", 0x11, 0x20, 63, 0, 8) + struct.pack("<HHBBBBI", 0, 64, 52, 11, 0, 52, 1023)
-    raise TypeError(f"unsupported dtype {dt} (float32/float64 only)")
+    if dt.kind == "S":   # fixed-length ASCII, null-padded (what h5py writes for numpy 'S' arrays)
+        return struct.pack("<BBBBI", 0x13, 0x01, 0, 0, dt.itemsize)
+    raise TypeError(f"unsupported dtype {dt} (float32/float64/fixed-length bytes only)")
 
 
 def _dataset_header(shape, dt, data_addr, nbytes) -> bytes:
@@ -57,10 +59,10 @@ def _dataset_header(shape, dt, data_addr, nbytes) -> bytes:
 def write(path: str, datasets: dict) -> None:
     """Write ``{name: ndarray}`` (float32/float64, C-contiguous) as root datasets."""
     names = sorted(datasets)                      # symbol-table entries are name-ordered
-    arrays = [np.ascontiguousarray(datasets[n]) for n in names]
+    arrays = [np.array(datasets[n], order="C", copy=True) for n in names]   # 0-d arrays -> scalar dataspace
     for a in arrays:
-        if a.dtype not in (np.float32, np.float64):
-            raise TypeError(f"{a.dtype}: only float32/float64 datasets are supported")
+        if a.dtype not in (np.float32, np.float64) and a.dtype.kind != "S":
+            raise TypeError(f"{a.dtype}: only float32/float64/'S' datasets are supported")
     if len(names) > 2 * _LEAF_K:
         raise ValueError("at most 8 datasets per file in this minimal writer")
 
@@ -121,7 +123,7 @@ def write(path: str, datasets: dict) -> None:
             cur = f.tell()
             if cur < data_addr[i]:
                 f.write(b"\0" * (data_addr[i] - cur))
-            f.write(a.astype(a.dtype.newbyteorder("<"), copy=False).tobytes())
+            f.write(a.tobytes() if a.dtype.kind == "S" else a.astype(a.dtype.newbyteorder("<"), copy=False).tobytes())
 
 
 # ---------------------------------------------------------------------------- reader
@@ -149,10 +151,13 @@ def _parse_dataset(buf: bytes, addr: int):
         elif mtype == 0x0003:
             cls = m[0] & 0x0F
             size = struct.unpack_from("<I", m, 4)[0]
-            if cls != 1 or size not in (4, 8):
-                raise ValueError("only IEEE float datasets are supported")
-            be = m[1] & 1
-            dtype = np.dtype(("<" if not be else ">") + ("f4" if size == 4 else "f8"))
+            if cls == 3:
+                dtype = np.dtype(f"S{size}")
+            elif cls != 1 or size not in (4, 8):
+                raise ValueError("only IEEE float and fixed-length string datasets are supported")
+            else:
+                be = m[1] & 1
+                dtype = np.dtype(("<" if not be else ">") + ("f4" if size == 4 else "f8"))
         elif mtype == 0x0008:
             if m[0] != 3 or m[1] != 1:
                 raise ValueError("only contiguous layout (v3) is supported")
@@ -162,11 +167,12 @@ def _parse_dataset(buf: bytes, addr: int):
     addr_, nbytes = data
     if addr_ == UNDEF:
         return np.zeros(shape, dtype)
-    return np.frombuffer(buf, dtype, count=int(np.prod(shape)), offset=addr_).reshape(shape).astype(dtype.newbyteorder("="))
+    arr = np.frombuffer(buf, dtype, count=int(np.prod(shape)), offset=addr_).reshape(shape)
+    return arr.copy() if dtype.kind == "S" else arr.astype(dtype.newbyteorder("="))
 
 
 def read(path: str) -> dict:
-    """``{name: ndarray}`` for every contiguous float dataset in the root group."""
+    """``{name: ndarray}`` for every contiguous float / fixed-length string dataset in the root group."""
     with open(path, "rb") as f:
         buf = f.read()
     if buf[:8] != _SIG:

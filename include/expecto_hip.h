@@ -26,6 +26,8 @@
  *   expecto_tss_reduce             pos_weights x pred_fwd_rc (compute_expecto_features.py:91-124)
  *   expecto_variant_reduce         exp-decay shift weights x effects (predict.py:87-136)
  *   expecto_gblinear_predict       xgboost gblinear scoring of feature rows (predict.py:150-166)
+ *   expecto_shift_reduce           200-shift reduction of consensus / eQTL sequences
+ *                                  (geuvadis_sed_for_top_eqtls.py:95-121, geuvadis_predict_consensus.py:110-128)
  *   expecto_beluga_destroy         (model teardown)
  */
 #ifndef EXPECTO_HIP_H
@@ -203,6 +205,18 @@ int expecto_tss_reduce(const float* fwd, const float* rc, const double* weights,
  * shifts[n_shift]; out [n, 10*nfeat] fp64 (predict.py:87-124 feature layout). */
 int expecto_variant_reduce(const float* effects, const long long* dist, const uint8_t* strand_plus,
                            const int* shifts, int n_shift, int n, int nfeat, double* out, void* stream);
+
+/* Shift reduction of per-sequence window predictions (fwd and rc [n, n_shift, nfeat] f32, DEVICE)
+ * with exp-decay weights [10, n_shift] f64 into float64 features, shifts summed in order.
+ * flags bit 0 (EXPECTO_REDUCE_F64AVG): average fwd/rc in float64 (numpy on float64 prediction
+ * arrays, geuvadis_*.py) instead of 0.5f*(a+b) in float32 (compute_expecto_features.py:123);
+ * bit 1 (EXPECTO_REDUCE_LEGACY20030): out[n, 10, nfeat+1] with a zero column ahead of each
+ * decay block ("backwards compatibility" layout, geuvadis_sed_for_top_eqtls.py:112-120),
+ * else out[n, 10, nfeat]. */
+#define EXPECTO_REDUCE_F64AVG 1
+#define EXPECTO_REDUCE_LEGACY20030 2
+int expecto_shift_reduce(const float* fwd, const float* rc, const double* weights, int n_genes, int n_shift, int nfeat,
+                         int flags, double* out, void* stream);
 
 /* ExPecto expression scoring with an xgboost gblinear model (predict.py:150-166;
  * xgboost 0.7 GBLinear::Pred): out[m] = init + sum_j float32(X[m*ld + cols[j]]) * w[j],

@@ -70,3 +70,27 @@ def test_keep_mask_and_repeats_match_reference():
                           [1, 5, 6, "A", "G", 3]])
     assert predict.get_num_repeats(genes) == [2, 1, 1]
     assert predict.get_num_repeats(genes.iloc[:0]) == [0]
+
+
+def test_consensus_fasta_and_natsort(tmp_path):
+    from expecto_amd import consensus
+    p = tmp_path / "x.fa"
+    p.write_text(">chr1:-5-393210 extra words\nacgt\nNNAC\n>second\nGG\n")
+    recs = list(consensus.parse_fasta(str(p)))
+    assert recs == [("chr1:-5-393210", "acgtNNAC"), ("second", "GG")]
+    s = consensus.normalize_consensus(*recs[0])
+    assert len(s) == consensus.ENFORMER_SEQ_LENGTH and s.endswith("ACGTNNAC") and s[0] == "N"
+    with pytest.raises(AssertionError):
+        consensus.normalize_consensus("chr1:1-10", "ACGT")
+    assert consensus.natsorted(["g10", "g2", "a", "g1"]) == ["a", "g1", "g2", "g10"]
+
+
+def test_h5_scalar_and_string_datasets(tmp_path):
+    from expecto_amd import h5
+    f = str(tmp_path / "t.h5")
+    h5.write(f, {"ref_preds": np.float32(1.25), "record_ids": np.array(["chr1:1-9|HG1", "x"], "S"),
+                 "m": np.arange(6.0).reshape(2, 3)})
+    r = h5.read(f)
+    assert r["ref_preds"].shape == () and r["ref_preds"] == np.float32(1.25)
+    assert list(r["record_ids"]) == [b"chr1:1-9|HG1", b"x"]
+    assert np.array_equal(r["m"], np.arange(6.0).reshape(2, 3))
