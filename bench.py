@@ -65,7 +65,9 @@ def kernel_name(layer: str, precision: str) -> str:
     if precision == "bf16x6":
         return f"beluga_gemm_x6q<{l}, {e}, 0>"
     if precision == "f16x3":
-        return f"beluga_gemm_h3q<{l}, {e}, 0, 3>" if l in (7, 8) else f"beluga_conv_h3q<{l}, {e}, 0>"
+        if l in (7, 8):
+            return f"beluga_gemm_h3q<{l}, {e}, 0, 3>"
+        return f"beluga_conv_h3w<{l}, {e}, 0>" if e == 0 else f"beluga_conv_h3q<{l}, {e}, 0>"
     return f"beluga_gemm<{l}, {e}, 4, 2, 32, 1>"
 WINDOW_MACS = sum(LAYER_MACS.values())
 

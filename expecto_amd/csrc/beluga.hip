@@ -240,18 +240,22 @@ __global__ void delta_codes(const uint8_t* __restrict__ alt, long long stride, i
 // layer l-1 (row stride ref_rows per window), except rows inside [r_{l-1}, r_{l-1}+W_{l-1})
 // which come from the alt run of layer l-1 (dprev, kDW[l-1] rows per window).  Rows are
 // row16 16-byte lanes (fp32 rows or bf16 planes of the same channels).
-__global__ void delta_assemble(const float* __restrict__ ref, int ref_rows, const float* __restrict__ dprev, int l,
-                               int row16, int nv, int v0, const int* __restrict__ var_pos,
-                               float* __restrict__ out) {
-  const int m = blockIdx.y;
-  const int i = blockIdx.x;
+// One block per alt window (all kDA[l] rows: 20-70 KB), so the copy runs near HBM rate.
+__global__ __launch_bounds__(256) void delta_assemble(const float* __restrict__ ref, int ref_rows,
+                                                      const float* __restrict__ dprev, int l, int row16, int nv, int v0,
+                                                      const int* __restrict__ var_pos, float* __restrict__ out) {
+  const int m = blockIdx.x;
   const DeltaRows d = delta_rows(pair_pos(var_pos, m, nv, v0));
-  const int src = d.base[l] + i, rp = d.r[l - 1];
-  const floatx4* from = (src >= rp && src < rp + kDW[l - 1])
-                            ? reinterpret_cast<const floatx4*>(dprev) + ((long long)m * kDW[l - 1] + src - rp) * row16
-                            : reinterpret_cast<const floatx4*>(ref) + ((long long)m * ref_rows + src) * row16;
-  floatx4* to = reinterpret_cast<floatx4*>(out) + ((long long)m * kDA[l] + i) * row16;
-  for (int c = threadIdx.x; c < row16; c += blockDim.x) to[c] = from[c];
+  const int rp = d.r[l - 1], wp = kDW[l - 1];
+  floatx4* to = reinterpret_cast<floatx4*>(out) + (long long)m * kDA[l] * row16;
+  for (int k = threadIdx.x; k < kDA[l] * row16; k += blockDim.x) {
+    const int i = k / row16, c = k - i * row16;
+    const int src = d.base[l] + i;
+    const floatx4* from = (src >= rp && src < rp + wp)
+                              ? reinterpret_cast<const floatx4*>(dprev) + ((long long)m * wp + src - rp) * row16
+                              : reinterpret_cast<const floatx4*>(ref) + ((long long)m * ref_rows + src) * row16;
+    to[k] = from[c];
+  }
 }
 
 // FC1 split-K slabs the alt run changes: alt window m differs from its ref window only in conv6
@@ -271,14 +275,13 @@ __global__ void fc1_slab_mask(const int* __restrict__ var_pos, int nv, int v0, i
 }
 
 // alt conv6 = ref conv6 (act6, 106 rows per window) with rows [r6, r6+20) from the alt run
-__global__ void pair_patch_apply(const float* __restrict__ d6, float* __restrict__ act6, int nv, int v0,
-                                 const int* __restrict__ var_pos, int row16) {
-  const int m = blockIdx.y;
-  const int r = blockIdx.x;
+__global__ __launch_bounds__(256) void pair_patch_apply(const float* __restrict__ d6, float* __restrict__ act6, int nv,
+                                                        int v0, const int* __restrict__ var_pos, int row16) {
+  const int m = blockIdx.x;
   const int r6 = delta_rows(pair_pos(var_pos, m, nv, v0)).r[6];
-  const floatx4* src = reinterpret_cast<const floatx4*>(d6) + ((long long)m * kDW[6] + r) * row16;
-  floatx4* dst = reinterpret_cast<floatx4*>(act6) + ((long long)m * 106 + r6 + r) * row16;
-  for (int c = threadIdx.x; c < row16; c += blockDim.x) dst[c] = src[c];
+  const floatx4* src = reinterpret_cast<const floatx4*>(d6) + (long long)m * kDW[6] * row16;
+  floatx4* dst = reinterpret_cast<floatx4*>(act6) + ((long long)m * 106 + r6) * row16;
+  for (int k = threadIdx.x; k < kDW[6] * row16; k += blockDim.x) dst[k] = src[k];
 }
 
 // ---- alt deltas on the segment path (shift sweeps) -------------------------------------
@@ -338,18 +341,22 @@ __global__ void seg_delta_codes(const uint8_t* __restrict__ codes, long long str
 // block), except rows inside [rp, rp + wprev), taken from the previous alt run.  Blocks are
 // segments (nb = 1) or (segment, phase) pairs (nb = n_ph, per-phase table entries).
 // base = mult * tab[ib (+ phase)], rp = tab[irp (+ phase)].
-__global__ void seg_delta_assemble(const float* __restrict__ ref, int ref_rows, const float* __restrict__ dprev,
-                                   int wprev, const int* __restrict__ tab, int nb, int ib, int mult, int irp,
-                                   int arows, int row16, float* __restrict__ out) {
-  const int m = blockIdx.y;
-  const int i = blockIdx.x;
+__global__ __launch_bounds__(256) void seg_delta_assemble(const float* __restrict__ ref, int ref_rows,
+                                                          const float* __restrict__ dprev, int wprev,
+                                                          const int* __restrict__ tab, int nb, int ib, int mult, int irp,
+                                                          int arows, int row16, float* __restrict__ out) {
+  const int m = blockIdx.x;
   const int seg = m / nb, off = nb > 1 ? m % nb : 0;
-  const int src = mult * tab[seg * kSegTab + ib + off] + i, rp = tab[seg * kSegTab + irp + off];
-  const floatx4* from = (src >= rp && src < rp + wprev)
-                            ? reinterpret_cast<const floatx4*>(dprev) + ((long long)m * wprev + src - rp) * row16
-                            : reinterpret_cast<const floatx4*>(ref) + ((long long)m * ref_rows + src) * row16;
-  floatx4* to = reinterpret_cast<floatx4*>(out) + ((long long)m * arows + i) * row16;
-  for (int c = threadIdx.x; c < row16; c += blockDim.x) to[c] = from[c];
+  const int base = mult * tab[seg * kSegTab + ib + off], rp = tab[seg * kSegTab + irp + off];
+  floatx4* to = reinterpret_cast<floatx4*>(out) + (long long)m * arows * row16;
+  for (int k = threadIdx.x; k < arows * row16; k += blockDim.x) {
+    const int i = k / row16, c = k - i * row16;
+    const int src = base + i;
+    const floatx4* from = (src >= rp && src < rp + wprev)
+                              ? reinterpret_cast<const floatx4*>(dprev) + ((long long)m * wprev + src - rp) * row16
+                              : reinterpret_cast<const floatx4*>(ref) + ((long long)m * ref_rows + src) * row16;
+    to[k] = from[c];
+  }
 }
 
 // pool2 of the alt run for each phase: pooled rows [r4p, r4p+6) of block (seg, phase) from the
@@ -677,7 +684,10 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st) {
     if (a.taps == 8) {   // conv: chunk-slab kernel (one Toeplitz A slab per 32-channel chunk)
       EXPECTO_REQUIRE(splits == 1 && a.kper == a.ldb && a.ldb == 8 * a.lda && !a.m_fastest && !a.a_rows,
                       "f16x3 conv GEMM: full K, no split, no row gather");
-      beluga_conv_h3q<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
+      if constexpr (EPI == EPI_RELU)   // 8-wave variant: +2-5 % on conv3/5/6 (tools/gemm_bench), same bits
+        beluga_conv_h3w<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
+      else
+        beluga_conv_h3q<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
     } else {
       beluga_gemm_h3q<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
     }
@@ -978,7 +988,7 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
       auto alt_layer = [&](int l, const float* ref, int ref_rows, const float* dprev, int wprev, int nbk, int ib,
                            int mult, int irp, int arows, int w, bool pool, float* dnext) -> int {
         const int row16 = kConv[l].cin * eb / 16;
-        seg_delta_assemble<<<dim3(arows, ns * nbk), dim3(64), 0, st>>>(ref, ref_rows, dprev, wprev, h->seg_tab, nbk,
+        seg_delta_assemble<<<dim3(ns * nbk), dim3(256), 0, st>>>(ref, ref_rows, dprev, wprev, h->seg_tab, nbk,
                                                                       ib, mult, irp, arows, row16, h->DA);
         int r = check_launch("seg_delta_assemble");
         return r ? r : run_conv(h, l, h->DA, dnext, (long long)ns * nbk, arows, w, w, pool, st);
@@ -1085,7 +1095,7 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
       const int L = l + 2;
       if ((rc = run_conv(h, l, src, dst, R, g.s_in, g.t_valid, g.s_out, g.pool != 0, st))) return rc;
       const int row16 = g.cin * eb / 16;
-      delta_assemble<<<dim3(kDA[L], R), dim3(64), 0, st>>>(src, g.s_in, dprev, L, row16, nv, v0, var_pos, h->DA);
+      delta_assemble<<<dim3(R), dim3(256), 0, st>>>(src, g.s_in, dprev, L, row16, nv, v0, var_pos, h->DA);
       if ((rc = check_launch("delta_assemble"))) return rc;
       if ((rc = run_conv(h, l, h->DA, dnext, R, kDA[L], kDW[L], kDW[L], g.pool != 0, st))) return rc;
       std::swap(src, dst);
@@ -1095,7 +1105,7 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
     pair_rows<<<dim3((R + 255) / 256), dim3(256), 0, st>>>(h->c_rows, R, nv, v0, strand_stride);
     if ((rc = check_launch("pair_rows"))) return rc;
     if ((rc = run_fc(h, act6, nullptr, R, y_ref, st, h->c_rows))) return rc;
-    pair_patch_apply<<<dim3(kDW[6], R), dim3(64), 0, st>>>(dprev, act6, nv, v0, var_pos, 640 * eb / 16);
+    pair_patch_apply<<<dim3(R), dim3(256), 0, st>>>(dprev, act6, nv, v0, var_pos, 640 * eb / 16);
     if ((rc = check_launch("pair_patch_apply"))) return rc;
     // alt FC1: only the split-K slabs the 20 changed conv6 rows touch (planes GEMMs)
     const unsigned* mask = nullptr;

@@ -531,12 +531,12 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
 // XOR swizzle on the SOURCE offset, undone on the read: position = chunk ^ (-(row >> 2) & 3).
 typedef float floatx4v __attribute__((ext_vector_type(4)));
 
-template <int EPI, int FMT>
-__device__ __forceinline__ void gemm_epilogue16(const GemmArgs& p, const floatx4v (&acc)[4][10], long long mw, int n0,
+template <int EPI, int FMT, int NB = 10>
+__device__ __forceinline__ void gemm_epilogue16(const GemmArgs& p, const floatx4v (&acc)[4][NB], long long mw, int n0,
                                                 int ks, int lane) {
   const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
-  for (int nb = 0; nb < 10; ++nb) {
+  for (int nb = 0; nb < NB; ++nb) {
     const int n = n0 + nb * 16 + fr;
     if (n >= p.n_store) continue;
     const float bn = (EPI == EPI_PARTIAL) ? 0.f : p.bias[n];
@@ -1042,6 +1042,228 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
   } else {
     gemm_epilogue16<EPI, 2>(p, acc, m0 + wave * 64, n0, 0, lane);
   }
+}
+
+// ---- f16x3 conv GEMM, 8 waves (two per SIMD) ---------------------------------------------
+// gemm_conv_h3_body with the 256 x 160 tile split over 8 waves of 64 rows x 80 columns
+// (wave w: rows 64*(w & 3), columns 80*(w >> 2); 4 x 5 accumulator blocks = 80 AGPRs), so the
+// two waves of a SIMD cover each other's barrier waits, LDS-DMA issue and LDS reads (with one
+// wave per SIMD the MFMA pipe idles through them: conv2 MFMA busy 63 %, waves parked 16 %).
+// Same slab / ring staging (A slab pieces: 5 or 4 per wave per chunk, B: 3 or 2 per wave per
+// stage), same products and k order per output: bitwise equal to gemm_conv_h3_body.
+template <int EPI>
+__device__ __forceinline__ void epilogue_relu_h2_lds8(const GemmArgs& p, const floatx4v (&acc)[4][5], long long m0,
+                                                      int wm, int wn, int n0, int lane, int tid, char* lds) {
+  const int fr = lane & 15, fq = lane >> 4;
+  const long long ldb = p.ldc >> 5;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    if ((wm >> 1) == pass) {            // this pass stages rows 128*pass .. +127 (waves wm = 2*pass, 2*pass+1)
+#pragma unroll
+      for (int nb = 0; nb < 5; ++nb) {
+        const int c = wn * 80 + nb * 16 + fr, n = n0 + c;
+        const float bn = n < p.n_store ? p.bias[n] : 0.f;
+        const float cs = n < p.n_store ? p.col_scale[n] : 0.f;
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float x = fmaxf(acc[mb][nb][j] * cs + bn, 0.f) * p.out_scale;
+            if (!(fabsf(x) < 65504.f)) *p.ovf = 1;
+            _Float16 hi, lo;
+            split_h2(x, hi, lo);
+            char* d = lds + ((wm & 1) * 64 + mb * 16 + 4 * fq + j) * H3E_ROW + (c >> 5) * 128 + (c & 31) * 2;
+            *(_Float16*)d = hi;
+            *(_Float16*)(d + 64) = lo;
+          }
+      }
+    }
+    __syncthreads();
+    // 128 rows x 40 chunks of 16 B = 5120 chunks over 512 threads
+#pragma unroll 2
+    for (int i = 0; i < 10; ++i) {
+      const int k = i * 512 + tid, row = k / 40, ch = k - row * 40;
+      const long long m = m0 + pass * 128 + row;
+      if (m < p.M) {
+        const long long w = m / p.s_in;
+        const int tpos = (int)(m - w * p.s_in);
+        if (tpos < p.t_valid && n0 + (ch >> 3) * 32 < p.n_store) {
+          char* g = (char*)p.C + ((w * p.s_out + tpos) * ldb + (n0 >> 5)) * 128 + ch * 16;
+          *(floatx4v*)g = *(const floatx4v*)(lds + row * H3E_ROW + ch * 16);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int LAYER, int EPI, int TM>
+__device__ __forceinline__ void gemm_conv_h3w_body(const GemmArgs& p, char* smem) {
+  constexpr int ROW_KB = 128;
+  constexpr int NSB = 3;
+  const unsigned nblk = gridDim.x, bid = blockIdx.x;
+  const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
+  const unsigned lin = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int nt = (int)(lin % (unsigned)p.n_tiles);
+  const long long mt = (long long)(lin / (unsigned)p.n_tiles) % p.m_tiles;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 3, wn = wave >> 2;
+  const long long m0 = mt * X6P_BM;
+  const int n0 = nt * GBN;
+  const int kb_total = (int)(p.ldb / GBK);
+  const long long lda_kb = p.lda / GBK;
+  const int nchunk = (int)lda_kb;
+  const int nk = nchunk * 8;
+  auto swz = [](int r) { return (-(r >> 2)) & 3; };
+  const char* Ab = (const char*)p.A + m0 * lda_kb * ROW_KB;
+  const long long last_row = p.M - 1 + 7;
+  const int na = wave < 4 ? 5 : 4;               // A slab pieces P = wave + 8*i < 36
+  unsigned aoff[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int P = min(wave + 8 * i, 35), g = P >> 1, pl = P & 1;
+    const int r = 16 * g + (lane >> 2);
+    const long long m = min(m0 + r, last_row);
+    const int c = (lane & 3) ^ swz(r);
+    aoff[i] = (unsigned)((m - m0) * lda_kb * ROW_KB + pl * 64 + 16 * c);
+  }
+  const char* Bb = (const char*)p.Bp + (long long)n0 * kb_total * ROW_KB;
+  const int nbp = wave < 4 ? 3 : 2;              // B pieces P = wave + 8*j < 20
+  unsigned boff[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int g = min(wave + 8 * j, 19);
+    const int pl = g / 10, r = 16 * (g % 10) + (lane >> 2);
+    const int c = (lane & 3) ^ swz(r);
+    boff[j] = (unsigned)((long long)r * kb_total * ROW_KB + pl * 64 + 16 * c);
+  }
+  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, 0x7fffffff, 0x00020000);
+  char* const aslab = smem;
+  char* const bring = smem + 2 * H3C_ASLAB;
+  auto issue_a = [&](int chunk, int i) {
+    if (i >= na) return;
+    const int P = wave + 8 * i;
+    char* dst = aslab + (chunk & 1) * H3C_ASLAB + (P & 1) * H3C_APLANE + (P >> 1) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (lds_void*)dst, 16, aoff[i], (unsigned)(chunk * ROW_KB), 0, 0);
+  };
+  auto issue_b = [&](int s, int slot) {
+    if constexpr ((TM & 8) != 0) s = 0;
+    char* base = bring + slot * H3C_BSTAGE;
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      if (j < nbp)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + (wave + 8 * j) * 1024), 16, boff[j],
+                                                 (unsigned)(s * ROW_KB), 0, 0);
+  };
+
+  floatx4v acc[4][5];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 5; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[mb][nb][r] = 0.f;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int brow = (wn * 5) * 1024 + fr * 64 + 16 * (fq ^ swz(fr));
+  auto read_a = [&](const char* slab, int t, bf16x8 (&a)[4][3]) {
+    const int rr2 = fr + t;
+    const int off = (wm * 64 + rr2) * 64 + 16 * (fq ^ swz(rr2));
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      a[mb][0] = *(const bf16x8*)(slab + off + mb * 1024);
+      a[mb][1] = *(const bf16x8*)(slab + off + mb * 1024 + H3C_APLANE);
+    }
+  };
+  auto read_b = [&](const char* base, int nb, bf16x8 (&b)[3]) {
+    const char* br = base + brow + nb * 1024;
+    b[0] = *(const bf16x8*)(br);
+    b[1] = *(const bf16x8*)(br + X6P_B_PLANE);
+  };
+  auto unit = [&](const bf16x8 (&a)[4][3], int nb, const bf16x8 (&b)[3]) {
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) acc[mb][nb] = planes_mfma<2>(acc[mb][nb], a[mb], b);
+  };
+  auto pin = [&](int nv) {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if ((i % 4) == 0 && i < 4 * nv) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      if ((i & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+    }
+  };
+
+  for (int i = 0; i < 5; ++i) issue_a(0, i);
+  issue_b(0, 0);
+  issue_b(min(1, nk - 1), 1);
+  if (wave < 4)
+    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  bf16x8 as[4][3];
+  read_a(aslab, 0, as);
+  int slot = 0;
+  for (int c = 0; c < nchunk; ++c) {
+    const char* slab = aslab + (c & 1) * H3C_ASLAB;
+    const bool more_a = (c + 1 < nchunk) && !(TM & 2);
+    for (int t = 0; t < 8; ++t) {
+      const int s = c * 8 + t;
+      const int nslot = slot + 1 == NSB ? 0 : slot + 1;
+      const int lslot = slot == 0 ? NSB - 1 : slot - 1;
+      const char* base = bring + slot * H3C_BSTAGE;
+      bf16x8 b0[3], b1[3];
+      read_b(base, 0, b0);
+#pragma unroll
+      for (int nb = 0; nb < 5; ++nb) {
+        int nv = 0;
+        if (nb == 0 && more_a && t < 4) {     // slab c+1: pieces 0,1 at tap 0, 2..4 at taps 1..3
+          if (t == 0) {
+            issue_a(c + 1, 0);
+            issue_a(c + 1, 1);
+            nv = 2;
+          } else {
+            issue_a(c + 1, t + 1);
+            nv = 1;
+          }
+        }
+        if (nb == 1 && !(TM & 2)) {
+          issue_b(min(s + 2, nk - 1), lslot);
+          nv = 3;
+        }
+        if (nb + 1 < 5) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
+        unit(as, nb, (nb & 1) ? b1 : b0);
+        pin(nv);
+      }
+      if (t < 7) read_a(slab, t + 1, as);
+      if constexpr (!(TM & 4)) {
+        if (wave < 4)
+          asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+      asm volatile("" ::: "memory");
+      slot = nslot;
+    }
+    if (c + 1 < nchunk) read_a(aslab + ((c + 1) & 1) * H3C_ASLAB, 0, as);
+  }
+  if constexpr (EPI == EPI_RELU) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    epilogue_relu_h2_lds8<EPI>(p, acc, m0, wm, wn, n0, lane, tid, smem);
+  } else {
+    gemm_epilogue16<EPI, 2, 5>(p, acc, m0 + wm * 64, n0 + wn * 80, 0, lane);
+  }
+}
+
+template <int LAYER, int EPI, int TM = 0>
+__global__ __launch_bounds__(512, 1) void beluga_conv_h3w(GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[h3c_lds<3>()];
+  gemm_conv_h3w_body<LAYER, EPI, TM>(p, smem);
 }
 
 // ---- the library's split-operand GEMMs (both on 16x16x32 MFMAs, LDS-DMA staged) ---------

@@ -57,6 +57,11 @@ Variant mkc3(const char* name) {
   return {name, X6P_BM, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3q<L, EPI, TM, NSB><<<nblk, 256>>>(a); }};
 }
 
+template <int L, int EPI, int TM = 0>
+Variant mkw3(const char* name) {
+  return {name, X6P_BM, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3w<L, EPI, TM><<<nblk, 512>>>(a); }};
+}
+
 template <int L, int EPI, int WM, int MINB, int BK, int PIPE = 0>
 Variant mk(const char* name) {
   return {name, 32 * WM, [](const GemmArgs& a, unsigned nblk) {
@@ -80,7 +85,8 @@ int main(int argc, char** argv) {
   Shape shapes[] = {{"conv2", 320, 320, 2000, 496, 500, 1, 1986.0 * 320 * 2560},
                     {"conv3", 320, 480, 500, 489, 500, 0, 489.0 * 480 * 2560},
                     {"conv4", 480, 480, 500, 120, 125, 1, 482.0 * 480 * 3840},
-                    {"conv6", 640, 640, 125, 106, 125, 0, 106.0 * 640 * 5120}};
+                    {"conv5", 480, 640, 120, 113, 113, 0, 113.0 * 640 * 3840},
+                    {"conv6", 640, 640, 113, 106, 106, 0, 106.0 * 640 * 5120}};
   Shape sh = shapes[0];
   for (auto& x : shapes) if (!strcmp(x.name, which)) sh = x;
   const long long M = (long long)nb * sh.s_in;
@@ -129,22 +135,14 @@ int main(int argc, char** argv) {
   if (sh.pool) {
     vs.push_back(mk6<2, EPI_RELU_POOL4, 4, 1>("x6_wm4_b1"));
     vs.push_back(mk6q<2, EPI_RELU_POOL4>("x6q"));
-    vs.push_back(mkh3q<2, EPI_RELU_POOL4>("h3q"));
     vs.push_back(mkc3<2, EPI_RELU_POOL4>("h3c"));
+    vs.push_back(mkw3<2, EPI_RELU_POOL4>("h3w"));
     vs.push_back(mkc3<2, EPI_RELU_POOL4, 2>("h3c_noglds"));
-    vs.push_back(mkh3q<2, EPI_RELU_POOL4, 0, 2>("h3q_ns2"));
-    vs.push_back(mkh3q<2, EPI_RELU_POOL4, 2>("h3q_noglds"));
-    vs.push_back(mkh3q<2, EPI_RELU_POOL4, 4>("h3q_nobar"));
-    vs.push_back(mk6q<2, EPI_RELU_POOL4, 2>("x6q_noglds"));
-    vs.push_back(mk<2, EPI_RELU_POOL4, 4, 2, 32, 1>("f32_pipe"));
   } else {
     vs.push_back(mk6<3, EPI_RELU, 4, 1>("x6_wm4_b1"));
     vs.push_back(mk6q<3, EPI_RELU>("x6q"));
-    vs.push_back(mkh3q<3, EPI_RELU>("h3q"));
     vs.push_back(mkc3<3, EPI_RELU>("h3c"));
-    vs.push_back(mkh3q<3, EPI_RELU, 0, 2>("h3q_ns2"));
-    vs.push_back(mkh3q<3, EPI_RELU, 2>("h3q_noglds"));
-    vs.push_back(mk<3, EPI_RELU, 4, 2, 32, 1>("f32_pipe"));
+    vs.push_back(mkw3<3, EPI_RELU>("h3w"));
   }
   auto args_for = [&](int bm, float* C) {
     GemmArgs a{};
@@ -159,6 +157,14 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   std::vector<std::vector<float>> times(vs.size());
   std::vector<float> ref(csz), out(csz);
+  const char* only = getenv("VARIANT");   // run just this variant (profiling)
+  if (only) {
+    std::vector<Variant> keep;
+    for (auto& v : vs)
+      if (v.name == only || v.name == vs[0].name) keep.push_back(v);
+    vs = keep;
+    times.assign(vs.size(), {});
+  }
   for (int r = 0; r < rounds; ++r) {
     for (size_t v = 0; v < vs.size(); ++v) {
       float* C = v == 0 ? C0 : C1;
