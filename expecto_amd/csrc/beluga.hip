@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -523,9 +524,10 @@ constexpr ConvGeo kConv[5] = {
     {480, 640, 120, 113, 113, 0},  // conv5
     {640, 640, 113, 106, 106, 0},  // conv6 -> FC1 reads 106*640 = 67840 contiguous floats
 };
-// FC1 split-K: always 10 slabs of 6784 (a divisor of 67840/32 = 2120 blocks), whatever the
-// batch, so an FC1 output never depends on how many windows shared the launch.
-constexpr int kFcSplits = 10;
+// FC1 split-K: a fixed number of slabs per handle (default 20 of 3392; a divisor of
+// 67840/32 = 2120 K blocks), whatever the batch, so an FC1 output never depends on how many
+// windows shared the launch.
+constexpr int kFcSplitsDefault = 20;   // 2080 workgroups for 2000 rows: 8.1 rounds of 256 CUs (10: 4.1)
 }  // namespace
 
 struct expecto_beluga {
@@ -578,6 +580,7 @@ struct expecto_beluga {
   size_t bytes = 0;
   std::vector<void*> allocs;
   int precision = EXPECTO_PRECISION_BF16X6;
+  int fc_splits = kFcSplitsDefault;   // FC1 split-K slabs: a divisor of 2120 K blocks, <= 32
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, int>> pending;  // (layer, event index of start)
@@ -753,7 +756,7 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
   int rc;
   const long long m_tiles = (nb + gemm_bm() - 1) / gemm_bm();
   const int n_tiles1 = npad_of(kFc1Out) / GBN;
-  const int splits = kFcSplits;
+  const int splits = h->fc_splits;
   {
     GemmArgs a{};
     a.A = act;
@@ -1115,7 +1118,7 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
       unsigned* md = reinterpret_cast<unsigned*>(h->slab_mask);
       EXPECTO_HIP_CHECK(hipMemsetAsync(md, 0, tiles * sizeof(unsigned), st));
       fc1_slab_mask<<<dim3((R + 255) / 256), dim3(256), 0, st>>>(var_pos, nv, v0, R, (int)gemm_bm(),
-                                                                  kFc1In / kFcSplits, md);
+                                                                  kFc1In / h->fc_splits, md);
       if ((rc = check_launch("fc1_slab_mask"))) return rc;
       mask = md;
       if (h->profiling) {   // executed share of the slabs, for the MAC count
@@ -1124,7 +1127,7 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
         EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
         int bits = 0;
         for (unsigned x : hm) bits += __builtin_popcount(x);
-        frac = (double)bits / (tiles * kFcSplits);
+        frac = (double)bits / (tiles * h->fc_splits);
       }
     }
     if ((rc = run_fc(h, act6, nullptr, R, y_alt, st, h->c_rows, mask, frac))) return rc;
@@ -1304,7 +1307,12 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   }
   if ((rc = check_launch("repack"))) return fail(rc);
   const size_t pf = p_floats(max_batch), qf = q_floats(max_batch);
-  const size_t partf = (size_t)kFcSplits * max_batch * kHidLd;
+  if (const char* e = getenv("EXPECTO_FC1_SPLITS")) {   // tuning knob (fixed per handle: sums never
+    const int v = atoi(e);                               // depend on the batch)
+    EXPECTO_REQUIRE(v >= 1 && v <= 32 && (kFc1In / GBK) % v == 0, "EXPECTO_FC1_SPLITS must divide 2120 and be <= 32");
+    h->fc_splits = v;
+  }
+  const size_t partf = (size_t)h->fc_splits * max_batch * kHidLd;
   if ((rc = dalloc(h, &h->P, act_alloc(pf))) || (rc = dalloc(h, &h->Q, act_alloc(qf))) ||
       (rc = dalloc(h, &h->part, partf)) || (rc = dalloc(h, &h->h1, act_alloc((size_t)max_batch * kHidLd))))
     return fail(rc);
