@@ -211,8 +211,70 @@ def replicate_main(argv=None):
             np.save(f'{args.out_dir}/{g[0]}', pr)
 
 
+def atac_peak_bins(chrom, tss, strand, peaks: dict) -> np.ndarray:
+    """expecto_intersect_chip_atac.py:198-217 get_atac_peak_bins: the 200 200-bp bins of the
+    TSS receptive field, 1 where more than half a bin is covered by peaks.  The intersection
+    (pybedtools ``tss_rf.intersect(peaks)``: the overlapping part of each peak) and the
+    reference's inclusive ``[start, end + 1)`` marking are reproduced; bins are in genomic
+    order for either strand, as in the reference."""
+    rf_start = tss - 20899 - strand * 100
+    rf_end = tss + 20900 - strand * 100
+    regions = np.zeros(200 * 200)
+    st, en = peaks.get(chrom, (np.zeros(0, np.int64), np.zeros(0, np.int64)))
+    hit = (st < rf_end) & (en > rf_start)
+    for s0, e0 in zip(np.maximum(st[hit], rf_start), np.minimum(en[hit], rf_end)):
+        regions[int(s0) - rf_start:int(e0) - rf_start + 1] = 1
+    return (regions.reshape(-1, 200).sum(axis=1) > 100).astype('float')
+
+
+def read_bed(path) -> dict:
+    """chrom -> (starts, ends) of a BED file (first three columns)."""
+    df = pd.read_csv(path, sep='\t', header=None, comment='#', usecols=[0, 1, 2], dtype={0: str})
+    return {c: (g[1].to_numpy(np.int64), g[2].to_numpy(np.int64)) for c, g in df.groupby(0, sort=False)}
+
+
+def intersect_main(argv=None):
+    """expecto_intersect_chip_atac.py main() (:16-111): TSS features with the ChIP-seq tracks
+    (TF, or TF + histone) of every window multiplied by the ATAC peak bin of its shift."""
+    p = argparse.ArgumentParser(description='Replicate ExPecto chromatin features')
+    p.add_argument('annoFile')
+    p.add_argument('peaks_file', help='Bed file containing ATAC binary peak calls')
+    p.add_argument('-o', dest="out_dir", type=str, default='temp_expecto_intersect')
+    p.add_argument('--tf_only', action='store_true')
+    p.add_argument('--features_tsv', default='./resources/deepsea_beluga_2002_features.tsv')
+    _common_args(p)
+    args = p.parse_args(argv)
+    if args.windowsize != 2000:
+        raise ValueError("--windowsize must be 2000 (Beluga.py:43)")
+    os.makedirs(args.out_dir, exist_ok=True)
+    fasta = Fasta(args.genome)
+    model = _load_model(args)
+    feats_df = pd.read_csv(args.features_tsv, sep='\t', header=0, index_col=0)
+    if args.tf_only:
+        chip = np.where(feats_df['Assay type'] == 'TF')[0]
+    else:
+        chip = np.where((feats_df['Assay type'] == 'Histone') | (feats_df['Assay type'] == 'TF'))[0]
+    genes = _anno_genes(args.annoFile)
+    peaks = read_bed(args.peaks_file)
+    dg = DeviceGenome(fasta)
+    pipe = TSSPipeline(model.engine(), dg)
+    chip_d = torch.from_numpy(chip.astype(np.int64)).to(pipe.dev)
+    out = []
+    for b in _batches(genes, args.gene_batch):
+        y = pipe.predict([g[1] for g in b], [g[2] for g in b], [g[3] for g in b])     # [2, G, S, 2002]
+        bins = np.stack([atac_peak_bins(g[1], g[2], g[3], peaks) for g in b]).astype(np.float32)
+        mask = torch.from_numpy(bins).to(pipe.dev)                                   # [G, S]
+        y[..., chip_d] *= mask[None, :, :, None]                                      # x1.0 / x0.0: exact
+        out.append(tss_reduce(y[0], y[1], pipe.w_d).cpu().numpy())
+    arr = np.concatenate(out, 0) if out else np.zeros((0, 20020))
+    np.save(f'{args.out_dir}/Xreducedall.2002.atac_x_chip', arr)
+    return arr
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "replicate":
         replicate_main(sys.argv[2:])
+    elif len(sys.argv) > 1 and sys.argv[1] == "intersect":
+        intersect_main(sys.argv[2:])
     else:
         compute_main(sys.argv[1:] if len(sys.argv) > 1 and sys.argv[1] != "compute" else sys.argv[2:])

@@ -94,3 +94,20 @@ def test_h5_scalar_and_string_datasets(tmp_path):
     assert r["ref_preds"].shape == () and r["ref_preds"] == np.float32(1.25)
     assert list(r["record_ids"]) == [b"chr1:1-9|HG1", b"x"]
     assert np.array_equal(r["m"], np.arange(6.0).reshape(2, 3))
+
+
+@pytest.mark.parametrize("rf", [False, True])
+def test_closest_genes_match_reference(tmp_path, rf):
+    """make_closest_genes_file.py drop-in (host logic) == the reference's files byte for byte."""
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import make_golden_extra as mg
+    from expecto_amd import closest
+    p = mg.write_inputs(str(tmp_path))
+    out = tmp_path / "cg"
+    closest.main([p["vcf"], "--geneanno_file", p["anno"], "-o", str(out)] + (["--all_in_receptive_field"] if rf else []))
+    tag = "_rf" if rf else ""
+    for name in ("closest_genes", "snps_hg19"):
+        ext = "tsv" if name == "closest_genes" else "vcf"
+        got = open(out / f"{name}.{ext}").read()
+        assert got == open(os.path.join(GOLDEN, "extra", f"{name}{tag}.{ext}")).read(), name
