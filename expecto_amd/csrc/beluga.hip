@@ -581,6 +581,7 @@ struct expecto_beluga {
   std::vector<void*> allocs;
   int precision = EXPECTO_PRECISION_BF16X6;
   int fc_splits = kFcSplitsDefault;   // FC1 split-K slabs: a divisor of 2120 K blocks, <= 32
+  int conv_tile = 0;                  // f16x3 conv M tile: 0 = auto (conv_tile_rows), 256 or 384
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, int>> pending;  // (layer, event index of start)
@@ -670,14 +671,29 @@ bool planes_gemm() { return g_precision != EXPECTO_PRECISION_FP32; }
 long long gemm_bm() { return planes_gemm() ? X6P_BM : GBM; }
 float exp2i(int e) { return std::ldexp(1.0f, e); }
 
+// M tile rows of an f16x3 conv launch.  beluga_conv_h3r (384 rows) and the 256-row kernels give
+// bitwise-equal results, so the choice is free per launch: 384 rows feed 1.5x the MFMAs per
+// weight piece and stage barrier (tools/gemm_bench, 1000 windows: conv2 +5 %, conv4 +3 %; conv3
+// equal to the 8-wave kernel; conv6 -3 %, its 113-row windows give a short grid), so auto takes
+// it for every launch of the pool layers (one kernel per layer, incl. the small alt-delta
+// launches) and leaves the ReLU layers on the 8-wave kernel.
+int conv_tile_rows(const expecto_beluga* h, bool pool) {
+  if (g_precision != EXPECTO_PRECISION_F16X3) return (int)gemm_bm();
+  if (h->conv_tile) return h->conv_tile;
+  return pool ? 384 : 256;
+}
+
 template <int LAYER, int EPI>
-int launch_gemm(const GemmArgs& a, int splits, hipStream_t st) {
+int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
+  if (bm == 0) bm = (int)gemm_bm();
   const long long nblk = a.m_tiles * a.n_tiles * splits;
   EXPECTO_REQUIRE(nblk > 0 && nblk < (1LL << 31), "gemm grid out of range");
   EXPECTO_REQUIRE(a.kper % GBK == 0 && a.kper > 0, "gemm K not a multiple of 32");
   EXPECTO_REQUIRE(a.lda % 4 == 0 && a.ldb % 4 == 0, "gemm leading dims must be multiples of 4");
   EXPECTO_REQUIRE(a.taps == 1 || (a.taps == 8 && a.lda % GBK == 0), "conv GEMM needs Cin % 32 == 0");
-  EXPECTO_REQUIRE(a.m_tiles * gemm_bm() >= a.M, "gemm M tiles do not cover M");
+  EXPECTO_REQUIRE(a.m_tiles * bm >= a.M, "gemm M tiles do not cover M");
+  EXPECTO_REQUIRE(bm == gemm_bm() || (bm == 384 && a.taps == 8 && g_precision == EXPECTO_PRECISION_F16X3),
+                  "384-row tiles: f16x3 conv kernel only");
   if (g_precision == EXPECTO_PRECISION_BF16X6) {
     EXPECTO_REQUIRE(a.Bp != nullptr && a.lda % GBK == 0 && a.ldb % GBK == 0, "bf16x6 GEMM needs planes, K % 32");
     beluga_gemm_x6q<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
@@ -687,7 +703,9 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st) {
     if (a.taps == 8) {   // conv: chunk-slab kernel (one Toeplitz A slab per 32-channel chunk)
       EXPECTO_REQUIRE(splits == 1 && a.kper == a.ldb && a.ldb == 8 * a.lda && !a.m_fastest && !a.a_rows,
                       "f16x3 conv GEMM: full K, no split, no row gather");
-      if constexpr (EPI == EPI_RELU)   // 8-wave variant: +2-5 % on conv3/5/6 (tools/gemm_bench), same bits
+      if (bm == 384)
+        beluga_conv_h3r<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
+      else if constexpr (EPI == EPI_RELU)   // 8-wave variant: +2-5 % on conv3/5/6 (tools/gemm_bench), same bits
         beluga_conv_h3w<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
       else
         beluga_conv_h3q<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
@@ -726,7 +744,8 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
   a.kper = 8 * g.cin;
   a.taps = 8;
   a.n_tiles = npad_of(g.cout) / GBN;
-  a.m_tiles = (a.M + gemm_bm() - 1) / gemm_bm();
+  const int bm = conv_tile_rows(h, pool);
+  a.m_tiles = (a.M + bm - 1) / bm;
   a.m_fastest = 0;
   a.bias = h->bt[l];
   a.C = dst;
@@ -739,13 +758,13 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
   if (h->profiling) h->macs[l + 1] += (double)a.M * g.cout * a.kper;
   if (pool) {
     EXPECTO_REQUIRE(s_in % 4 == 0, "pool epilogue needs 4-aligned row groups");
-    return l == 0 ? launch_gemm<2, EPI_RELU_POOL4>(a, 1, st) : launch_gemm<4, EPI_RELU_POOL4>(a, 1, st);
+    return l == 0 ? launch_gemm<2, EPI_RELU_POOL4>(a, 1, st, bm) : launch_gemm<4, EPI_RELU_POOL4>(a, 1, st, bm);
   }
   switch (l) {
-    case 1: return launch_gemm<3, EPI_RELU>(a, 1, st);
-    case 2: return launch_gemm<4, EPI_RELU>(a, 1, st);
-    case 3: return launch_gemm<5, EPI_RELU>(a, 1, st);
-    default: return launch_gemm<6, EPI_RELU>(a, 1, st);
+    case 1: return launch_gemm<3, EPI_RELU>(a, 1, st, bm);
+    case 2: return launch_gemm<4, EPI_RELU>(a, 1, st, bm);
+    case 3: return launch_gemm<5, EPI_RELU>(a, 1, st, bm);
+    default: return launch_gemm<6, EPI_RELU>(a, 1, st, bm);
   }
 }
 
@@ -1311,6 +1330,11 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
     const int v = atoi(e);                               // depend on the batch)
     EXPECTO_REQUIRE(v >= 1 && v <= 32 && (kFc1In / GBK) % v == 0, "EXPECTO_FC1_SPLITS must divide 2120 and be <= 32");
     h->fc_splits = v;
+  }
+  if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)
+    const int v = atoi(e);
+    EXPECTO_REQUIRE(v == 0 || v == 256 || v == 384, "EXPECTO_CONV_TILE must be 0 (auto), 256 or 384");
+    h->conv_tile = v;
   }
   const size_t partf = (size_t)h->fc_splits * max_batch * kHidLd;
   if ((rc = dalloc(h, &h->P, act_alloc(pf))) || (rc = dalloc(h, &h->Q, act_alloc(qf))) ||

@@ -531,8 +531,8 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
 // XOR swizzle on the SOURCE offset, undone on the read: position = chunk ^ (-(row >> 2) & 3).
 typedef float floatx4v __attribute__((ext_vector_type(4)));
 
-template <int EPI, int FMT, int NB = 10>
-__device__ __forceinline__ void gemm_epilogue16(const GemmArgs& p, const floatx4v (&acc)[4][NB], long long mw, int n0,
+template <int EPI, int FMT, int NB = 10, int MB = 4>
+__device__ __forceinline__ void gemm_epilogue16(const GemmArgs& p, const floatx4v (&acc)[MB][NB], long long mw, int n0,
                                                 int ks, int lane) {
   const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
@@ -543,7 +543,7 @@ __device__ __forceinline__ void gemm_epilogue16(const GemmArgs& p, const floatx4
     // f16x3: acc * 2^-(s_in + s_w[n]) is exact (power of 2), so the value equals the unscaled sum
     const float cs = (FMT == 2 && EPI != EPI_PARTIAL) ? p.col_scale[n] : 1.f;
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) {
+    for (int mb = 0; mb < MB; ++mb) {
       const long long m4 = mw + mb * 16 + 4 * fq;   // first of this lane's 4 rows (multiple of 4)
       if (EPI == EPI_PARTIAL) {
         float* cp = p.C + (long long)ks * p.split_stride + n;
@@ -821,6 +821,27 @@ constexpr int H3C_BSTAGE = 2 * X6P_B_PLANE;            // 20,480 B
 template <int NSB>
 constexpr int h3c_lds() { return 2 * H3C_ASLAB + NSB * H3C_BSTAGE; }
 
+// Slab geometry of the chunk-slab kernel for MB 16-row blocks per wave (tile BM = 64 * MB rows):
+//   MB 4: 256-row tile, 288-row slab (18 groups, 9 LDS-DMA pieces per wave and chunk);
+//   MB 6: 384-row tile, 400-row slab (25 groups = 50 pieces, 13 per wave: waves 2 and 3 repeat
+//         piece 49, identical bytes to the same LDS address), LDS 2 x 51,200 + 3 x 20,480 =
+//         163,840 B = all of a CU's LDS.  Each B (weight) piece then feeds 1.5x the MFMAs, and
+//         a K-block stage (one barrier) is 180 instead of 120 MFMAs per wave.
+template <int MB>
+struct SlabGeo {
+  static constexpr int BM = 64 * MB;
+  static constexpr int GROUPS = MB == 4 ? 18 : (BM + 7 + 15) / 16;
+  static constexpr int AROWS = 16 * GROUPS;
+  static constexpr int APLANE = AROWS * 64;
+  static constexpr int ASLAB = 2 * APLANE;
+  static constexpr int PIECES = 2 * GROUPS;
+  static constexpr int NA = (PIECES + 3) / 4;          // slab pieces per wave and chunk
+  static constexpr int EXTRA = NA - 8;                 // taps 0 .. EXTRA-1 issue 2 pieces, the rest 1
+  static_assert(AROWS >= BM + 7 && NA >= 8 && NA <= 16, "slab geometry");
+};
+template <int NSB, int MB>
+constexpr int h3c_lds_mb() { return 2 * SlabGeo<MB>::ASLAB + NSB * H3C_BSTAGE; }
+
 // ReLU epilogue of the f16x3 conv kernel through LDS.  A wave's 64 x 160 tile is, per output
 // row, ONE contiguous 640-B run of the planes layout (5 blocks x [hi 64 B | lo 64 B]); the
 // accumulator layout scatters it over 2-byte pieces.  Each half of the tile (32 rows) is split
@@ -829,11 +850,12 @@ constexpr int h3c_lds() { return 2 * H3C_ASLAB + NSB * H3C_BSTAGE; }
 constexpr int H3E_ROW = 656;
 constexpr int H3E_WAVE = 32 * H3E_ROW;                 // 20,992 B per wave
 
-__device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const floatx4v (&acc)[4][10], long long mw,
+template <int MB = 4>
+__device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const floatx4v (&acc)[MB][10], long long mw,
                                                      int n0, int lane, char* lds) {
   const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
+  for (int half = 0; half < MB / 2; ++half) {
 #pragma unroll
     for (int nb = 0; nb < 10; ++nb) {
       const int n = n0 + nb * 16 + fr;
@@ -876,9 +898,10 @@ __device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const fl
 
 // NSB: depth of the B ring (3: loads of stage s+2 in flight during stage s; 4: s+3).
 // TM 16 (timing probe, wrong results): no vmcnt wait at stage ends.
-template <int LAYER, int EPI, int TM, int NSB>
+template <int LAYER, int EPI, int TM, int NSB, int MB = 4>
 __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem) {
-  static_assert(NSB == 3 || NSB == 4, "B ring depth");
+  static_assert(NSB == 3 || (NSB == 4 && MB == 4), "B ring depth");
+  using G = SlabGeo<MB>;
   constexpr int ROW_KB = 128;                         // global bytes per row and 32-channel block
   const unsigned nblk = gridDim.x, bid = blockIdx.x;
   const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
@@ -887,20 +910,20 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
   const long long mt = (long long)(lin / (unsigned)p.n_tiles) % p.m_tiles;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const long long m0 = mt * X6P_BM;
+  const long long m0 = mt * G::BM;
   const int n0 = nt * GBN;
   const int kb_total = (int)(p.ldb / GBK);
   const long long lda_kb = p.lda / GBK;
   const int nchunk = (int)lda_kb;                     // Cin / 32
   const int nk = nchunk * 8;
   auto swz = [](int r) { return (-(r >> 2)) & 3; };
-  // A slab pieces: P = wave + 4*i (i < 9) of 36 = 18 row groups x 2 planes
+  // A slab pieces: P = wave + 4*i (i < NA) of G::PIECES = row groups x 2 planes
   const char* Ab = (const char*)p.A + m0 * lda_kb * ROW_KB;
   const long long last_row = p.M - 1 + 7;             // Toeplitz rows read by the last output row
-  unsigned aoff[9];
+  unsigned aoff[G::NA];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    const int P = wave + 4 * i, g = P >> 1, pl = P & 1;
+  for (int i = 0; i < G::NA; ++i) {
+    const int P = min(wave + 4 * i, G::PIECES - 1), g = P >> 1, pl = P & 1;
     const int r = 16 * g + (lane >> 2);
     const long long m = min(m0 + r, last_row);
     const int c = (lane & 3) ^ swz(r);
@@ -918,12 +941,12 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
   const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, 0x7fffffff, 0x00020000);
   char* const aslab = smem;
-  char* const bring = smem + 2 * H3C_ASLAB;
+  char* const bring = smem + 2 * G::ASLAB;
   auto issue_a = [&](int chunk, int i0, int ni) {      // pieces i0.. of chunk's slab
-    char* base = aslab + (chunk & 1) * H3C_ASLAB;
+    char* base = aslab + (chunk & 1) * G::ASLAB;
     for (int i = i0; i < i0 + ni; ++i) {
-      const int P = wave + 4 * i;
-      char* dst = base + (P & 1) * H3C_APLANE + (P >> 1) * 1024;
+      const int P = min(wave + 4 * i, G::PIECES - 1);
+      char* dst = base + (P & 1) * G::APLANE + (P >> 1) * 1024;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (lds_void*)dst, 16, aoff[i], (unsigned)(chunk * ROW_KB), 0, 0);
     }
   };
@@ -936,23 +959,23 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
                                                (unsigned)(s * ROW_KB), 0, 0);
   };
 
-  floatx4v acc[4][10];
+  floatx4v acc[MB][10];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
+  for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
     for (int nb = 0; nb < 10; ++nb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[mb][nb][r] = 0.f;
   const int fr = lane & 15, fq = lane >> 4;
   const int brow = fr * 64 + 16 * (fq ^ swz(fr));
-  // A fragment of (row group mb, tap t): slab row wave*64 + mb*16 + fr + t
-  auto read_a = [&](const char* slab, int t, bf16x8 (&a)[4][3]) {
+  // A fragment of (row group mb, tap t): slab row wave*16*MB + mb*16 + fr + t
+  auto read_a = [&](const char* slab, int t, bf16x8 (&a)[MB][3]) {
     const int rr2 = fr + t;
-    const int off = (wave * 64 + rr2) * 64 + 16 * (fq ^ swz(rr2));
+    const int off = (wave * 16 * MB + rr2) * 64 + 16 * (fq ^ swz(rr2));
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) {
+    for (int mb = 0; mb < MB; ++mb) {
       a[mb][0] = *(const bf16x8*)(slab + off + mb * 1024);
-      a[mb][1] = *(const bf16x8*)(slab + off + mb * 1024 + H3C_APLANE);
+      a[mb][1] = *(const bf16x8*)(slab + off + mb * 1024 + G::APLANE);
     }
   };
   auto read_b = [&](const char* base, int nb, bf16x8 (&b)[3]) {
@@ -960,13 +983,13 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
     b[0] = *(const bf16x8*)(br);
     b[1] = *(const bf16x8*)(br + X6P_B_PLANE);
   };
-  auto unit = [&](const bf16x8 (&a)[4][3], int nb, const bf16x8 (&b)[3]) {
+  auto unit = [&](const bf16x8 (&a)[MB][3], int nb, const bf16x8 (&b)[3]) {
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) acc[mb][nb] = planes_mfma<2>(acc[mb][nb], a[mb], b);
+    for (int mb = 0; mb < MB; ++mb) acc[mb][nb] = planes_mfma<2>(acc[mb][nb], a[mb], b);
   };
   auto pin = [&](int nv) {
 #pragma unroll
-    for (int i = 0; i < 12; ++i) {
+    for (int i = 0; i < 3 * MB; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       if ((i % 6) == 0 && i < 6 * nv) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
       if ((i & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
@@ -975,7 +998,7 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
   };
 
   // prologue: slab 0, B stages 0 .. NSB-2
-  issue_a(0, 0, 9);
+  issue_a(0, 0, G::NA);
   issue_b(0, 0);
   issue_b(min(1, nk - 1), 1);
   if constexpr (NSB == 4) {
@@ -986,11 +1009,11 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
   }
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  bf16x8 as[4][3];
+  bf16x8 as[MB][3];
   read_a(aslab, 0, as);
   int slot = 0;
   for (int c = 0; c < nchunk; ++c) {
-    const char* slab = aslab + (c & 1) * H3C_ASLAB;
+    const char* slab = aslab + (c & 1) * G::ASLAB;
     const bool more_a = (c + 1 < nchunk) && !(TM & 2);
     for (int t = 0; t < 8; ++t) {
       const int s = c * 8 + t;
@@ -1003,16 +1026,18 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
       for (int nb = 0; nb < 10; ++nb) {
         int nv = 0;
         if (nb == 0 && more_a) {
-          // slab c+1, 9 pieces: NSB 3 -> taps 0..7 as 2,1,1,1,1,1,1,1; NSB 4 -> taps 0..5 as
-          // 2,2,2,1,1,1 (the last two taps issue B only, so vmcnt(10) at tap 7 covers the slab)
-          const int i0 = NSB == 3 ? (t == 0 ? 0 : t + 1) : (t < 3 ? 2 * t : t + 3);
-          const int ni = NSB == 3 ? (t == 0 ? 2 : 1) : (t < 3 ? 2 : (t < 6 ? 1 : 0));
+          // slab c+1, NA pieces: NSB 3 -> taps 0..EXTRA-1 two pieces, the others one (MB 4:
+          // 2,1,1,1,1,1,1,1; MB 6: 2,2,2,2,2,1,1,1); NSB 4 (MB 4) -> taps 0..5 as 2,2,2,1,1,1
+          // (the last two taps issue B only, so vmcnt(10) at tap 7 covers the slab)
+          constexpr int E = G::EXTRA;
+          const int i0 = NSB == 3 ? (t < E ? 2 * t : E + t) : (t < 3 ? 2 * t : t + 3);
+          const int ni = NSB == 3 ? (t < E ? 2 : 1) : (t < 3 ? 2 : (t < 6 ? 1 : 0));
           if (ni > 0) issue_a(c + 1, i0, ni);
           nv = ni;
         }
         if (nb == 2 && !(TM & 2)) {
           issue_b(min(s + NSB - 1, nk - 1), lslot);
-          nv = 2;
+          nv = MB == 4 ? 2 : 3;
         }
         if (nb + 1 < 10) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
         unit(as, nb, (nb & 1) ? b1 : b0);
@@ -1032,15 +1057,15 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
       asm volatile("" ::: "memory");
       slot = nslot;
     }
-    if (c + 1 < nchunk) read_a(aslab + ((c + 1) & 1) * H3C_ASLAB, 0, as);
+    if (c + 1 < nchunk) read_a(aslab + ((c + 1) & 1) * G::ASLAB, 0, as);
   }
   if constexpr (EPI == EPI_RELU) {
     // the ring's last (duplicate) B pieces may still be landing: drain before reusing LDS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    epilogue_relu_h2_lds(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
+    epilogue_relu_h2_lds<MB>(p, acc, m0 + wave * 16 * MB, n0, lane, smem + wave * H3E_WAVE);
   } else {
-    gemm_epilogue16<EPI, 2>(p, acc, m0 + wave * 64, n0, 0, lane);
+    gemm_epilogue16<EPI, 2, 10, MB>(p, acc, m0 + wave * 16 * MB, n0, 0, lane);
   }
 }
 
@@ -1287,6 +1312,14 @@ template <int LAYER, int EPI, int TM = 0, int NSB = 3>
 __global__ __launch_bounds__(256, 1) void beluga_conv_h3q(GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[h3c_lds<NSB>()];
   gemm_conv_h3_body<LAYER, EPI, TM, NSB>(p, smem);
+}
+
+// the same with 384-row tiles (6 row blocks per wave): 1.5x the MFMAs per weight piece and per
+// stage barrier; bitwise equal to beluga_conv_h3q (same products and k order per output)
+template <int LAYER, int EPI, int TM = 0>
+__global__ __launch_bounds__(256, 1) void beluga_conv_h3r(GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[h3c_lds_mb<3, 6>()];
+  gemm_conv_h3_body<LAYER, EPI, TM, 3, 6>(p, smem);
 }
 
 // B planes for beluga_gemm_x6q from a K-contiguous fp32 B [rows][K] (K % 32 == 0).

@@ -58,6 +58,11 @@ Variant mkc3(const char* name) {
 }
 
 template <int L, int EPI, int TM = 0>
+Variant mkr3(const char* name) {
+  return {name, 384, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3r<L, EPI, TM><<<nblk, 256>>>(a); }};
+}
+
+template <int L, int EPI, int TM = 0>
 Variant mkw3(const char* name) {
   return {name, X6P_BM, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3w<L, EPI, TM><<<nblk, 512>>>(a); }};
 }
@@ -137,12 +142,15 @@ int main(int argc, char** argv) {
     vs.push_back(mk6q<2, EPI_RELU_POOL4>("x6q"));
     vs.push_back(mkc3<2, EPI_RELU_POOL4>("h3c"));
     vs.push_back(mkw3<2, EPI_RELU_POOL4>("h3w"));
+    vs.push_back(mkr3<2, EPI_RELU_POOL4>("h3r"));
+    vs.push_back(mkr3<2, EPI_RELU_POOL4, 2>("h3r_noglds"));
     vs.push_back(mkc3<2, EPI_RELU_POOL4, 2>("h3c_noglds"));
   } else {
     vs.push_back(mk6<3, EPI_RELU, 4, 1>("x6_wm4_b1"));
     vs.push_back(mk6q<3, EPI_RELU>("x6q"));
     vs.push_back(mkc3<3, EPI_RELU>("h3c"));
     vs.push_back(mkw3<3, EPI_RELU>("h3w"));
+    vs.push_back(mkr3<3, EPI_RELU>("h3r"));
   }
   auto args_for = [&](int bm, float* C) {
     GemmArgs a{};
@@ -156,7 +164,7 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   std::vector<std::vector<float>> times(vs.size());
-  std::vector<float> ref(csz), out(csz);
+  std::vector<float> ref(csz), out(csz), ref_h3;
   const char* only = getenv("VARIANT");   // run just this variant (profiling)
   if (only) {
     std::vector<Variant> keep;
@@ -207,6 +215,13 @@ int main(int argc, char** argv) {
           }
         } else {
           CK(hipMemcpy(v == 0 ? ref.data() : out.data(), C, csz * 4, hipMemcpyDeviceToHost));
+        }
+        if (vs[v].name == "h3c") ref_h3 = out;
+        if (vs[v].name.rfind("h3", 0) == 0 && vs[v].name != "h3c" && !ref_h3.empty() &&
+            vs[v].name.find("noglds") == std::string::npos) {
+          size_t bad = 0;
+          for (size_t i = 0; i < csz; ++i) bad += memcmp(&ref_h3[i], &out[i], 4) != 0;
+          printf("variant %s vs h3c: %zu elements differ bitwise\n", vs[v].name.c_str(), bad);
         }
         if (v > 0) {
           double mx = 0, md = 0;
