@@ -144,6 +144,8 @@ int main(int argc, char** argv) {
     vs.push_back(mkw3<2, EPI_RELU_POOL4>("h3w"));
     vs.push_back(mkr3<2, EPI_RELU_POOL4>("h3r"));
     vs.push_back(mkr3<2, EPI_RELU_POOL4, 2>("h3r_noglds"));
+    vs.push_back(mkr3<2, EPI_RELU_POOL4, 4>("h3r_nobar"));
+    vs.push_back(mkr3<2, EPI_RELU_POOL4, 6>("h3r_noglds_nobar"));
     vs.push_back(mkc3<2, EPI_RELU_POOL4, 2>("h3c_noglds"));
   } else {
     vs.push_back(mk6<3, EPI_RELU, 4, 1>("x6_wm4_b1"));
