@@ -66,7 +66,7 @@ def kernel_name(layer: str, precision: str) -> str:
         return f"beluga_gemm_x6q<{l}, {e}, 0>"
     if precision == "f16x3":
         if l in (7, 8):
-            return f"beluga_gemm_h3q<{l}, {e}, 0, 3>"
+            return f"beluga_fc_h3<{l}, {e}, 0, 3>"
         return f"beluga_conv_h3w<{l}, {e}, 0>" if e == 0 else f"beluga_conv_h3r<{l}, {e}, 0>"
     return f"beluga_gemm<{l}, {e}, 4, 2, 32, 1>"
 WINDOW_MACS = sum(LAYER_MACS.values())
@@ -266,6 +266,20 @@ def main():
             "layer_ms_per_step": {k: ms / 2 for k, (ms, c, m) in l2.items()},
             "layer_tflops": {k: 2.0 * m / (ms * 1e-3) / 1e12 for k, (ms, c, m) in l2.items() if ms > 0},
             "roofline": roofline(l2, eng.precision)}
+        # the same headline workload under the other two arithmetics (all three pass the same
+        # parity bar; DESIGN.md accuracy table): exact fp32 MFMA and fp32-faithful bf16x6
+        alt_prec = {}
+        for prec in ("bf16x6", "fp32"):
+            if prec == eng.precision:
+                continue
+            base = eng.precision
+            eng.set_precision(prec)
+            elp, lp = time_workload(pipe, eng, prep, shifts, n, 3, 1, dev, 1)
+            eng.set_precision(base)
+            rp = roofline(lp, prec)
+            alt_prec[prec] = {"variants_per_s": n * 3 / elp, "ms_per_step": elp / 3 * 1e3,
+                              "dominant": {k: rp[k] for k in ("kernel", "layer", "achieved", "peak", "frac")}}
+        extras["headline_other_precisions"] = alt_prec
         rec["extra_workloads"] = extras
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from expecto_amd.encode import seqs_to_codes

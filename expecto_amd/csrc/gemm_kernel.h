@@ -8,6 +8,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 namespace expecto {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -524,7 +526,8 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
 }
 
 // TM: timing-only probes for tools/gemm_bench (wrong results): 2 = no LDS-DMA in the loop,
-// 4 = no barrier in the loop, 8 = LDS-DMA always from stage 0's (L2-hot) addresses.
+// 4 = no barrier in the loop, 8 = LDS-DMA always from stage 0's (L2-hot) addresses;
+// beluga_fc_h3 also 16 = no A loads in the loop, 32 = no B pieces in the loop.
 // 16x16x32 lane layout: A/B lane l holds row/col (l & 15), k = 8*(l >> 4)..+7; C lane l
 // holds col (l & 15), rows 4*(l >> 4)..+3.  The 16 lanes of one ds_read_b128 lane group then
 // read mixed chunks, so LDS-DMA pieces (lane-linear 1 KiB = 16 rows x 64 B) are placed with an
@@ -802,6 +805,188 @@ __device__ __forceinline__ void gemm_planes_body(const GemmArgs& p, char* smem) 
     buf = nbuf;
   }
   gemm_epilogue16<EPI, FMT>(p, acc, m0 + wave * 64, n0, ks, lane);
+}
+
+// ---- f16x3 FC GEMM: A fragments straight into registers ---------------------------------
+// In the FC layers every wave owns its 64 A rows (no Toeplitz overlap, nothing shared between
+// the waves), so staging A through LDS is pure overhead: 8 LDS-DMA pieces + 8 ds_reads per
+// wave and K block, next to 5 B pieces (tools/gemm_bench fc1: 364 fp32-equivalent TF/s, 538
+// with the in-loop LDS-DMA removed).  Here each lane loads its own MFMA fragments (row l & 15
+// of a 16-row block, k 8*(l >> 4)..+7: 16 B per plane) with global_load_dwordx4 two K blocks
+// ahead into a 3-deep register ring; only B (shared by the 4 waves) goes through an LDS ring.
+// Same operands, products and k order per output as gemm_planes_body<PL=2>: bitwise equal.
+constexpr int FCH_BSTAGE = 2 * X6P_B_PLANE;           // one B stage: 160 cols x 32 k x 2 planes
+
+// NS: ring depth of both operands (A register sets and B LDS slots): K block s+NS-1 is loaded
+// while block s computes.
+template <int LAYER, int EPI, int TM, int NS>
+__device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
+  static_assert(NS == 3 || NS == 4, "ring depth");
+  constexpr int ROW_KB = 128;                          // bytes per row and 32-deep K block (2 planes)
+  const unsigned nblk = gridDim.x, bid = blockIdx.x;
+  const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
+  const unsigned lin =
+      p.linear_order ? bid : (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  long long mt;
+  int nt, ks;
+  if (p.m_fastest) {
+    mt = lin % p.m_tiles;
+    const long long rest = lin / p.m_tiles;
+    nt = (int)(rest % p.n_tiles);
+    ks = (int)(rest / p.n_tiles);
+  } else {
+    nt = (int)(lin % (unsigned)p.n_tiles);
+    const long long rest = lin / (unsigned)p.n_tiles;
+    mt = rest % p.m_tiles;
+    ks = (int)(rest / p.m_tiles);
+  }
+  if (p.ks_mask && !((p.ks_mask[mt] >> ks) & 1u)) return;   // slab unchanged: partials already in C
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const long long m0 = mt * X6P_BM;
+  const int n0 = nt * GBN;
+  const int kb_total = (int)(p.ldb / GBK);
+  const int gs0 = ks * (p.kper / GBK);
+  const long long lda_kb = p.lda / GBK;
+  const int nk = p.kper / GBK;
+  auto swz = [](int r) { return (-(r >> 2)) & 3; };
+  const int fr = lane & 15, fq = lane >> 4;
+  // this lane's A source: row m0 + wave*64 + 16*mb + fr (clamped), bytes 16*fq of each plane
+  const char* aptr[4];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) {
+    long long m = m0 + wave * 64 + mb * 16 + fr;
+    if (m > p.M - 1) m = p.M - 1;
+    const long long kb0 = (p.a_rows ? p.a_rows[m] / GBK : m * lda_kb) + gs0;
+    aptr[mb] = (const char*)p.A + kb0 * ROW_KB + 16 * fq;
+  }
+  const char* Bb = (const char*)p.Bp + ((long long)n0 * kb_total + gs0) * ROW_KB;
+  unsigned boff[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int g = wave + 4 * j;                        // 20 pieces: plane g / 10, cols 16*(g % 10)
+    const int pl = g / 10, r = 16 * (g % 10) + (lane >> 2);
+    const int c = (lane & 3) ^ swz(r);
+    boff[j] = (unsigned)((long long)r * kb_total * ROW_KB + pl * 64 + 16 * c);
+  }
+  const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, 0x7fffffff, 0x00020000);
+  auto issue_b = [&](int s, int slot, int j0, int nj) {
+    if constexpr ((TM & 8) != 0) s = 0;
+    char* base = smem + slot * FCH_BSTAGE;
+    for (int j = j0; j < j0 + nj; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + (wave + 4 * j) * 1024), 16, boff[j],
+                                               (unsigned)(s * ROW_KB), 0, 0);
+  };
+  // A fragments of K block s into ring set `set` (two loads per row block: hi, lo plane)
+  bf16x8 afr[NS][4][3];
+  auto load_a = [&](int s, bf16x8 (&a)[4][3], int mb0, int nmb) {
+    if constexpr ((TM & 8) != 0) s = 0;
+    const long long off = (long long)s * ROW_KB;
+    for (int mb = mb0; mb < mb0 + nmb; ++mb) {
+      a[mb][0] = *(const bf16x8*)(aptr[mb] + off);
+      a[mb][1] = *(const bf16x8*)(aptr[mb] + off + 64);
+    }
+  };
+
+  floatx4v acc[4][10];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 10; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[mb][nb][r] = 0.f;
+  const int brow = fr * 64 + 16 * (fq ^ swz(fr));
+  auto read_b = [&](const char* base, int nb, bf16x8 (&b)[3]) {
+    const char* br = base + brow + nb * 1024;
+    b[0] = *(const bf16x8*)(br);
+    b[1] = *(const bf16x8*)(br + X6P_B_PLANE);
+  };
+  auto pin = [&](int nv) {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if ((i % 6) == 0 && i < 6 * nv) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      if ((i & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+    }
+  };
+
+  // prologue: A and B of K blocks 0 .. NS-2
+  load_a(0, afr[0], 0, 4);
+  issue_b(0, 0, 0, 5);
+  load_a(min(1, nk - 1), afr[1], 0, 4);
+  issue_b(min(1, nk - 1), 1, 0, 5);
+  if constexpr (NS == 4) {
+    load_a(min(2, nk - 1), afr[2], 0, 4);
+    issue_b(min(2, nk - 1), 2, 0, 5);
+  }
+  __builtin_amdgcn_s_waitcnt(0);     // (prologue only) everything above landed
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  // one K block: compute on ring set I (block s); load A and B of block s+NS-1 into the A set and
+  // the B slot that block s-1 used
+  auto stage = [&](auto I, int s, int& slot) {
+    constexpr int cur = decltype(I)::value, nxt = (cur + NS - 1) % NS;
+    const int sa = (TM & 2) ? s : min(s + NS - 1, nk - 1);
+    const int sb = (TM & 2) ? s : min(s + NS - 1, nk - 1);
+    const int nslot = slot + 1 == NS ? 0 : slot + 1;
+    const int lslot = slot == 0 ? NS - 1 : slot - 1;
+    const char* base = smem + slot * FCH_BSTAGE;
+    bf16x8 b0[3], b1[3];
+    read_b(base, 0, b0);
+#pragma unroll
+    for (int nb = 0; nb < 10; ++nb) {
+      int nv = 0;
+      if (!(TM & 2)) {
+        if (nb < 4) {                      // A of block s+NS-1: 2 loads per unit
+          if (!(TM & 16)) load_a(sa, afr[nxt], nb, 1);
+          nv = 2;
+        } else if (nb < 9) {               // B of block s+NS-1: 1 piece per unit
+          if (!(TM & 32)) issue_b(sb, lslot, nb - 4, 1);
+          nv = 1;
+        }
+      }
+      if (nb + 1 < 10) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+        acc[mb][nb] = planes_mfma<2>(acc[mb][nb], afr[cur][mb], (nb & 1) ? b1 : b0);
+      pin(nv);
+    }
+    if constexpr (!(TM & 4)) {
+      // A and B of block s+1 landed in every wave (in flight: blocks s+2 .. s+NS-1, 13 loads
+      // each).  The builtin, not asm: the compiler's own wait insertion then knows what has
+      // landed (simm16 = vmcnt[3:0] | expcnt 7 << 4 | lgkmcnt 0 << 8 | vmcnt[5:4] << 14).
+      if constexpr (NS == 4)
+        __builtin_amdgcn_s_waitcnt(0x407A);      // vmcnt(26) lgkmcnt(0)
+      else
+        __builtin_amdgcn_s_waitcnt(0x007D);      // vmcnt(13) lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
+    }
+    asm volatile("" ::: "memory");
+    slot = nslot;
+  };
+  // unconditional NS-stage loop body (the compiler's own vmcnt tracking then sees every back
+  // edge with all loads issued after the set it waits for), tail after the loop
+  int slot = 0, s = 0;
+  for (; s + NS <= nk; s += NS) {
+    stage(std::integral_constant<int, 0>{}, s, slot);
+    stage(std::integral_constant<int, 1>{}, s + 1, slot);
+    stage(std::integral_constant<int, 2>{}, s + 2, slot);
+    if constexpr (NS == 4) stage(std::integral_constant<int, 3>{}, s + 3, slot);
+  }
+  if (s < nk) stage(std::integral_constant<int, 0>{}, s, slot);
+  if (s + 1 < nk) stage(std::integral_constant<int, 1>{}, s + 1, slot);
+  if constexpr (NS == 4)
+    if (s + 2 < nk) stage(std::integral_constant<int, 2>{}, s + 2, slot);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the ring's duplicate tail loads
+  gemm_epilogue16<EPI, 2>(p, acc, m0 + wave * 64, n0, ks, lane);
+}
+
+template <int LAYER, int EPI, int TM = 0, int NS = 3>
+__global__ __launch_bounds__(256, 1) void beluga_fc_h3(GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[NS * FCH_BSTAGE];
+  gemm_fc_h3_body<LAYER, EPI, TM, NS>(p, smem);
 }
 
 // ---- f16x3 conv GEMM with the Toeplitz A tile staged once per channel chunk -------------

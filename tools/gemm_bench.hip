@@ -82,10 +82,96 @@ static void fill(float* d, size_t n, float lo, float hi, unsigned seed) {
   CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
 }
 
+__global__ void hash_fill(float* d, long long n, float lo, float hi, unsigned seed) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  unsigned x = (unsigned)i * 2654435761u ^ seed * 40503u;
+  x ^= x >> 15; x *= 2246822519u; x ^= x >> 13; x *= 3266489917u; x ^= x >> 16;
+  d[i] = lo + (hi - lo) * (float)(x >> 8) * (1.0f / 16777216.0f);
+}
+
+// FC1 shape (M = windows, N = 2003 -> 2080, K = 67840, split-K slabs, partial epilogue):
+// the f16x3 planes GEMM and its timing probes (TM 2: no LDS-DMA in the loop).
+template <int TM>
+void fc1_launch(const GemmArgs& a, unsigned nblk) { beluga_gemm_h3q<7, EPI_PARTIAL, TM, 3><<<nblk, 256>>>(a); }
+template <int TM, int NS = 3>
+void fc1r_launch(const GemmArgs& a, unsigned nblk) { beluga_fc_h3<7, EPI_PARTIAL, TM, NS><<<nblk, 256>>>(a); }
+
+int fc1_bench(int nb, int rounds, int splits) {
+  const int K = 67840, npad = 2080, ldc = 2016;
+  float *X, *W, *C;
+  CK(hipMalloc(&X, (size_t)nb * K * 4));
+  CK(hipMalloc(&W, (size_t)npad * K * 4));
+  CK(hipMalloc(&C, (size_t)splits * nb * ldc * 4));
+  hash_fill<<<(unsigned)(((long long)nb * K + 255) / 256), 256>>>(X, (long long)nb * K, 0.f, 1.f, 1);
+  hash_fill<<<(unsigned)(((long long)npad * K + 255) / 256), 256>>>(W, (long long)npad * K, -0.05f, 0.05f, 2);
+  int* zs;
+  CK(hipMalloc(&zs, std::max(nb, npad) * 4));
+  CK(hipMemset(zs, 0, std::max(nb, npad) * 4));
+  _Float16 *Xh, *Bh;
+  CK(hipMalloc(&Xh, (size_t)nb * K * 4));
+  CK(hipMalloc(&Bh, (size_t)npad * K * 4));
+  split_planes_h2<<<(unsigned)(((long long)nb * K / 4 + 255) / 256), 256>>>(X, nb, K, zs, Xh);
+  split_planes_h2<<<(unsigned)(((long long)npad * K / 4 + 255) / 256), 256>>>(W, npad, K, zs, Bh);
+  CK(hipDeviceSynchronize());
+  GemmArgs a{};
+  a.A = (const float*)Xh; a.lda = K; a.M = nb; a.B = W; a.Bp = Bh; a.ldb = K; a.kper = K / splits; a.taps = 1;
+  a.n_tiles = npad / GBN; a.m_tiles = (nb + X6P_BM - 1) / X6P_BM; a.m_fastest = 1; a.linear_order = 1;
+  a.C = C; a.ldc = ldc; a.n_store = ldc; a.split_stride = (long long)nb * ldc;
+  const unsigned nblk = (unsigned)(a.m_tiles * a.n_tiles * splits);
+  struct V { const char* name; void (*f)(const GemmArgs&, unsigned); };
+  // block orders: m = M tiles fastest in dispatch order (the library's FC1 order), n = N tiles
+  // fastest in dispatch order, x = N tiles fastest per XCD (XCD-aware remap)
+  V vs[] = {{"h3q_m", fc1_launch<0>}, {"h3q_n", fc1_launch<0>}, {"h3q_x", fc1_launch<0>},
+            {"fcr_m", fc1r_launch<0>}, {"fcr_n", fc1r_launch<0>}, {"fcr_x", fc1r_launch<0>},
+            {"fcr_x_noload", fc1r_launch<2>}, {"fcr_x_hotAB", fc1r_launch<8>},
+            {"fc4_m", fc1r_launch<0, 4>}, {"fc4_x", fc1r_launch<0, 4>}};
+  constexpr int NV = sizeof(vs) / sizeof(vs[0]);
+  const size_t csz = (size_t)splits * nb * ldc;
+  std::vector<float> ref(csz), out(csz);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<std::vector<float>> t(NV);
+  for (int r = 0; r < rounds; ++r)
+    for (int v = 0; v < NV; ++v) {
+      CK(hipMemset(C, 0, csz * 4));
+      const char o = vs[v].name[3] == '_' ? vs[v].name[4] : vs[v].name[4] == '_' ? vs[v].name[5] : vs[v].name[4];
+      a.m_fastest = o == 'm';
+      a.linear_order = o != 'x';
+      vs[v].f(a, nblk);
+      if (r == 0 && strstr(vs[v].name, "no") == nullptr) {
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(v == 0 ? ref.data() : out.data(), C, csz * 4, hipMemcpyDeviceToHost));
+        if (v > 0) {
+          size_t bad = 0;
+          for (size_t i = 0; i < csz; ++i) bad += memcmp(&ref[i], &out[i], 4) != 0;
+          printf("variant %s vs h3q: %zu of %zu partials differ bitwise\n", vs[v].name, bad, csz);
+        }
+      }
+      CK(hipEventRecord(e0));
+      vs[v].f(a, nblk);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      t[v].push_back(ms);
+    }
+  const double flops = 2.0 * nb * 2003.0 * K;
+  printf("shape fc1 windows %d splits %d (M=%d K=%d N=2003)\n", nb, splits, nb, K);
+  for (int v = 0; v < NV; ++v) {
+    std::sort(t[v].begin(), t[v].end());
+    printf("  %-12s median %8.3f ms  %7.1f TFLOP/s fp32-equivalent\n", vs[v].name, t[v][t[v].size() / 2],
+           flops / (t[v][t[v].size() / 2] * 1e-3) / 1e12);
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const int nb = argc > 1 ? atoi(argv[1]) : 1000;
   const int rounds = argc > 2 ? atoi(argv[2]) : 5;
   const char* which = argc > 3 ? argv[3] : "conv2";
+  if (!strcmp(which, "fc1")) return fc1_bench(nb, rounds, argc > 4 ? atoi(argv[4]) : 20);
   struct Shape { const char* name; int cin, cout, s_in, t_valid, s_out, pool; double macs; };
   Shape shapes[] = {{"conv2", 320, 320, 2000, 496, 500, 1, 1986.0 * 320 * 2560},
                     {"conv3", 320, 480, 500, 489, 500, 0, 489.0 * 480 * 2560},
