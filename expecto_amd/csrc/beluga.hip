@@ -582,6 +582,7 @@ struct expecto_beluga {
   int precision = EXPECTO_PRECISION_BF16X6;
   int fc_splits = kFcSplitsDefault;   // FC1 split-K slabs: a divisor of 2120 K blocks, <= 32
   int conv_tile = 0;                  // f16x3 conv M tile: 0 = auto (conv_tile_rows), 256 or 384
+  int cus = 0;                        // compute units of the device (workgroups per round)
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, int>> pending;  // (layer, event index of start)
@@ -677,10 +678,21 @@ float exp2i(int e) { return std::ldexp(1.0f, e); }
 // equal to the 8-wave kernel; conv6 -3 %, its 113-row windows give a short grid), so auto takes
 // it for every launch of the pool layers (one kernel per layer, incl. the small alt-delta
 // launches) and leaves the ReLU layers on the 8-wave kernel.
-int conv_tile_rows(const expecto_beluga* h, bool pool) {
+// l: 0 = conv2 .. 4 = conv6.  384-row tiles run 2-5 % faster per row than 256-row tiles except
+// on conv6 (tools/gemm_bench), but one workgroup fills a CU, so a launch of few tiles (the
+// alt-delta runs of the pair path: 30-60 k rows) is priced by its rounds of 256 workgroups:
+// the tile with the fewer row-rounds wins there (e.g. conv3 alt: 297 x 384 = 2 rounds of 384
+// rows vs 447 x 256 = 2 rounds of 256 rows).  Every conv kernel gives the same bits.
+int conv_tile_rows(const expecto_beluga* h, int l, bool pool, long long M, int n_tiles) {
   if (g_precision != EXPECTO_PRECISION_F16X3) return (int)gemm_bm();
   if (h->conv_tile) return h->conv_tile;
-  return pool ? 384 : 256;
+  if (!pool && l == 4) return 256;
+  const int cus = h->cus > 0 ? h->cus : 256;
+  auto cost = [&](int bm, double per_row) {
+    const long long blocks = (M + bm - 1) / bm * n_tiles;
+    return (double)((blocks + cus - 1) / cus) * bm * per_row;
+  };
+  return cost(384, 1.0) <= cost(256, 1.04) ? 384 : 256;
 }
 
 template <int LAYER, int EPI>
@@ -703,12 +715,18 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
     if (a.taps == 8) {   // conv: chunk-slab kernel (one Toeplitz A slab per 32-channel chunk)
       EXPECTO_REQUIRE(splits == 1 && a.kper == a.ldb && a.ldb == 8 * a.lda && !a.m_fastest && !a.a_rows,
                       "f16x3 conv GEMM: full K, no split, no row gather");
-      if (bm == 384)
+      // all bitwise equal (same products and k order per output); per-layer choice from
+      // tools/gemm_bench: pool layers 4 waves x 96 rows, ReLU layers 8 waves (two per SIMD)
+      if constexpr (EPI == EPI_RELU) {
+        if (bm == 384)
+          beluga_conv_h3s<LAYER, EPI, 0, 6><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
+        else
+          beluga_conv_h3s<LAYER, EPI, 0, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
+      } else if (bm == 384) {
         beluga_conv_h3r<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
-      else if constexpr (EPI == EPI_RELU)   // 8-wave variant: +2-5 % on conv3/5/6 (tools/gemm_bench), same bits
-        beluga_conv_h3w<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
-      else
+      } else {
         beluga_conv_h3q<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
+      }
     } else {   // FC layers: A fragments straight into registers, B through LDS (same bits)
       beluga_fc_h3<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
     }
@@ -744,7 +762,7 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
   a.kper = 8 * g.cin;
   a.taps = 8;
   a.n_tiles = npad_of(g.cout) / GBN;
-  const int bm = conv_tile_rows(h, pool);
+  const int bm = conv_tile_rows(h, l, pool, a.M, (int)a.n_tiles);
   a.m_tiles = (a.M + bm - 1) / bm;
   a.m_fastest = 0;
   a.bias = h->bt[l];
@@ -1294,6 +1312,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   auto* h = new expecto_beluga();
   h->device = device;
   h->max_batch = max_batch;
+  if (hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) h->cus = 0;
   int rc = 0;
   auto fail = [&](int code) {
     expecto_beluga_destroy(h);

@@ -816,10 +816,21 @@ __device__ __forceinline__ void gemm_planes_body(const GemmArgs& p, char* smem) 
 // ahead into a 3-deep register ring; only B (shared by the 4 waves) goes through an LDS ring.
 // Same operands, products and k order per output as gemm_planes_body<PL=2>: bitwise equal.
 constexpr int FCH_BSTAGE = 2 * X6P_B_PLANE;           // one B stage: 160 cols x 32 k x 2 planes
+// NB: 16-column blocks per tile (10: 160-column tiles; 21: 336-column tiles, 6 of which cover
+// FC1's 2016 padded outputs with 0.6 % padding instead of 13 x 160 = 2080's 3.8 %, and each A
+// fragment feeds 2.1x the MFMAs: half the A traffic from L2 / Infinity Cache per MFMA).
+template <int NB>
+struct FcGeo {
+  static constexpr int BN = 16 * NB;
+  static constexpr int PLANE = NB * 1024;              // one plane of a B stage
+  static constexpr int STAGE = 2 * PLANE;
+  static constexpr int PIECES = 2 * NB;                // 1 KiB LDS-DMA pieces per stage
+  static constexpr int NBP = (PIECES + 3) / 4;         // pieces per wave (the last repeated)
+};
 
 // NS: ring depth of both operands (A register sets and B LDS slots): K block s+NS-1 is loaded
 // while block s computes.
-template <int LAYER, int EPI, int TM, int NS>
+template <int LAYER, int EPI, int TM, int NS, int NB = 10>
 __device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
   static_assert(NS == 3 || NS == 4, "ring depth");
   constexpr int ROW_KB = 128;                          // bytes per row and 32-deep K block (2 planes)
@@ -844,7 +855,8 @@ __device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const long long m0 = mt * X6P_BM;
-  const int n0 = nt * GBN;
+  using F = FcGeo<NB>;
+  const int n0 = nt * F::BN;
   const int kb_total = (int)(p.ldb / GBK);
   const int gs0 = ks * (p.kper / GBK);
   const long long lda_kb = p.lda / GBK;
@@ -861,20 +873,20 @@ __device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
     aptr[mb] = (const char*)p.A + kb0 * ROW_KB + 16 * fq;
   }
   const char* Bb = (const char*)p.Bp + ((long long)n0 * kb_total + gs0) * ROW_KB;
-  unsigned boff[5];
+  unsigned boff[F::NBP];
 #pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    const int g = wave + 4 * j;                        // 20 pieces: plane g / 10, cols 16*(g % 10)
-    const int pl = g / 10, r = 16 * (g % 10) + (lane >> 2);
+  for (int j = 0; j < F::NBP; ++j) {
+    const int g = min(wave + 4 * j, F::PIECES - 1);    // piece g: plane g / NB, cols 16*(g % NB)
+    const int pl = g / NB, r = 16 * (g % NB) + (lane >> 2);
     const int c = (lane & 3) ^ swz(r);
     boff[j] = (unsigned)((long long)r * kb_total * ROW_KB + pl * 64 + 16 * c);
   }
   const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, 0x7fffffff, 0x00020000);
   auto issue_b = [&](int s, int slot, int j0, int nj) {
     if constexpr ((TM & 8) != 0) s = 0;
-    char* base = smem + slot * FCH_BSTAGE;
+    char* base = smem + slot * F::STAGE;
     for (int j = j0; j < j0 + nj; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + (wave + 4 * j) * 1024), 16, boff[j],
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + min(wave + 4 * j, F::PIECES - 1) * 1024), 16, boff[j],
                                                (unsigned)(s * ROW_KB), 0, 0);
   };
   // A fragments of K block s into ring set `set` (two loads per row block: hi, lo plane)
@@ -888,18 +900,18 @@ __device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
     }
   };
 
-  floatx4v acc[4][10];
+  floatx4v acc[4][NB];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-    for (int nb = 0; nb < 10; ++nb)
+    for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[mb][nb][r] = 0.f;
   const int brow = fr * 64 + 16 * (fq ^ swz(fr));
   auto read_b = [&](const char* base, int nb, bf16x8 (&b)[3]) {
     const char* br = base + brow + nb * 1024;
     b[0] = *(const bf16x8*)(br);
-    b[1] = *(const bf16x8*)(br + X6P_B_PLANE);
+    b[1] = *(const bf16x8*)(br + F::PLANE);
   };
   auto pin = [&](int nv) {
 #pragma unroll
@@ -913,12 +925,12 @@ __device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
 
   // prologue: A and B of K blocks 0 .. NS-2
   load_a(0, afr[0], 0, 4);
-  issue_b(0, 0, 0, 5);
+  issue_b(0, 0, 0, F::NBP);
   load_a(min(1, nk - 1), afr[1], 0, 4);
-  issue_b(min(1, nk - 1), 1, 0, 5);
+  issue_b(min(1, nk - 1), 1, 0, F::NBP);
   if constexpr (NS == 4) {
     load_a(min(2, nk - 1), afr[2], 0, 4);
-    issue_b(min(2, nk - 1), 2, 0, 5);
+    issue_b(min(2, nk - 1), 2, 0, F::NBP);
   }
   __builtin_amdgcn_s_waitcnt(0);     // (prologue only) everything above landed
   __builtin_amdgcn_s_barrier();
@@ -932,22 +944,22 @@ __device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
     const int sb = (TM & 2) ? s : min(s + NS - 1, nk - 1);
     const int nslot = slot + 1 == NS ? 0 : slot + 1;
     const int lslot = slot == 0 ? NS - 1 : slot - 1;
-    const char* base = smem + slot * FCH_BSTAGE;
+    const char* base = smem + slot * F::STAGE;
     bf16x8 b0[3], b1[3];
     read_b(base, 0, b0);
 #pragma unroll
-    for (int nb = 0; nb < 10; ++nb) {
+    for (int nb = 0; nb < NB; ++nb) {
       int nv = 0;
       if (!(TM & 2)) {
         if (nb < 4) {                      // A of block s+NS-1: 2 loads per unit
           if (!(TM & 16)) load_a(sa, afr[nxt], nb, 1);
           nv = 2;
-        } else if (nb < 9) {               // B of block s+NS-1: 1 piece per unit
+        } else if (nb < 4 + F::NBP) {      // B of block s+NS-1: 1 piece per unit
           if (!(TM & 32)) issue_b(sb, lslot, nb - 4, 1);
           nv = 1;
         }
       }
-      if (nb + 1 < 10) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
+      if (nb + 1 < NB) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb)
         acc[mb][nb] = planes_mfma<2>(acc[mb][nb], afr[cur][mb], (nb & 1) ? b1 : b0);
@@ -957,10 +969,9 @@ __device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
       // A and B of block s+1 landed in every wave (in flight: blocks s+2 .. s+NS-1, 13 loads
       // each).  The builtin, not asm: the compiler's own wait insertion then knows what has
       // landed (simm16 = vmcnt[3:0] | expcnt 7 << 4 | lgkmcnt 0 << 8 | vmcnt[5:4] << 14).
-      if constexpr (NS == 4)
-        __builtin_amdgcn_s_waitcnt(0x407A);      // vmcnt(26) lgkmcnt(0)
-      else
-        __builtin_amdgcn_s_waitcnt(0x007D);      // vmcnt(13) lgkmcnt(0)
+      constexpr int VM = (NS - 2) * (8 + F::NBP);   // loads of blocks s+2 .. s+NS-1 stay in flight
+      static_assert(VM < 64, "vmcnt field");
+      __builtin_amdgcn_s_waitcnt((VM & 15) | (7 << 4) | ((VM >> 4) << 14));   // vmcnt(VM) lgkmcnt(0)
       __builtin_amdgcn_s_barrier();
     }
     asm volatile("" ::: "memory");
@@ -980,13 +991,13 @@ __device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
   if constexpr (NS == 4)
     if (s + 2 < nk) stage(std::integral_constant<int, 2>{}, s + 2, slot);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the ring's duplicate tail loads
-  gemm_epilogue16<EPI, 2>(p, acc, m0 + wave * 64, n0, ks, lane);
+  gemm_epilogue16<EPI, 2, NB>(p, acc, m0 + wave * 64, n0, ks, lane);
 }
 
-template <int LAYER, int EPI, int TM = 0, int NS = 3>
+template <int LAYER, int EPI, int TM = 0, int NS = 3, int NB = 10>
 __global__ __launch_bounds__(256, 1) void beluga_fc_h3(GemmArgs p) {
-  __shared__ __attribute__((aligned(1024))) char smem[NS * FCH_BSTAGE];
-  gemm_fc_h3_body<LAYER, EPI, TM, NS>(p, smem);
+  __shared__ __attribute__((aligned(1024))) char smem[NS * FcGeo<NB>::STAGE];
+  gemm_fc_h3_body<LAYER, EPI, TM, NS, NB>(p, smem);
 }
 
 // ---- f16x3 conv GEMM with the Toeplitz A tile staged once per channel chunk -------------
@@ -1255,45 +1266,55 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
 }
 
 // ---- f16x3 conv GEMM, 8 waves (two per SIMD) ---------------------------------------------
-// gemm_conv_h3_body with the 256 x 160 tile split over 8 waves of 64 rows x 80 columns
-// (wave w: rows 64*(w & 3), columns 80*(w >> 2); 4 x 5 accumulator blocks = 80 AGPRs), so the
-// two waves of a SIMD cover each other's barrier waits, LDS-DMA issue and LDS reads (with one
-// wave per SIMD the MFMA pipe idles through them: conv2 MFMA busy 63 %, waves parked 16 %).
-// Same slab / ring staging (A slab pieces: 5 or 4 per wave per chunk, B: 3 or 2 per wave per
-// stage), same products and k order per output: bitwise equal to gemm_conv_h3_body.
-template <int EPI>
-__device__ __forceinline__ void epilogue_relu_h2_lds8(const GemmArgs& p, const floatx4v (&acc)[4][5], long long m0,
-                                                      int wm, int wn, int n0, int lane, int tid, char* lds) {
+// gemm_conv_h3_body's tile split over 8 waves of 16*MB rows x 80 columns (tile 64*MB x 160:
+// MB 4 = 256 rows, MB 6 = 384 rows with the 400-row slab of SlabGeo<6>; wave w: rows
+// 16*MB*(w & 3), columns 80*(w >> 2); MB x 5 accumulator blocks), so the two waves of a SIMD
+// cover each other's barrier waits, LDS-DMA issue and LDS reads (with one wave per SIMD the
+// MFMA pipe idles through them).  Same slab / ring staging (A slab pieces P = wave + 8*i, B
+// pieces wave + 8*j of 20).  tools/gemm_bench, 2000 windows, fp32-equivalent TF/s: conv3 465
+// (4-wave 256-row h3q 456) -> 487 at MB 6, conv5 466 -> 489 at MB 6, conv6 484 at MB 4 (468 at
+// MB 6); the pool layers stay on the 4-wave 384-row beluga_conv_h3r (conv4 517 vs 507).
+// STG 1 (measured slower, 3-8 %: kept as a probe) staggers the two waves of a SIMD (w and w+4) by half a K stage
+// (MI355X_MICROARCH.md "Two waves per SIMD" item 9): waves 4-7 run units 3,4 of stage s-1
+// (their B fragments read into registers before that stage's barrier, since the slot is
+// refilled right after it) and units 0-2 of stage s between barriers s-1 and s, so the
+// partners' LDS-read bursts and MFMA runs interleave instead of colliding.  Load issue per
+// barrier interval, LDS ring and slab schedule are the same for both halves.  Same products
+// and k order per output as every other f16x3 conv kernel: bitwise equal.
+template <int MB>
+__device__ __forceinline__ void epilogue_relu_h2_lds8m(const GemmArgs& p, const floatx4v (&acc)[MB][5], long long m0,
+                                                       int wm, int wn, int n0, int lane, int tid, char* lds) {
+  constexpr int WR = 16 * MB;                          // rows per wave
   const int fr = lane & 15, fq = lane >> 4;
   const long long ldb = p.ldc >> 5;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
-    if ((wm >> 1) == pass) {            // this pass stages rows 128*pass .. +127 (waves wm = 2*pass, 2*pass+1)
+    if ((wm >> 1) == pass) {            // this pass stages rows 2*WR*pass .. +2*WR-1 (waves wm = 2*pass, 2*pass+1)
 #pragma unroll
       for (int nb = 0; nb < 5; ++nb) {
         const int c = wn * 80 + nb * 16 + fr, n = n0 + c;
         const float bn = n < p.n_store ? p.bias[n] : 0.f;
         const float cs = n < p.n_store ? p.col_scale[n] : 0.f;
 #pragma unroll
-        for (int mb = 0; mb < 4; ++mb)
+        for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const float x = fmaxf(acc[mb][nb][j] * cs + bn, 0.f) * p.out_scale;
             if (!(fabsf(x) < 65504.f)) *p.ovf = 1;
             _Float16 hi, lo;
             split_h2(x, hi, lo);
-            char* d = lds + ((wm & 1) * 64 + mb * 16 + 4 * fq + j) * H3E_ROW + (c >> 5) * 128 + (c & 31) * 2;
+            char* d = lds + ((wm & 1) * WR + mb * 16 + 4 * fq + j) * H3E_ROW + (c >> 5) * 128 + (c & 31) * 2;
             *(_Float16*)d = hi;
             *(_Float16*)(d + 64) = lo;
           }
       }
     }
     __syncthreads();
-    // 128 rows x 40 chunks of 16 B = 5120 chunks over 512 threads
+    // 2*WR rows x 40 chunks of 16 B over 512 threads
 #pragma unroll 2
-    for (int i = 0; i < 10; ++i) {
+    for (int i = 0; i < (2 * WR * 40) / 512; ++i) {
       const int k = i * 512 + tid, row = k / 40, ch = k - row * 40;
-      const long long m = m0 + pass * 128 + row;
+      const long long m = m0 + pass * 2 * WR + row;
       if (m < p.M) {
         const long long w = m / p.s_in;
         const int tpos = (int)(m - w * p.s_in);
@@ -1307,10 +1328,13 @@ __device__ __forceinline__ void epilogue_relu_h2_lds8(const GemmArgs& p, const f
   }
 }
 
-template <int LAYER, int EPI, int TM>
-__device__ __forceinline__ void gemm_conv_h3w_body(const GemmArgs& p, char* smem) {
+template <int LAYER, int EPI, int TM, int MB, int STG>
+__device__ __forceinline__ void gemm_conv_h3s_body(const GemmArgs& p, char* smem) {
+  using G = SlabGeo<MB>;
   constexpr int ROW_KB = 128;
   constexpr int NSB = 3;
+  constexpr int NA8 = (G::PIECES + 7) / 8;            // slab pieces per wave and chunk (max)
+  static_assert(NA8 <= 7, "slab pieces must be issued by tap 6");
   const unsigned nblk = gridDim.x, bid = blockIdx.x;
   const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
   const unsigned lin = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
@@ -1319,7 +1343,7 @@ __device__ __forceinline__ void gemm_conv_h3w_body(const GemmArgs& p, char* smem
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave & 3, wn = wave >> 2;
-  const long long m0 = mt * X6P_BM;
+  const long long m0 = mt * G::BM;
   const int n0 = nt * GBN;
   const int kb_total = (int)(p.ldb / GBK);
   const long long lda_kb = p.lda / GBK;
@@ -1328,11 +1352,11 @@ __device__ __forceinline__ void gemm_conv_h3w_body(const GemmArgs& p, char* smem
   auto swz = [](int r) { return (-(r >> 2)) & 3; };
   const char* Ab = (const char*)p.A + m0 * lda_kb * ROW_KB;
   const long long last_row = p.M - 1 + 7;
-  const int na = wave < 4 ? 5 : 4;               // A slab pieces P = wave + 8*i < 36
-  unsigned aoff[5];
+  const int na = (G::PIECES - wave + 7) / 8;          // A slab pieces P = wave + 8*i < PIECES
+  unsigned aoff[NA8];
 #pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    const int P = min(wave + 8 * i, 35), g = P >> 1, pl = P & 1;
+  for (int i = 0; i < NA8; ++i) {
+    const int P = min(wave + 8 * i, G::PIECES - 1), g = P >> 1, pl = P & 1;
     const int r = 16 * g + (lane >> 2);
     const long long m = min(m0 + r, last_row);
     const int c = (lane & 3) ^ swz(r);
@@ -1351,11 +1375,11 @@ __device__ __forceinline__ void gemm_conv_h3w_body(const GemmArgs& p, char* smem
   const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, 0x7fffffff, 0x00020000);
   char* const aslab = smem;
-  char* const bring = smem + 2 * H3C_ASLAB;
+  char* const bring = smem + 2 * G::ASLAB;
   auto issue_a = [&](int chunk, int i) {
     if (i >= na) return;
     const int P = wave + 8 * i;
-    char* dst = aslab + (chunk & 1) * H3C_ASLAB + (P & 1) * H3C_APLANE + (P >> 1) * 1024;
+    char* dst = aslab + (chunk & 1) * G::ASLAB + (P & 1) * G::APLANE + (P >> 1) * 1024;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (lds_void*)dst, 16, aoff[i], (unsigned)(chunk * ROW_KB), 0, 0);
   };
   auto issue_b = [&](int s, int slot) {
@@ -1367,23 +1391,36 @@ __device__ __forceinline__ void gemm_conv_h3w_body(const GemmArgs& p, char* smem
         __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + (wave + 8 * j) * 1024), 16, boff[j],
                                                  (unsigned)(s * ROW_KB), 0, 0);
   };
+  // slab c+1 pieces issued at tap t (unit 0): pieces 0,1 at tap 0, piece t+1 at taps 1..NA8-2
+  auto issue_a_tap = [&](int c, int t) -> int {
+    if (t == 0) {
+      issue_a(c + 1, 0);
+      issue_a(c + 1, 1);
+      return 2;
+    }
+    if (t <= NA8 - 2) {
+      issue_a(c + 1, t + 1);
+      return 1;
+    }
+    return 0;
+  };
 
-  floatx4v acc[4][5];
+  floatx4v acc[MB][5];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
+  for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
     for (int nb = 0; nb < 5; ++nb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[mb][nb][r] = 0.f;
   const int fr = lane & 15, fq = lane >> 4;
   const int brow = (wn * 5) * 1024 + fr * 64 + 16 * (fq ^ swz(fr));
-  auto read_a = [&](const char* slab, int t, bf16x8 (&a)[4][3]) {
+  auto read_a = [&](const char* slab, int t, bf16x8 (&a)[MB][3]) {
     const int rr2 = fr + t;
-    const int off = (wm * 64 + rr2) * 64 + 16 * (fq ^ swz(rr2));
+    const int off = (wm * 16 * MB + rr2) * 64 + 16 * (fq ^ swz(rr2));
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) {
+    for (int mb = 0; mb < MB; ++mb) {
       a[mb][0] = *(const bf16x8*)(slab + off + mb * 1024);
-      a[mb][1] = *(const bf16x8*)(slab + off + mb * 1024 + H3C_APLANE);
+      a[mb][1] = *(const bf16x8*)(slab + off + mb * 1024 + G::APLANE);
     }
   };
   auto read_b = [&](const char* base, int nb, bf16x8 (&b)[3]) {
@@ -1391,21 +1428,32 @@ __device__ __forceinline__ void gemm_conv_h3w_body(const GemmArgs& p, char* smem
     b[0] = *(const bf16x8*)(br);
     b[1] = *(const bf16x8*)(br + X6P_B_PLANE);
   };
-  auto unit = [&](const bf16x8 (&a)[4][3], int nb, const bf16x8 (&b)[3]) {
+  auto unit = [&](const bf16x8 (&a)[MB][3], int nb, const bf16x8 (&b)[3]) {
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) acc[mb][nb] = planes_mfma<2>(acc[mb][nb], a[mb], b);
+    for (int mb = 0; mb < MB; ++mb) acc[mb][nb] = planes_mfma<2>(acc[mb][nb], a[mb], b);
   };
-  auto pin = [&](int nv) {
+  // nv VMEM issues and nd ds_reads spread over this unit's 3*MB MFMAs
+  auto pin = [&](int nv, int nd) {
 #pragma unroll
-    for (int i = 0; i < 12; ++i) {
+    for (int i = 0; i < 3 * MB; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       if ((i % 4) == 0 && i < 4 * nv) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      if ((i & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      if ((i & 1) == 0 && (i >> 1) < nd) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
     }
   };
+  auto stage_wait = [&]() {
+    if constexpr (!(TM & 4)) {
+      if (wave < 4)
+        asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    asm volatile("" ::: "memory");
+  };
 
-  for (int i = 0; i < 5; ++i) issue_a(0, i);
+  for (int i = 0; i < NA8; ++i) issue_a(0, i);
   issue_b(0, 0);
   issue_b(min(1, nk - 1), 1);
   if (wave < 4)
@@ -1414,66 +1462,113 @@ __device__ __forceinline__ void gemm_conv_h3w_body(const GemmArgs& p, char* smem
     asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  bf16x8 as[4][3];
+  bf16x8 as[MB][3];
   read_a(aslab, 0, as);
   int slot = 0;
-  for (int c = 0; c < nchunk; ++c) {
-    const char* slab = aslab + (c & 1) * H3C_ASLAB;
-    const bool more_a = (c + 1 < nchunk) && !(TM & 2);
-    for (int t = 0; t < 8; ++t) {
-      const int s = c * 8 + t;
-      const int nslot = slot + 1 == NSB ? 0 : slot + 1;
-      const int lslot = slot == 0 ? NSB - 1 : slot - 1;
-      const char* base = bring + slot * H3C_BSTAGE;
-      bf16x8 b0[3], b1[3];
-      read_b(base, 0, b0);
+  if (!STG || wn == 0) {
+    for (int c = 0; c < nchunk; ++c) {
+      const char* slab = aslab + (c & 1) * G::ASLAB;
+      const bool more_a = (c + 1 < nchunk) && !(TM & 2);
+      for (int t = 0; t < 8; ++t) {
+        const int s = c * 8 + t;
+        const int nslot = slot + 1 == NSB ? 0 : slot + 1;
+        const int lslot = slot == 0 ? NSB - 1 : slot - 1;
+        const char* base = bring + slot * H3C_BSTAGE;
+        bf16x8 b0[3], b1[3];
+        read_b(base, 0, b0);
 #pragma unroll
-      for (int nb = 0; nb < 5; ++nb) {
-        int nv = 0;
-        if (nb == 0 && more_a && t < 4) {     // slab c+1: pieces 0,1 at tap 0, 2..4 at taps 1..3
-          if (t == 0) {
-            issue_a(c + 1, 0);
-            issue_a(c + 1, 1);
-            nv = 2;
-          } else {
-            issue_a(c + 1, t + 1);
-            nv = 1;
+        for (int nb = 0; nb < 5; ++nb) {
+          int nv = 0;
+          if (nb == 0 && more_a) nv = issue_a_tap(c, t);
+          if (nb == 1 && !(TM & 2)) {
+            issue_b(min(s + 2, nk - 1), lslot);
+            nv = 3;
           }
+          if (nb + 1 < 5) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
+          unit(as, nb, (nb & 1) ? b1 : b0);
+          pin(nv, 2 * MB);
         }
-        if (nb == 1 && !(TM & 2)) {
-          issue_b(min(s + 2, nk - 1), lslot);
-          nv = 3;
-        }
-        if (nb + 1 < 5) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
-        unit(as, nb, (nb & 1) ? b1 : b0);
-        pin(nv);
+        if (t < 7) read_a(slab, t + 1, as);
+        stage_wait();
+        slot = nslot;
       }
-      if (t < 7) read_a(slab, t + 1, as);
-      if constexpr (!(TM & 4)) {
-        if (wave < 4)
-          asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-      }
-      asm volatile("" ::: "memory");
-      slot = nslot;
+      if (c + 1 < nchunk) read_a(aslab + ((c + 1) & 1) * G::ASLAB, 0, as);
     }
-    if (c + 1 < nchunk) read_a(aslab + ((c + 1) & 1) * H3C_ASLAB, 0, as);
+  } else {
+    // staggered half: interval s = units 3,4 of stage s-1 (A in `as`, B in bs3/bs4), then A of
+    // stage s and its units 0-2; B of units 3,4 read before barrier s
+    bf16x8 bs3[3], bs4[3];
+    for (int c = 0; c < nchunk; ++c) {
+      const char* slab = aslab + (c & 1) * G::ASLAB;
+      const bool more_a = (c + 1 < nchunk) && !(TM & 2);
+      for (int t = 0; t < 8; ++t) {
+        const int s = c * 8 + t;
+        const int nslot = slot + 1 == NSB ? 0 : slot + 1;
+        const int lslot = slot == 0 ? NSB - 1 : slot - 1;
+        const char* base = bring + slot * H3C_BSTAGE;
+        bf16x8 b0[3], b1[3];
+        if (s > 0) {
+          // units 3,4 of stage s-1 row block by row block; each block's A registers are
+          // refilled with stage s's fragments as soon as its 6 MFMAs have issued
+          const int nv = more_a ? issue_a_tap(c, t) : 0;
+          const int rr2 = fr + t;
+          const int off = (wm * 16 * MB + rr2) * 64 + 16 * (fq ^ swz(rr2));
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb) {
+            acc[mb][3] = planes_mfma<2>(acc[mb][3], as[mb], bs3);
+            acc[mb][4] = planes_mfma<2>(acc[mb][4], as[mb], bs4);
+            as[mb][0] = *(const bf16x8*)(slab + off + mb * 1024);
+            as[mb][1] = *(const bf16x8*)(slab + off + mb * 1024 + G::APLANE);
+          }
+          read_b(base, 0, b0);
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb) {
+            if (mb < nv) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        } else {
+          if (more_a) issue_a_tap(c, t);
+          read_b(base, 0, b0);
+        }
+#pragma unroll
+        for (int nb = 0; nb < 3; ++nb) {
+          int nv = 0;
+          if (nb == 0 && !(TM & 2)) {
+            issue_b(min(s + 2, nk - 1), lslot);
+            nv = 3;
+          }
+          if (nb == 0) read_b(base, 1, b1);
+          if (nb == 1) read_b(base, 2, b0);
+          if (nb == 2) {
+            read_b(base, 3, bs3);
+            read_b(base, 4, bs4);
+          }
+          unit(as, nb, (nb & 1) ? b1 : b0);
+          pin(nv, nb == 2 ? 4 : 2);
+        }
+        stage_wait();
+        slot = nslot;
+      }
+    }
+    unit(as, 3, bs3);
+    unit(as, 4, bs4);
   }
   if constexpr (EPI == EPI_RELU) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    epilogue_relu_h2_lds8<EPI>(p, acc, m0, wm, wn, n0, lane, tid, smem);
+    epilogue_relu_h2_lds8m<MB>(p, acc, m0, wm, wn, n0, lane, tid, smem);
   } else {
-    gemm_epilogue16<EPI, 2, 5>(p, acc, m0 + wm * 64, n0 + wn * 80, 0, lane);
+    gemm_epilogue16<EPI, 2, 5, MB>(p, acc, m0 + wm * 16 * MB, n0 + wn * 80, 0, lane);
   }
 }
 
-template <int LAYER, int EPI, int TM = 0>
-__global__ __launch_bounds__(512, 1) void beluga_conv_h3w(GemmArgs p) {
-  __shared__ __attribute__((aligned(1024))) char smem[h3c_lds<3>()];
-  gemm_conv_h3w_body<LAYER, EPI, TM>(p, smem);
+// MB 4 / 6 row blocks per wave, STG 0 / 1 (see gemm_conv_h3s_body)
+template <int LAYER, int EPI, int TM = 0, int MB = 6, int STG = 0>
+__global__ __launch_bounds__(512, 1) void beluga_conv_h3s(GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[h3c_lds_mb<3, MB>()];
+  gemm_conv_h3s_body<LAYER, EPI, TM, MB, STG>(p, smem);
 }
 
 // ---- the library's split-operand GEMMs (both on 16x16x32 MFMAs, LDS-DMA staged) ---------

@@ -62,9 +62,9 @@ Variant mkr3(const char* name) {
   return {name, 384, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3r<L, EPI, TM><<<nblk, 256>>>(a); }};
 }
 
-template <int L, int EPI, int TM = 0>
-Variant mkw3(const char* name) {
-  return {name, X6P_BM, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3w<L, EPI, TM><<<nblk, 512>>>(a); }};
+template <int L, int EPI, int MB, int STG, int TM = 0>
+Variant mks3(const char* name) {
+  return {name, 64 * MB, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3s<L, EPI, TM, MB, STG><<<nblk, 512>>>(a); }};
 }
 
 template <int L, int EPI, int WM, int MINB, int BK, int PIPE = 0>
@@ -94,8 +94,8 @@ __global__ void hash_fill(float* d, long long n, float lo, float hi, unsigned se
 // the f16x3 planes GEMM and its timing probes (TM 2: no LDS-DMA in the loop).
 template <int TM>
 void fc1_launch(const GemmArgs& a, unsigned nblk) { beluga_gemm_h3q<7, EPI_PARTIAL, TM, 3><<<nblk, 256>>>(a); }
-template <int TM, int NS = 3>
-void fc1r_launch(const GemmArgs& a, unsigned nblk) { beluga_fc_h3<7, EPI_PARTIAL, TM, NS><<<nblk, 256>>>(a); }
+template <int TM, int NS = 3, int NB = 10>
+void fc1r_launch(const GemmArgs& a, unsigned nblk) { beluga_fc_h3<7, EPI_PARTIAL, TM, NS, NB><<<nblk, 256>>>(a); }
 
 int fc1_bench(int nb, int rounds, int splits) {
   const int K = 67840, npad = 2080, ldc = 2016;
@@ -118,14 +118,16 @@ int fc1_bench(int nb, int rounds, int splits) {
   a.A = (const float*)Xh; a.lda = K; a.M = nb; a.B = W; a.Bp = Bh; a.ldb = K; a.kper = K / splits; a.taps = 1;
   a.n_tiles = npad / GBN; a.m_tiles = (nb + X6P_BM - 1) / X6P_BM; a.m_fastest = 1; a.linear_order = 1;
   a.C = C; a.ldc = ldc; a.n_store = ldc; a.split_stride = (long long)nb * ldc;
-  const unsigned nblk = (unsigned)(a.m_tiles * a.n_tiles * splits);
-  struct V { const char* name; void (*f)(const GemmArgs&, unsigned); };
+  struct V { const char* name; void (*f)(const GemmArgs&, unsigned); int nb = 10; };
   // block orders: m = M tiles fastest in dispatch order (the library's FC1 order), n = N tiles
   // fastest in dispatch order, x = N tiles fastest per XCD (XCD-aware remap)
   V vs[] = {{"h3q_m", fc1_launch<0>}, {"h3q_n", fc1_launch<0>}, {"h3q_x", fc1_launch<0>},
             {"fcr_m", fc1r_launch<0>}, {"fcr_n", fc1r_launch<0>}, {"fcr_x", fc1r_launch<0>},
             {"fcr_x_noload", fc1r_launch<2>}, {"fcr_x_hotAB", fc1r_launch<8>},
-            {"fc4_m", fc1r_launch<0, 4>}, {"fc4_x", fc1r_launch<0, 4>}};
+            {"fc4_m", fc1r_launch<0, 4>}, {"fc4_x", fc1r_launch<0, 4>},
+            {"fcw_m", fc1r_launch<0, 3, 16>, 16}, {"fcw_n", fc1r_launch<0, 3, 16>, 16},
+            {"fcw_x", fc1r_launch<0, 3, 16>, 16}, {"fcw_x_noload", fc1r_launch<2, 3, 16>, 16},
+            {"fcw_x_hotAB", fc1r_launch<8, 3, 16>, 16}};
   constexpr int NV = sizeof(vs) / sizeof(vs[0]);
   const size_t csz = (size_t)splits * nb * ldc;
   std::vector<float> ref(csz), out(csz);
@@ -139,6 +141,8 @@ int fc1_bench(int nb, int rounds, int splits) {
       const char o = vs[v].name[3] == '_' ? vs[v].name[4] : vs[v].name[4] == '_' ? vs[v].name[5] : vs[v].name[4];
       a.m_fastest = o == 'm';
       a.linear_order = o != 'x';
+      a.n_tiles = (2016 + 16 * vs[v].nb - 1) / (16 * vs[v].nb);
+      const unsigned nblk = (unsigned)(a.m_tiles * a.n_tiles * splits);
       vs[v].f(a, nblk);
       if (r == 0 && strstr(vs[v].name, "no") == nullptr) {
         CK(hipDeviceSynchronize());
@@ -227,8 +231,11 @@ int main(int argc, char** argv) {
     vs.push_back(mk6<2, EPI_RELU_POOL4, 4, 1>("x6_wm4_b1"));
     vs.push_back(mk6q<2, EPI_RELU_POOL4>("x6q"));
     vs.push_back(mkc3<2, EPI_RELU_POOL4>("h3c"));
-    vs.push_back(mkw3<2, EPI_RELU_POOL4>("h3w"));
     vs.push_back(mkr3<2, EPI_RELU_POOL4>("h3r"));
+    vs.push_back(mks3<2, EPI_RELU_POOL4, 4, 0>("h3s4"));
+    vs.push_back(mks3<2, EPI_RELU_POOL4, 4, 1>("h3s4_stg"));
+    vs.push_back(mks3<2, EPI_RELU_POOL4, 6, 0>("h3s6"));
+    vs.push_back(mks3<2, EPI_RELU_POOL4, 6, 1>("h3s6_stg"));
     vs.push_back(mkr3<2, EPI_RELU_POOL4, 2>("h3r_noglds"));
     vs.push_back(mkr3<2, EPI_RELU_POOL4, 4>("h3r_nobar"));
     vs.push_back(mkr3<2, EPI_RELU_POOL4, 6>("h3r_noglds_nobar"));
@@ -237,8 +244,11 @@ int main(int argc, char** argv) {
     vs.push_back(mk6<3, EPI_RELU, 4, 1>("x6_wm4_b1"));
     vs.push_back(mk6q<3, EPI_RELU>("x6q"));
     vs.push_back(mkc3<3, EPI_RELU>("h3c"));
-    vs.push_back(mkw3<3, EPI_RELU>("h3w"));
     vs.push_back(mkr3<3, EPI_RELU>("h3r"));
+    vs.push_back(mks3<3, EPI_RELU, 4, 0>("h3s4"));
+    vs.push_back(mks3<3, EPI_RELU, 4, 1>("h3s4_stg"));
+    vs.push_back(mks3<3, EPI_RELU, 6, 0>("h3s6"));
+    vs.push_back(mks3<3, EPI_RELU, 6, 1>("h3s6_stg"));
   }
   auto args_for = [&](int bm, float* C) {
     GemmArgs a{};
