@@ -819,20 +819,25 @@ constexpr int FCH_BSTAGE = 2 * X6P_B_PLANE;           // one B stage: 160 cols x
 // NB: 16-column blocks per tile (10: 160-column tiles; 21: 336-column tiles, 6 of which cover
 // FC1's 2016 padded outputs with 0.6 % padding instead of 13 x 160 = 2080's 3.8 %, and each A
 // fragment feeds 2.1x the MFMAs: half the A traffic from L2 / Infinity Cache per MFMA).
-template <int NB>
+// NW: waves per workgroup (4: 64 rows each, one per SIMD; 8: 32 rows each, two per SIMD, so a
+// 336-column tile's 168 accumulators fit the 256 registers of a wave).
+template <int NB, int NW = 4>
 struct FcGeo {
   static constexpr int BN = 16 * NB;
+  static constexpr int MBW = 16 / NW;                  // 16-row blocks per wave (tile: 256 rows)
   static constexpr int PLANE = NB * 1024;              // one plane of a B stage
   static constexpr int STAGE = 2 * PLANE;
   static constexpr int PIECES = 2 * NB;                // 1 KiB LDS-DMA pieces per stage
-  static constexpr int NBP = (PIECES + 3) / 4;         // pieces per wave (the last repeated)
+  static constexpr int NBP = (PIECES + NW - 1) / NW;   // pieces per wave (the last repeated)
 };
 
 // NS: ring depth of both operands (A register sets and B LDS slots): K block s+NS-1 is loaded
 // while block s computes.
-template <int LAYER, int EPI, int TM, int NS, int NB = 10>
+template <int LAYER, int EPI, int TM, int NS, int NB = 10, int NW = 4>
 __device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
-  static_assert(NS == 3 || NS == 4, "ring depth");
+  static_assert(NS >= 2 && NS <= 4, "ring depth");
+  using F = FcGeo<NB, NW>;
+  constexpr int MBW = F::MBW;
   constexpr int ROW_KB = 128;                          // bytes per row and 32-deep K block (2 planes)
   const unsigned nblk = gridDim.x, bid = blockIdx.x;
   const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
@@ -855,7 +860,6 @@ __device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const long long m0 = mt * X6P_BM;
-  using F = FcGeo<NB>;
   const int n0 = nt * F::BN;
   const int kb_total = (int)(p.ldb / GBK);
   const int gs0 = ks * (p.kper / GBK);
@@ -863,11 +867,11 @@ __device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
   const int nk = p.kper / GBK;
   auto swz = [](int r) { return (-(r >> 2)) & 3; };
   const int fr = lane & 15, fq = lane >> 4;
-  // this lane's A source: row m0 + wave*64 + 16*mb + fr (clamped), bytes 16*fq of each plane
-  const char* aptr[4];
+  // this lane's A source: row m0 + wave*16*MBW + 16*mb + fr (clamped), bytes 16*fq of each plane
+  const char* aptr[MBW];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) {
-    long long m = m0 + wave * 64 + mb * 16 + fr;
+  for (int mb = 0; mb < MBW; ++mb) {
+    long long m = m0 + wave * 16 * MBW + mb * 16 + fr;
     if (m > p.M - 1) m = p.M - 1;
     const long long kb0 = (p.a_rows ? p.a_rows[m] / GBK : m * lda_kb) + gs0;
     aptr[mb] = (const char*)p.A + kb0 * ROW_KB + 16 * fq;
@@ -876,7 +880,7 @@ __device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
   unsigned boff[F::NBP];
 #pragma unroll
   for (int j = 0; j < F::NBP; ++j) {
-    const int g = min(wave + 4 * j, F::PIECES - 1);    // piece g: plane g / NB, cols 16*(g % NB)
+    const int g = min(wave + NW * j, F::PIECES - 1);   // piece g: plane g / NB, cols 16*(g % NB)
     const int pl = g / NB, r = 16 * (g % NB) + (lane >> 2);
     const int c = (lane & 3) ^ swz(r);
     boff[j] = (unsigned)((long long)r * kb_total * ROW_KB + pl * 64 + 16 * c);
@@ -886,12 +890,12 @@ __device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
     if constexpr ((TM & 8) != 0) s = 0;
     char* base = smem + slot * F::STAGE;
     for (int j = j0; j < j0 + nj; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + min(wave + 4 * j, F::PIECES - 1) * 1024), 16, boff[j],
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + min(wave + NW * j, F::PIECES - 1) * 1024), 16, boff[j],
                                                (unsigned)(s * ROW_KB), 0, 0);
   };
   // A fragments of K block s into ring set `set` (two loads per row block: hi, lo plane)
-  bf16x8 afr[NS][4][3];
-  auto load_a = [&](int s, bf16x8 (&a)[4][3], int mb0, int nmb) {
+  bf16x8 afr[NS][MBW][3];
+  auto load_a = [&](int s, bf16x8 (&a)[MBW][3], int mb0, int nmb) {
     if constexpr ((TM & 8) != 0) s = 0;
     const long long off = (long long)s * ROW_KB;
     for (int mb = mb0; mb < mb0 + nmb; ++mb) {
@@ -900,9 +904,9 @@ __device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
     }
   };
 
-  floatx4v acc[4][NB];
+  floatx4v acc[MBW][NB];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
+  for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
@@ -914,22 +918,25 @@ __device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
     b[1] = *(const bf16x8*)(br + F::PLANE);
   };
   auto pin = [&](int nv) {
+    constexpr int MF = 3 * MBW;                        // MFMAs per unit
 #pragma unroll
-    for (int i = 0; i < 12; ++i) {
+    for (int i = 0; i < MF; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      if ((i % 6) == 0 && i < 6 * nv) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      if ((i % (MF / 2)) == 0 && i < (MF / 2) * nv) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
       if ((i & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
     }
   };
 
   // prologue: A and B of K blocks 0 .. NS-2
-  load_a(0, afr[0], 0, 4);
+  load_a(0, afr[0], 0, MBW);
   issue_b(0, 0, 0, F::NBP);
-  load_a(min(1, nk - 1), afr[1], 0, 4);
-  issue_b(min(1, nk - 1), 1, 0, F::NBP);
+  if constexpr (NS >= 3) {
+    load_a(min(1, nk - 1), afr[1], 0, MBW);
+    issue_b(min(1, nk - 1), 1, 0, F::NBP);
+  }
   if constexpr (NS == 4) {
-    load_a(min(2, nk - 1), afr[2], 0, 4);
+    load_a(min(2, nk - 1), afr[2], 0, MBW);
     issue_b(min(2, nk - 1), 2, 0, F::NBP);
   }
   __builtin_amdgcn_s_waitcnt(0);     // (prologue only) everything above landed
@@ -951,17 +958,17 @@ __device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
     for (int nb = 0; nb < NB; ++nb) {
       int nv = 0;
       if (!(TM & 2)) {
-        if (nb < 4) {                      // A of block s+NS-1: 2 loads per unit
+        if (nb < MBW) {                    // A of block s+NS-1: 2 loads per unit
           if (!(TM & 16)) load_a(sa, afr[nxt], nb, 1);
           nv = 2;
-        } else if (nb < 4 + F::NBP) {      // B of block s+NS-1: 1 piece per unit
-          if (!(TM & 32)) issue_b(sb, lslot, nb - 4, 1);
+        } else if (nb < MBW + F::NBP) {    // B of block s+NS-1: 1 piece per unit
+          if (!(TM & 32)) issue_b(sb, lslot, nb - MBW, 1);
           nv = 1;
         }
       }
       if (nb + 1 < NB) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
 #pragma unroll
-      for (int mb = 0; mb < 4; ++mb)
+      for (int mb = 0; mb < MBW; ++mb)
         acc[mb][nb] = planes_mfma<2>(acc[mb][nb], afr[cur][mb], (nb & 1) ? b1 : b0);
       pin(nv);
     }
@@ -969,7 +976,7 @@ __device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
       // A and B of block s+1 landed in every wave (in flight: blocks s+2 .. s+NS-1, 13 loads
       // each).  The builtin, not asm: the compiler's own wait insertion then knows what has
       // landed (simm16 = vmcnt[3:0] | expcnt 7 << 4 | lgkmcnt 0 << 8 | vmcnt[5:4] << 14).
-      constexpr int VM = (NS - 2) * (8 + F::NBP);   // loads of blocks s+2 .. s+NS-1 stay in flight
+      constexpr int VM = (NS - 2) * (2 * MBW + F::NBP);   // loads of blocks s+2 .. s+NS-1 in flight
       static_assert(VM < 64, "vmcnt field");
       __builtin_amdgcn_s_waitcnt((VM & 15) | (7 << 4) | ((VM >> 4) << 14));   // vmcnt(VM) lgkmcnt(0)
       __builtin_amdgcn_s_barrier();
@@ -983,21 +990,22 @@ __device__ __forceinline__ void gemm_fc_h3_body(const GemmArgs& p, char* smem) {
   for (; s + NS <= nk; s += NS) {
     stage(std::integral_constant<int, 0>{}, s, slot);
     stage(std::integral_constant<int, 1>{}, s + 1, slot);
-    stage(std::integral_constant<int, 2>{}, s + 2, slot);
+    if constexpr (NS >= 3) stage(std::integral_constant<int, 2>{}, s + 2, slot);
     if constexpr (NS == 4) stage(std::integral_constant<int, 3>{}, s + 3, slot);
   }
   if (s < nk) stage(std::integral_constant<int, 0>{}, s, slot);
-  if (s + 1 < nk) stage(std::integral_constant<int, 1>{}, s + 1, slot);
+  if constexpr (NS >= 3)
+    if (s + 1 < nk) stage(std::integral_constant<int, 1>{}, s + 1, slot);
   if constexpr (NS == 4)
     if (s + 2 < nk) stage(std::integral_constant<int, 2>{}, s + 2, slot);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the ring's duplicate tail loads
-  gemm_epilogue16<EPI, 2, NB>(p, acc, m0 + wave * 64, n0, ks, lane);
+  gemm_epilogue16<EPI, 2, NB, MBW>(p, acc, m0 + wave * 16 * MBW, n0, ks, lane);
 }
 
-template <int LAYER, int EPI, int TM = 0, int NS = 3, int NB = 10>
-__global__ __launch_bounds__(256, 1) void beluga_fc_h3(GemmArgs p) {
-  __shared__ __attribute__((aligned(1024))) char smem[NS * FcGeo<NB>::STAGE];
-  gemm_fc_h3_body<LAYER, EPI, TM, NS, NB>(p, smem);
+template <int LAYER, int EPI, int TM = 0, int NS = 3, int NB = 10, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 1) void beluga_fc_h3(GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[NS * FcGeo<NB, NW>::STAGE];
+  gemm_fc_h3_body<LAYER, EPI, TM, NS, NB, NW>(p, smem);
 }
 
 // ---- f16x3 conv GEMM with the Toeplitz A tile staged once per channel chunk -------------
