@@ -66,7 +66,7 @@ def kernel_name(layer: str, precision: str) -> str:
         return f"beluga_gemm_x6q<{l}, {e}, 0>"
     if precision == "f16x3":
         if l in (7, 8):
-            return f"beluga_fc_h3<{l}, {e}, 0, 3, 10>"
+            return f"beluga_fc_h3<{l}, {e}, 0, 3, 10, 4>"
         if e == 0:
             return f"beluga_conv_h3s<{l}, {e}, 0, {4 if l == 6 else 6}, 0>"
         return f"beluga_conv_h3r<{l}, {e}, 0>"

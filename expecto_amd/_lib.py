@@ -67,8 +67,10 @@ SIGNATURES = {
 STRAND_FWD, STRAND_RC, STRAND_BOTH = 0, 1, 2
 PRECISION_FP32, PRECISION_BF16X6, PRECISION_F16X3 = 0, 1, 2
 PRECISIONS = {"fp32": PRECISION_FP32, "bf16x6": PRECISION_BF16X6, "f16x3": PRECISION_F16X3}
-N_LAYERS = 9
-LAYER_NAMES = ("conv1", "conv2", "conv3", "conv4", "conv5", "conv6", "fc1", "fc1_reduce", "fc2")
+_BASE_LAYERS = ("conv1", "conv2", "conv3", "conv4", "conv5", "conv6", "fc1", "fc1_reduce", "fc2")
+# expecto_beluga_layer_times slots: the layers of every forward, then their alt-delta launches
+LAYER_NAMES = _BASE_LAYERS + tuple(f"{n}_delta" for n in _BASE_LAYERS)
+N_LAYERS = len(LAYER_NAMES)
 
 _lib = None
 

@@ -587,9 +587,12 @@ struct expecto_beluga {
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, int>> pending;  // (layer, event index of start)
   size_t ev_next = 0;
-  double ms[kNumLayers] = {};
-  long long calls[kNumLayers] = {};
-  double macs[kNumLayers] = {};  // executed multiply-adds per layer while profiling (host-side count)
+  // timing slots 0..8: the layers of every forward; 9..17: the same layers' alt-delta launches
+  // (pair / segment-pair paths), kept apart so a slot's launches are those of one kernel shape
+  int timer_base = 0;            // kNumLayers while an alt-delta run is being launched
+  double ms[2 * kNumLayers] = {};
+  long long calls[2 * kNumLayers] = {};
+  double macs[2 * kNumLayers] = {};  // executed multiply-adds per slot while profiling (host-side count)
 };
 
 namespace {
@@ -644,7 +647,7 @@ struct LayerTimer {
   int layer;
   int idx = -1;
   hipStream_t st;
-  LayerTimer(expecto_beluga* hh, int l, hipStream_t s) : h(hh), layer(l), st(s) {
+  LayerTimer(expecto_beluga* hh, int l, hipStream_t s) : h(hh), layer(hh->timer_base + l), st(s) {
     if (!h->profiling) return;
     if (h->ev_next + 2 > h->ev_pool.size()) resolve_events(h);
     idx = (int)h->ev_next;
@@ -656,6 +659,13 @@ struct LayerTimer {
     (void)hipEventRecord(h->ev_pool[idx + 1], st);
     h->pending.push_back({layer, idx});
   }
+};
+
+// Launches inside this scope are timed and counted in the alt-delta slots (layer + kNumLayers).
+struct DeltaScope {
+  expecto_beluga* h;
+  explicit DeltaScope(expecto_beluga* hh) : h(hh) { h->timer_base = kNumLayers; }
+  ~DeltaScope() { h->timer_base = 0; }
 };
 
 // Arithmetic of the MFMA GEMMs: exact fp32 (v_mfma_f32_32x32x2_f32), the fp32-faithful 3-way
@@ -672,12 +682,9 @@ bool planes_gemm() { return g_precision != EXPECTO_PRECISION_FP32; }
 long long gemm_bm() { return planes_gemm() ? X6P_BM : GBM; }
 float exp2i(int e) { return std::ldexp(1.0f, e); }
 
-// M tile rows of an f16x3 conv launch.  beluga_conv_h3r (384 rows) and the 256-row kernels give
-// bitwise-equal results, so the choice is free per launch: 384 rows feed 1.5x the MFMAs per
-// weight piece and stage barrier (tools/gemm_bench, 1000 windows: conv2 +5 %, conv4 +3 %; conv3
-// equal to the 8-wave kernel; conv6 -3 %, its 113-row windows give a short grid), so auto takes
-// it for every launch of the pool layers (one kernel per layer, incl. the small alt-delta
-// launches) and leaves the ReLU layers on the 8-wave kernel.
+// M tile rows of an f16x3 conv launch.  The 384-row kernels (beluga_conv_h3r, beluga_conv_h3s<6>)
+// and the 256-row ones (beluga_conv_h3q, beluga_conv_h3s<4>) give bitwise-equal results, so the
+// choice is free per launch (tests/test_gpu_forward.py::test_conv_tile_choice_is_bitwise).
 // l: 0 = conv2 .. 4 = conv6.  384-row tiles run 2-5 % faster per row than 256-row tiles except
 // on conv6 (tools/gemm_bench), but one workgroup fills a CU, so a launch of few tiles (the
 // alt-delta runs of the pair path: 30-60 k rows) is priced by its rounds of 256 workgroups:
@@ -738,7 +745,7 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
 int run_conv1(expecto_beluga* h, const float* x, const uint8_t* codes, long long code_stride, int n_src, int mode,
               long long row0, int nb, int len, int out_rows, hipStream_t st, float* dst = nullptr) {
   LayerTimer lt(h, 0, st);
-  if (h->profiling) h->macs[0] += (double)nb * (len - 7) * 320 * 32;
+  if (h->profiling) h->macs[h->timer_base + 0] += (double)nb * (len - 7) * 320 * 32;
   dim3 grid((len - 7 + C1_T - 1) / C1_T, nb);
   beluga_conv1<<<grid, dim3(320), 0, st>>>(x, codes, code_stride, n_src, mode, row0, h->w1, h->b1,
                                            dst ? dst : h->P, out_rows, len, act_fmt(), exp2i(h->sx[0]), h->ovf);
@@ -773,7 +780,7 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
   a.t_valid = t_valid;
   a.s_out = s_out;
   LayerTimer lt(h, l + 1, st);
-  if (h->profiling) h->macs[l + 1] += (double)a.M * g.cout * a.kper;
+  if (h->profiling) h->macs[h->timer_base + l + 1] += (double)a.M * g.cout * a.kper;
   if (pool) {
     EXPECTO_REQUIRE(s_in % 4 == 0, "pool epilogue needs 4-aligned row groups");
     return l == 0 ? launch_gemm<2, EPI_RELU_POOL4>(a, 1, st, bm) : launch_gemm<4, EPI_RELU_POOL4>(a, 1, st, bm);
@@ -820,7 +827,7 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     a.ks_mask = ks_mask;
     EXPECTO_REQUIRE(!ks_mask || planes_gemm(), "slab mask needs the planes GEMM");
     LayerTimer lt(h, 6, st);
-    if (h->profiling) h->macs[6] += (double)nb * kFc1Out * kFc1In * slab_frac;
+    if (h->profiling) h->macs[h->timer_base + 6] += (double)nb * kFc1Out * kFc1In * slab_frac;
     if ((rc = launch_gemm<7, EPI_PARTIAL>(a, splits, st))) return rc;
   }
   {
@@ -854,7 +861,7 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     a.t_valid = 1;
     a.s_out = 1;
     LayerTimer lt(h, 8, st);
-    if (h->profiling) h->macs[8] += (double)nb * kNFeat * kFc1Out;
+    if (h->profiling) h->macs[h->timer_base + 8] += (double)nb * kNFeat * kFc1Out;
     if ((rc = launch_gemm<8, EPI_SIGMOID>(a, 1, st))) return rc;
   }
   return EXPECTO_OK;
@@ -1035,6 +1042,7 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
         seg_delta_assemble<<<dim3(ns * nbk), dim3(256), 0, st>>>(ref, ref_rows, dprev, wprev, h->seg_tab, nbk,
                                                                       ib, mult, irp, arows, row16, h->DA);
         int r = check_launch("seg_delta_assemble");
+        DeltaScope ds(h);
         return r ? r : run_conv(h, l, h->DA, dnext, (long long)ns * nbk, arows, w, w, pool, st);
       };
       // conv1 from codes: virtual rows = segments; rc mode mirrors inside the kernel
@@ -1048,6 +1056,7 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
         seg_delta_codes<<<dim3((ns + 15) / 16), dim3(256), 0, st>>>(codes, code_stride, pr->alt_code, s0, ns,
                                                                    is_rc ? 1 : 0, L, h->seg_tab, h->delta_codes);
         if ((rc = check_launch("seg_delta_codes"))) return rc;
+        DeltaScope ds(h);
         if ((rc = run_conv1(h, nullptr, h->delta_codes, 16, ns, EXPECTO_STRAND_FWD, 0, ns, kDA[1], kDW[1], st,
                             h->D0)))
           return rc;
@@ -1100,6 +1109,7 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
                 h->win_seg_d, h->win_off_d, win_row ? h->win_row_d : nullptr, h->alt_w_d + ia0, 0, ia1 - ia0, s0,
                 is_rc ? 1 : 0, L, n_ph, phi, g.T6, row_base, h->a_rows, h->c_rows);
             if ((rc = check_launch("seg_a_rows"))) return rc;
+            DeltaScope ds(h);
             if ((rc = run_fc(h, h->Q, h->a_rows, ia1 - ia0, pr->y_alt, st, h->c_rows))) return rc;
           }
           if (ic1 > ic0) {
@@ -1128,8 +1138,11 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
     if ((rc = run_conv1(h, nullptr, ref + (long long)v0 * stride, stride, nv, mode, 0, R, kLen, kS1, st))) return rc;
     delta_codes<<<dim3((R + 15) / 16), dim3(256), 0, st>>>(alt, stride, nv, v0, var_pos, h->delta_codes, R);
     if ((rc = check_launch("delta_codes"))) return rc;
-    if ((rc = run_conv1(h, nullptr, h->delta_codes, 16, R, EXPECTO_STRAND_FWD, 0, R, kDA[1], kDW[1], st, h->D0)))
-      return rc;
+    {
+      DeltaScope ds(h);
+      if ((rc = run_conv1(h, nullptr, h->delta_codes, 16, R, EXPECTO_STRAND_FWD, 0, R, kDA[1], kDW[1], st, h->D0)))
+        return rc;
+    }
     float* src = h->P;
     float* dst = h->Q;
     float* dprev = h->D0;
@@ -1141,6 +1154,7 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
       const int row16 = g.cin * eb / 16;
       delta_assemble<<<dim3(R), dim3(256), 0, st>>>(src, g.s_in, dprev, L, row16, nv, v0, var_pos, h->DA);
       if ((rc = check_launch("delta_assemble"))) return rc;
+      DeltaScope ds(h);
       if ((rc = run_conv(h, l, h->DA, dnext, R, kDA[L], kDW[L], kDW[L], g.pool != 0, st))) return rc;
       std::swap(src, dst);
       std::swap(dprev, dnext);
@@ -1171,6 +1185,7 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
         frac = (double)bits / (tiles * h->fc_splits);
       }
     }
+    DeltaScope ds(h);
     if ((rc = run_fc(h, act6, nullptr, R, y_alt, st, h->c_rows, mask, frac))) return rc;
   }
   return EXPECTO_OK;
@@ -1537,9 +1552,9 @@ int expecto_beluga_set_profiling(expecto_beluga_t h, int on) {
   }
   h->profiling = on != 0;
   if (on) {
-    std::fill(h->ms, h->ms + kNumLayers, 0.0);
-    std::fill(h->calls, h->calls + kNumLayers, 0LL);
-    std::fill(h->macs, h->macs + kNumLayers, 0.0);
+    std::fill(h->ms, h->ms + 2 * kNumLayers, 0.0);
+    std::fill(h->calls, h->calls + 2 * kNumLayers, 0LL);
+    std::fill(h->macs, h->macs + 2 * kNumLayers, 0.0);
   }
   return EXPECTO_OK;
 }
@@ -1548,13 +1563,13 @@ int expecto_beluga_layer_times(expecto_beluga_t h, double* ms, long long* calls,
   EXPECTO_REQUIRE(h != nullptr, "null handle");
   int rc = resolve_events(h);
   if (rc) return rc;
-  const int n = std::min(max_layers, kNumLayers);
+  const int n = std::min(max_layers, 2 * kNumLayers);
   for (int i = 0; i < n; ++i) {
     if (ms) ms[i] = h->ms[i];
     if (calls) calls[i] = h->calls[i];
     if (macs) macs[i] = h->macs[i];
   }
-  return kNumLayers;
+  return 2 * kNumLayers;
 }
 
 }  // extern "C"

@@ -169,7 +169,9 @@ long long expecto_beluga_f16_fallbacks(expecto_beluga_t h, int* sx);
  * (`calls`) and executed multiply-adds (`macs`: GEMM M x N x K actually run, including the
  * few padding rows; reuse paths execute fewer than the dense per-window count).
  * Layers: 0 conv1, 1 conv2, 2 conv3, 3 conv4 (+ pool2 on the segment/patch paths), 4 conv5,
- * 5 conv6, 6 fc1, 7 fc1-reduce, 8 fc2.  Returns the number of layers. */
+ * 5 conv6, 6 fc1, 7 fc1-reduce, 8 fc2; entries 9..17 are the same layers' alt-delta launches
+ * (forward_pairs / forward_segment_pairs), timed apart from the full-window launches.
+ * Fills min(max_layers, 18) entries and returns 18. */
 int expecto_beluga_set_profiling(expecto_beluga_t h, int on);
 int expecto_beluga_layer_times(expecto_beluga_t h, double* ms, long long* calls, double* macs, int max_layers);
 

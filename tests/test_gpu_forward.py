@@ -171,3 +171,22 @@ def test_f16x3_overflow_recomputes_with_bf16x6():
     ya = a.forward_codes(codes, 0).cpu()
     assert a.engine().f16_state()[0] == n0 + 2
     assert_close(ya.numpy(), yb.numpy(), what="f16x3 after re-calibration")
+
+
+def test_conv_tile_choice_is_bitwise(monkeypatch):
+    """The f16x3 conv kernels of every tile shape (384-row: 4-wave pool / 8-wave ReLU; 256-row:
+    4-wave pool / 8-wave ReLU) produce the same bits, so the per-launch choice (auto: by CU
+    rounds) never changes a result: auto, all-256 and all-384 handles agree exactly."""
+    import torch
+    from expecto_amd import beluga
+    rng = np.random.default_rng(11)
+    codes = torch.from_numpy(rng.integers(0, 5, (150, 2000)).astype(np.uint8)).cuda()
+    out = {}
+    for tile in ("0", "256", "384"):
+        monkeypatch.setenv("EXPECTO_CONV_TILE", tile)
+        m = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=300).cuda()
+        m.engine().set_precision("f16x3")
+        out[tile] = m.forward_codes(codes, 2).cpu()
+        del m
+    assert torch.equal(out["0"], out["256"])
+    assert torch.equal(out["0"], out["384"])
