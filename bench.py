@@ -67,9 +67,9 @@ def kernel_name(layer: str, precision: str) -> str:
     if precision == "f16x3":
         if l in (7, 8):
             return f"beluga_fc_h3<{l}, {e}, 0, 3, 10, 4>"
-        if e == 0:
-            return f"beluga_conv_h3s<{l}, {e}, 0, {4 if l == 6 else 6}, 0>"
-        return f"beluga_conv_h3r<{l}, {e}, 0>"
+        if l == 2:   # conv2: 384-row tiles (the other conv layers: producer/consumer 256-row tiles)
+            return f"beluga_conv_h3r<{l}, {e}, 0>"
+        return f"beluga_conv_h3p<{l}, {e}, 0, 3>"
     return f"beluga_gemm<{l}, {e}, 4, 2, 32, 1>"
 WINDOW_MACS = sum(LAYER_MACS.values())
 

@@ -683,23 +683,23 @@ long long gemm_bm() { return planes_gemm() ? X6P_BM : GBM; }
 float exp2i(int e) { return std::ldexp(1.0f, e); }
 
 // M tile rows of an f16x3 conv launch.  The 384-row kernels (beluga_conv_h3r, beluga_conv_h3s<6>)
-// and the 256-row ones (beluga_conv_h3q, beluga_conv_h3s<4>) give bitwise-equal results, so the
+// and the 256-row producer/consumer kernel (beluga_conv_h3p) give bitwise-equal results, so the
 // choice is free per launch (tests/test_gpu_forward.py::test_conv_tile_choice_is_bitwise).
-// l: 0 = conv2 .. 4 = conv6.  384-row tiles run 2-5 % faster per row than 256-row tiles except
-// on conv6 (tools/gemm_bench), but one workgroup fills a CU, so a launch of few tiles (the
-// alt-delta runs of the pair path: 30-60 k rows) is priced by its rounds of 256 workgroups:
-// the tile with the fewer row-rounds wins there (e.g. conv3 alt: 297 x 384 = 2 rounds of 384
-// rows vs 447 x 256 = 2 rounds of 256 rows).  Every conv kernel gives the same bits.
+// tools/gemm_bench (2000 windows, fp32-equivalent TF/s): conv2 h3r 520 vs h3p 505-510; conv3
+// h3p 484 vs 468 (h3s<6>), conv4 522 vs 496 (h3r), conv5 491 vs 480, conv6 497 vs 467: 384-row
+// tiles only for conv2.  One workgroup fills a CU, so a launch is priced by its rounds of 256
+// workgroups (the alt-delta runs of the pair path, 30-60 k rows, take whichever tile needs the
+// fewer row-rounds).  l: 0 = conv2 .. 4 = conv6.
 int conv_tile_rows(const expecto_beluga* h, int l, bool pool, long long M, int n_tiles) {
   if (g_precision != EXPECTO_PRECISION_F16X3) return (int)gemm_bm();
   if (h->conv_tile) return h->conv_tile;
-  if (!pool && l == 4) return 256;
+  if (!(pool && l == 0)) return 256;
   const int cus = h->cus > 0 ? h->cus : 256;
   auto cost = [&](int bm, double per_row) {
     const long long blocks = (M + bm - 1) / bm * n_tiles;
     return (double)((blocks + cus - 1) / cus) * bm * per_row;
   };
-  return cost(384, 1.0) <= cost(256, 1.04) ? 384 : 256;
+  return cost(384, 1.0) <= cost(256, 1.02) ? 384 : 256;
 }
 
 template <int LAYER, int EPI>
@@ -723,16 +723,15 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
       EXPECTO_REQUIRE(splits == 1 && a.kper == a.ldb && a.ldb == 8 * a.lda && !a.m_fastest && !a.a_rows,
                       "f16x3 conv GEMM: full K, no split, no row gather");
       // all bitwise equal (same products and k order per output); per-layer choice from
-      // tools/gemm_bench: pool layers 4 waves x 96 rows, ReLU layers 8 waves (two per SIMD)
-      if constexpr (EPI == EPI_RELU) {
-        if (bm == 384)
+      // tools/gemm_bench: 256-row tiles on the producer/consumer kernel (MFMA waves never issue
+      // LDS-DMA), 384-row tiles (conv2) on the 4-wave 96-row kernel
+      if (bm == 384) {
+        if constexpr (EPI == EPI_RELU)
           beluga_conv_h3s<LAYER, EPI, 0, 6><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
         else
-          beluga_conv_h3s<LAYER, EPI, 0, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
-      } else if (bm == 384) {
-        beluga_conv_h3r<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
+          beluga_conv_h3r<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
       } else {
-        beluga_conv_h3q<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
+        beluga_conv_h3p<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
       }
     } else {   // FC layers: A fragments straight into registers, B through LDS (same bits)
       beluga_fc_h3<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);

@@ -62,6 +62,11 @@ Variant mkr3(const char* name) {
   return {name, 384, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3r<L, EPI, TM><<<nblk, 256>>>(a); }};
 }
 
+template <int L, int EPI, int TM = 0, int NSB = 3>
+Variant mkp3(const char* name) {
+  return {name, X6P_BM, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3p<L, EPI, TM, NSB><<<nblk, 512>>>(a); }};
+}
+
 template <int L, int EPI, int MB, int STG, int TM = 0>
 Variant mks3(const char* name) {
   return {name, 64 * MB, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3s<L, EPI, TM, MB, STG><<<nblk, 512>>>(a); }};
@@ -233,9 +238,10 @@ int main(int argc, char** argv) {
     vs.push_back(mkc3<2, EPI_RELU_POOL4>("h3c"));
     vs.push_back(mkr3<2, EPI_RELU_POOL4>("h3r"));
     vs.push_back(mks3<2, EPI_RELU_POOL4, 4, 0>("h3s4"));
-    vs.push_back(mks3<2, EPI_RELU_POOL4, 4, 1>("h3s4_stg"));
+    vs.push_back(mkp3<2, EPI_RELU_POOL4>("h3p"));
+    vs.push_back(mkp3<2, EPI_RELU_POOL4, 0, 4>("h3p4"));
+    vs.push_back(mkp3<2, EPI_RELU_POOL4, 2>("h3p_noglds"));
     vs.push_back(mks3<2, EPI_RELU_POOL4, 6, 0>("h3s6"));
-    vs.push_back(mks3<2, EPI_RELU_POOL4, 6, 1>("h3s6_stg"));
     vs.push_back(mkr3<2, EPI_RELU_POOL4, 2>("h3r_noglds"));
     vs.push_back(mkr3<2, EPI_RELU_POOL4, 4>("h3r_nobar"));
     vs.push_back(mkr3<2, EPI_RELU_POOL4, 6>("h3r_noglds_nobar"));
@@ -246,9 +252,9 @@ int main(int argc, char** argv) {
     vs.push_back(mkc3<3, EPI_RELU>("h3c"));
     vs.push_back(mkr3<3, EPI_RELU>("h3r"));
     vs.push_back(mks3<3, EPI_RELU, 4, 0>("h3s4"));
-    vs.push_back(mks3<3, EPI_RELU, 4, 1>("h3s4_stg"));
+    vs.push_back(mkp3<3, EPI_RELU>("h3p"));
+    vs.push_back(mkp3<3, EPI_RELU, 0, 4>("h3p4"));
     vs.push_back(mks3<3, EPI_RELU, 6, 0>("h3s6"));
-    vs.push_back(mks3<3, EPI_RELU, 6, 1>("h3s6_stg"));
   }
   auto args_for = [&](int bm, float* C) {
     GemmArgs a{};
