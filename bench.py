@@ -66,7 +66,7 @@ def kernel_name(layer: str, precision: str) -> str:
         return f"beluga_gemm_x6q<{l}, {e}, 0>"
     if precision == "f16x3":
         if l in (7, 8):
-            return f"beluga_fc_h3<{l}, {e}, 0, 3, 10, 4>"
+            return f"beluga_fc_h3p<{l}, {e}, 0, 3>"
         if l == 2:   # conv2: 384-row tiles (the other conv layers: producer/consumer 256-row tiles)
             return f"beluga_conv_h3r<{l}, {e}, 0>"
         return f"beluga_conv_h3p<{l}, {e}, 0, 3>"

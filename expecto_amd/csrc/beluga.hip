@@ -733,8 +733,8 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
       } else {
         beluga_conv_h3p<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
       }
-    } else {   // FC layers: A fragments straight into registers, B through LDS (same bits)
-      beluga_fc_h3<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
+    } else {   // FC layers: producer / consumer waves, both operands through an LDS ring (same bits)
+      beluga_fc_h3p<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
     }
   } else
     beluga_gemm<LAYER, EPI, kWM, kMinBlocks, GBK, kPipe><<<dim3((unsigned)nblk), dim3(64 * kWM), 0, st>>>(a);

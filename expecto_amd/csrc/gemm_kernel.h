@@ -1008,6 +1008,170 @@ __global__ __launch_bounds__(64 * NW, 1) void beluga_fc_h3(GemmArgs p) {
   gemm_fc_h3_body<LAYER, EPI, TM, NS, NB, NW>(p, smem);
 }
 
+// ---- f16x3 FC GEMM, producer / consumer waves ---------------------------------------------
+// beluga_fc_h3's tile (256 rows x 160 columns, 4 MFMA waves of 64 rows) with both operands
+// staged through an LDS ring by 4 producer waves (one per SIMD beside its MFMA wave), so the
+// MFMA waves issue only ds_reads and MFMAs.  A stage = one 32-deep K block: A 256 rows x 2
+// planes (32 pieces, per-lane 64-bit sources: a_rows gathers windows from anywhere in the
+// activation buffer) + B 160 columns x 2 planes (20 pieces); 3 stages = 156 KB.  Same operands,
+// products and k order per output as beluga_fc_h3: bitwise equal.
+constexpr int FCP_APLANE = 256 * 64;                   // 16 KB
+constexpr int FCP_STAGE = 2 * FCP_APLANE + 2 * X6P_B_PLANE;   // 52 KB
+
+template <int LAYER, int EPI, int TM, int NS>
+__device__ __forceinline__ void gemm_fc_h3p_body(const GemmArgs& p, char* smem) {
+  static_assert(NS == 3 || NS == 4, "ring depth");
+  constexpr int ROW_KB = 128;
+  const unsigned nblk = gridDim.x, bid = blockIdx.x;
+  const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
+  const unsigned lin =
+      p.linear_order ? bid : (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  long long mt;
+  int nt, ks;
+  if (p.m_fastest) {
+    mt = lin % p.m_tiles;
+    const long long rest = lin / p.m_tiles;
+    nt = (int)(rest % p.n_tiles);
+    ks = (int)(rest / p.n_tiles);
+  } else {
+    nt = (int)(lin % (unsigned)p.n_tiles);
+    const long long rest = lin / (unsigned)p.n_tiles;
+    mt = rest % p.m_tiles;
+    ks = (int)(rest / p.m_tiles);
+  }
+  if (p.ks_mask && !((p.ks_mask[mt] >> ks) & 1u)) return;   // slab unchanged: partials already in C
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const long long m0 = mt * X6P_BM;
+  const int n0 = nt * GBN;
+  const int kb_total = (int)(p.ldb / GBK);
+  const int gs0 = ks * (p.kper / GBK);
+  const long long lda_kb = p.lda / GBK;
+  const int nk = p.kper / GBK;
+  auto swz = [](int r) { return (-(r >> 2)) & 3; };
+
+  if (wave >= 4) {
+    // ---------------- producer ----------------
+    const int pw = wave - 4;
+    // A pieces P = pw + 4*i (i < 8) of 32: plane P & 1, rows 16*(P >> 1) + (lane >> 2)
+    const char* asrc[8];
+    unsigned adst[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int P = pw + 4 * i, g = P >> 1, pl = P & 1;
+      const int r = 16 * g + (lane >> 2);
+      long long m = m0 + r;
+      if (m > p.M - 1) m = p.M - 1;
+      const long long kb0 = (p.a_rows ? p.a_rows[m] / GBK : m * lda_kb) + gs0;
+      const int c = (lane & 3) ^ swz(r);
+      asrc[i] = (const char*)p.A + kb0 * ROW_KB + pl * 64 + 16 * c;
+      adst[i] = (unsigned)(pl * FCP_APLANE + g * 1024);
+    }
+    const char* Bb = (const char*)p.Bp + ((long long)n0 * kb_total + gs0) * ROW_KB;
+    unsigned boff[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int g = pw + 4 * j;
+      const int pl = g / 10, r = 16 * (g % 10) + (lane >> 2);
+      const int c = (lane & 3) ^ swz(r);
+      boff[j] = (unsigned)((long long)r * kb_total * ROW_KB + pl * 64 + 16 * c);
+    }
+    const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, 0x7fffffff, 0x00020000);
+    auto issue = [&](int s, int slot) {
+      if constexpr ((TM & 8) != 0) s = 0;
+      char* base = smem + slot * FCP_STAGE;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) glds16(asrc[i] + (long long)s * ROW_KB, base + adst[i]);
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + 2 * FCP_APLANE + (pw + 4 * j) * 1024), 16,
+                                                 boff[j], (unsigned)(s * ROW_KB), 0, 0);
+    };
+    for (int s = 0; s < NS - 1; ++s) issue(min(s, nk - 1), s);
+    if constexpr (NS == 3)
+      asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(26)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    int slot = 0;
+    for (int s = 0; s < nk; ++s) {
+      const int lslot = slot == 0 ? NS - 1 : slot - 1;   // stage s+NS-1 goes where s-1 was
+      if (!(TM & 2)) issue(min(s + NS - 1, nk - 1), lslot);
+      // all but the pieces of the last NS-2 stages: stage s+1 landed
+      if constexpr (NS == 3)
+        asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(26)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      slot = slot + 1 == NS ? 0 : slot + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
+
+  // ---------------- consumer ----------------
+  floatx4v acc[4][10];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 10; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[mb][nb][r] = 0.f;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int brow = fr * 64 + 16 * (fq ^ swz(fr));
+  const int arow = (wave * 64 + fr) * 64 + 16 * (fq ^ swz(fr));   // swz(wave*64 + mb*16 + fr) = swz(fr)
+  auto read_a = [&](const char* base, bf16x8 (&a)[4][3]) {
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      a[mb][0] = *(const bf16x8*)(base + arow + mb * 1024);
+      a[mb][1] = *(const bf16x8*)(base + arow + mb * 1024 + FCP_APLANE);
+    }
+  };
+  auto read_b = [&](const char* base, int nb, bf16x8 (&b)[3]) {
+    const char* br = base + 2 * FCP_APLANE + brow + nb * 1024;
+    b[0] = *(const bf16x8*)(br);
+    b[1] = *(const bf16x8*)(br + X6P_B_PLANE);
+  };
+  auto pin = [&]() {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if ((i & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+    }
+  };
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  bf16x8 as[4][3];
+  read_a(smem, as);
+  int slot = 0;
+  for (int s = 0; s < nk; ++s) {
+    const char* base = smem + slot * FCP_STAGE;
+    const int nslot = slot + 1 == NS ? 0 : slot + 1;
+    bf16x8 b0[3], b1[3];
+    read_b(base, 0, b0);
+#pragma unroll
+    for (int nb = 0; nb < 10; ++nb) {
+      if (nb + 1 < 10) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) acc[mb][nb] = planes_mfma<2>(acc[mb][nb], as[mb], (nb & 1) ? b1 : b0);
+      pin();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + 1 < nk) read_a(smem + nslot * FCP_STAGE, as);
+    slot = nslot;
+  }
+  gemm_epilogue16<EPI, 2, 10, 4>(p, acc, m0 + wave * 64, n0, ks, lane);
+}
+
+template <int LAYER, int EPI, int TM = 0, int NS = 3>
+__global__ __launch_bounds__(512, 1) void beluga_fc_h3p(GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[NS * FCP_STAGE];
+  gemm_fc_h3p_body<LAYER, EPI, TM, NS>(p, smem);
+}
+
 // ---- f16x3 conv GEMM with the Toeplitz A tile staged once per channel chunk -------------
 // For a k=8 conv the 8 taps of one 32-channel chunk read A rows m0+tap .. m0+tap+255: the same
 // 263 rows shifted by one.  gemm_planes_body re-stages them for every tap (8x the A traffic);

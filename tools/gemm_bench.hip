@@ -99,6 +99,8 @@ __global__ void hash_fill(float* d, long long n, float lo, float hi, unsigned se
 // the f16x3 planes GEMM and its timing probes (TM 2: no LDS-DMA in the loop).
 template <int TM>
 void fc1_launch(const GemmArgs& a, unsigned nblk) { beluga_gemm_h3q<7, EPI_PARTIAL, TM, 3><<<nblk, 256>>>(a); }
+template <int TM, int NS = 3>
+void fc1p_launch(const GemmArgs& a, unsigned nblk) { beluga_fc_h3p<7, EPI_PARTIAL, TM, NS><<<nblk, 512>>>(a); }
 template <int TM, int NS = 3, int NB = 10, int NW = 4>
 void fc1r_launch(const GemmArgs& a, unsigned nblk) { beluga_fc_h3<7, EPI_PARTIAL, TM, NS, NB, NW><<<nblk, 64 * NW>>>(a); }
 
@@ -130,9 +132,8 @@ int fc1_bench(int nb, int rounds, int splits) {
             {"fcr_m", fc1r_launch<0>}, {"fcr_n", fc1r_launch<0>}, {"fcr_x", fc1r_launch<0>},
             {"fcr_x_noload", fc1r_launch<2>}, {"fcr_x_hotAB", fc1r_launch<8>},
             {"fc4_m", fc1r_launch<0, 4>}, {"fc4_x", fc1r_launch<0, 4>},
-            {"f8w_m", fc1r_launch<0, 3, 21, 8>, 21}, {"f8w_x", fc1r_launch<0, 3, 21, 8>, 21},
-            {"f8w2_m", fc1r_launch<0, 2, 21, 8>, 21}, {"f8w_x_noload", fc1r_launch<2, 3, 21, 8>, 21},
-            {"f8w_x_hotAB", fc1r_launch<8, 3, 21, 8>, 21}, {"f8n_m", fc1r_launch<0, 3, 10, 8>, 10}};
+            {"fcp_m", fc1p_launch<0>}, {"fcp_x", fc1p_launch<0>}, {"fcp_x_noload", fc1p_launch<2>},
+            {"fcp_x_hotAB", fc1p_launch<8>}, {"fc4p_m", fc1p_launch<0, 4>}};
   constexpr int NV = sizeof(vs) / sizeof(vs[0]);
   const size_t csz = (size_t)splits * nb * ldc;
   std::vector<float> ref(csz), out(csz);
