@@ -1837,13 +1837,15 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
     const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, 0x7fffffff, 0x00020000);
     auto issue_a = [&](int chunk, int i0, int ni) {
       char* base = aslab + (chunk & 1) * G::ASLAB;
+      const int src_chunk = (TM & 8) ? 0 : chunk;
       for (int i = i0; i < i0 + ni; ++i) {
         const int P = min(pw + 4 * i, G::PIECES - 1);
         char* dst = base + (P & 1) * G::APLANE + (P >> 1) * 1024;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (lds_void*)dst, 16, aoff[i], (unsigned)(chunk * ROW_KB), 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (lds_void*)dst, 16, aoff[i], (unsigned)(src_chunk * ROW_KB), 0, 0);
       }
     };
     auto issue_b = [&](int s, int slot) {
+      if constexpr ((TM & 8) != 0) s = 0;
       char* base = bring + slot * H3C_BSTAGE;
 #pragma unroll
       for (int j = 0; j < 5; ++j)

@@ -133,7 +133,7 @@ int fc1_bench(int nb, int rounds, int splits) {
             {"fcr_x_noload", fc1r_launch<2>}, {"fcr_x_hotAB", fc1r_launch<8>},
             {"fc4_m", fc1r_launch<0, 4>}, {"fc4_x", fc1r_launch<0, 4>},
             {"fcp_m", fc1p_launch<0>}, {"fcp_x", fc1p_launch<0>}, {"fcp_x_noload", fc1p_launch<2>},
-            {"fcp_x_hotAB", fc1p_launch<8>}, {"fc4p_m", fc1p_launch<0, 4>}};
+            {"fcp_x_hotAB", fc1p_launch<8>}};
   constexpr int NV = sizeof(vs) / sizeof(vs[0]);
   const size_t csz = (size_t)splits * nb * ldc;
   std::vector<float> ref(csz), out(csz);
@@ -242,6 +242,7 @@ int main(int argc, char** argv) {
     vs.push_back(mkp3<2, EPI_RELU_POOL4>("h3p"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 0, 4>("h3p4"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 2>("h3p_noglds"));
+    vs.push_back(mkp3<2, EPI_RELU_POOL4, 8>("h3p_hotAB"));
     vs.push_back(mks3<2, EPI_RELU_POOL4, 6, 0>("h3s6"));
     vs.push_back(mkr3<2, EPI_RELU_POOL4, 2>("h3r_noglds"));
     vs.push_back(mkr3<2, EPI_RELU_POOL4, 4>("h3r_nobar"));
