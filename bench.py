@@ -190,9 +190,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the cfg3 / 200-window extra workloads")
     ap.add_argument("--precision", default=None, help="GEMM arithmetic (default: the engine default)")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for the scaling runs; gloo to "
+                    "rehearse several ranks on one GPU")
     args = ap.parse_args()
 
-    rank, world, local = edist.init("nccl")
+    rank, world, local = edist.init(args.dist_backend)
+    # one rank per GPU; a rehearsal on fewer GPUs than ranks (--dist-backend gloo) shares them
+    local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     from expecto_amd.pipeline import shift_order
