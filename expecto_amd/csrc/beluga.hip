@@ -570,6 +570,9 @@ struct expecto_beluga {
   int seg_var_cap = 0;
   int* win_off_d = nullptr;
   int* win_row_d = nullptr;
+  hipStream_t st2 = nullptr;     // pair path: alt-delta launches overlap the ref launches
+  hipEvent_t pev[12] = {};       //   (ordering events, no timing)
+  bool overlap = true;           //   EXPECTO_OVERLAP=0: one stream (same bits either way)
   float* DA = nullptr;           // alt-delta buffers (pair path), lazily allocated:
   float* D0 = nullptr;           //   DA = assembled input patch, D0/D1 = alternating W_l-row runs
   float* D1 = nullptr;
@@ -897,6 +900,10 @@ int ensure_delta(expecto_beluga* h) {
     return rc;
   h->delta_codes = reinterpret_cast<uint8_t*>(pc);
   h->seg_tab = reinterpret_cast<int*>(tb);
+  if (h->overlap) {
+    EXPECTO_HIP_CHECK(hipStreamCreateWithFlags(&h->st2, hipStreamNonBlocking));
+    for (hipEvent_t& e : h->pev) EXPECTO_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   return EXPECTO_OK;
 }
 
@@ -1131,15 +1138,27 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
   if ((rc = ensure_delta(h))) return rc;
   const int eb = act_bytes();   // bytes per activation element
   const int nv_max = std::max(1, h->max_batch / strands);
+  // Alt-delta launches go to a second stream (st2) so their few workgroups fill the rounds the
+  // ref launches leave partly empty: alt layer l needs the ref layer l-1 output (event after the
+  // ref launch that wrote it) and the ref layer l+1 launch, which overwrites that buffer (ping-
+  // pong), waits until the alt patch of layer l has been assembled.
+  hipStream_t sa = h->st2 ? h->st2 : st;
+  auto order = [&](hipStream_t from, hipStream_t to, hipEvent_t e) -> int {
+    if (from == to) return EXPECTO_OK;
+    EXPECTO_HIP_CHECK(hipEventRecord(e, from));
+    EXPECTO_HIP_CHECK(hipStreamWaitEvent(to, e, 0));
+    return EXPECTO_OK;
+  };
   for (int v0 = 0; v0 < n; v0 += nv_max) {
     const int nv = std::min(nv_max, n - v0), R = strands * nv;
+    if ((rc = order(st, sa, h->pev[0]))) return rc;   // caller's inputs (and the previous chunk)
     // conv1: ref windows (full) and the alt runs (15 codes -> 8 rows)
     if ((rc = run_conv1(h, nullptr, ref + (long long)v0 * stride, stride, nv, mode, 0, R, kLen, kS1, st))) return rc;
-    delta_codes<<<dim3((R + 15) / 16), dim3(256), 0, st>>>(alt, stride, nv, v0, var_pos, h->delta_codes, R);
+    delta_codes<<<dim3((R + 15) / 16), dim3(256), 0, sa>>>(alt, stride, nv, v0, var_pos, h->delta_codes, R);
     if ((rc = check_launch("delta_codes"))) return rc;
     {
       DeltaScope ds(h);
-      if ((rc = run_conv1(h, nullptr, h->delta_codes, 16, R, EXPECTO_STRAND_FWD, 0, R, kDA[1], kDW[1], st, h->D0)))
+      if ((rc = run_conv1(h, nullptr, h->delta_codes, 16, R, EXPECTO_STRAND_FWD, 0, R, kDA[1], kDW[1], sa, h->D0)))
         return rc;
     }
     float* src = h->P;
@@ -1149,15 +1168,18 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
     for (int l = 0; l < 5; ++l) {   // conv2..conv6 (layer index l+2 in the delta tables)
       const ConvGeo& g = kConv[l];
       const int L = l + 2;
+      if ((rc = order(st, sa, h->pev[1 + 2 * l]))) return rc;   // src (ref layer l-1) written
       if ((rc = run_conv(h, l, src, dst, R, g.s_in, g.t_valid, g.s_out, g.pool != 0, st))) return rc;
       const int row16 = g.cin * eb / 16;
-      delta_assemble<<<dim3(R), dim3(256), 0, st>>>(src, g.s_in, dprev, L, row16, nv, v0, var_pos, h->DA);
+      delta_assemble<<<dim3(R), dim3(256), 0, sa>>>(src, g.s_in, dprev, L, row16, nv, v0, var_pos, h->DA);
       if ((rc = check_launch("delta_assemble"))) return rc;
+      if ((rc = order(sa, st, h->pev[2 + 2 * l]))) return rc;   // src read: ref l+1 may overwrite it
       DeltaScope ds(h);
-      if ((rc = run_conv(h, l, h->DA, dnext, R, kDA[L], kDW[L], kDW[L], g.pool != 0, st))) return rc;
+      if ((rc = run_conv(h, l, h->DA, dnext, R, kDA[L], kDW[L], kDW[L], g.pool != 0, sa))) return rc;
       std::swap(src, dst);
       std::swap(dprev, dnext);
     }
+    if ((rc = order(sa, st, h->pev[11]))) return rc;   // alt conv6 runs done
     float* act6 = src;   // ref conv6 rows; dprev = the alt runs' conv6 rows
     pair_rows<<<dim3((R + 255) / 256), dim3(256), 0, st>>>(h->c_rows, R, nv, v0, strand_stride);
     if ((rc = check_launch("pair_rows"))) return rc;
@@ -1368,6 +1390,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
     EXPECTO_REQUIRE(v >= 1 && v <= 32 && (kFc1In / GBK) % v == 0, "EXPECTO_FC1_SPLITS must divide 2120 and be <= 32");
     h->fc_splits = v;
   }
+  if (const char* e = getenv("EXPECTO_OVERLAP")) h->overlap = atoi(e) != 0;   // same bits either way
   if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)
     const int v = atoi(e);
     EXPECTO_REQUIRE(v == 0 || v == 256 || v == 384, "EXPECTO_CONV_TILE must be 0 (auto), 256 or 384");
@@ -1403,6 +1426,9 @@ void expecto_beluga_destroy(expecto_beluga_t h) {
   if (h->win_row_d) (void)hipFree(h->win_row_d);
   for (void* p : h->allocs) (void)hipFree(p);
   for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+  for (hipEvent_t e : h->pev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->st2) (void)hipStreamDestroy(h->st2);
   delete h;
 }
 
