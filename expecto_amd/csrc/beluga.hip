@@ -396,6 +396,27 @@ __global__ void seg_alt_blocks(const float* __restrict__ ref6, const float* __re
   for (int c = threadIdx.x; c < row16; c += blockDim.x) dst[c] = src[c];
 }
 
+// FC1 split-K slabs the alt windows of a segment chunk change (FC row m = window widx[m]; cf.
+// fc1_slab_mask): the window reads conv6 rows [off6, off6+106) of block (segment, pool2
+// phase), whose alt run replaced block rows [r6, r6+20) (seg_delta_table), so its FC1 K range
+// that changed is 640 x that intersection.
+__global__ void fc1_slab_mask_seg(const int* __restrict__ widx, int n_alt, const int* __restrict__ win_seg,
+                                  const int* __restrict__ win_off, int seg_base, int rc, int seg_len, int4 ph_idx,
+                                  const int* __restrict__ tab, int tile_rows, int slab_k, unsigned* __restrict__ mask) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= n_alt) return;
+  const int w = widx[m];
+  const int o = rc ? seg_len - 2000 - win_off[w] : win_off[w];
+  const int q = o >> 2, p = q & 3, off6 = (q - p) >> 2;
+  const int pi = p == 0 ? ph_idx.x : p == 1 ? ph_idx.y : p == 2 ? ph_idx.z : ph_idx.w;
+  const int r6 = tab[(win_seg[w] - seg_base) * kSegTab + 13 + pi];
+  const int lo = max(r6 - off6, 0), hi = min(r6 + kDW[6] - off6, 106);
+  if (lo >= hi) return;
+  unsigned bits = 0;
+  for (int ks = lo * 640 / slab_k; ks <= (hi * 640 - 1) / slab_k; ++ks) bits |= 1u << ks;
+  atomicOr(mask + m / tile_rows, bits);
+}
+
 // y_alt rows of windows whose alt sequence equals the ref one (the SNV lies outside them)
 __global__ void copy_rows(const float* __restrict__ src, float* __restrict__ dst, const int* __restrict__ widx,
                           const int* __restrict__ win_row, long long row_base) {
@@ -570,6 +591,7 @@ struct expecto_beluga {
   int seg_var_cap = 0;
   int* win_off_d = nullptr;
   int* win_row_d = nullptr;
+  int* fc_perm_d = nullptr;      // segment pairs: FC row order per strand (2 x win_cap)
   hipStream_t st2 = nullptr;     // pair path: alt-delta launches overlap the ref launches
   hipEvent_t pev[12] = {};       //   (ordering events, no timing)
   bool overlap = true;           //   EXPECTO_OVERLAP=0: one stream (same bits either way)
@@ -797,8 +819,13 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
 
 // FC1 (split-K) + reduce + FC2/sigmoid for nb windows whose conv6 rows are at act
 // (+ a_rows[m] when given, else m*67840).
+// part_rows: row count of the split-K partial slabs (default nb): an alt FC1 that recomputes
+// only some slabs of the first nb rows of an earlier ref FC1 over part_rows rows reuses its
+// partials for the others.
 int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb, float* y, hipStream_t st,
-           const long long* c_rows = nullptr, const unsigned* ks_mask = nullptr, double slab_frac = 1.0) {
+           const long long* c_rows = nullptr, const unsigned* ks_mask = nullptr, double slab_frac = 1.0,
+           long long part_rows = 0) {
+  if (part_rows <= 0) part_rows = nb;
   int rc;
   const long long m_tiles = (nb + gemm_bm() - 1) / gemm_bm();
   const int n_tiles1 = npad_of(kFc1Out) / GBN;
@@ -824,7 +851,7 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     a.C = h->part;
     a.ldc = kHidLd;
     a.n_store = kHidLd;
-    a.split_stride = (long long)nb * kHidLd;
+    a.split_stride = part_rows * kHidLd;
     a.linear_order = 1;
     a.ks_mask = ks_mask;
     EXPECTO_REQUIRE(!ks_mask || planes_gemm(), "slab mask needs the planes GEMM");
@@ -837,7 +864,7 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     const long long count = (long long)nb * kHidLd;
     const bool f16 = g_precision == EXPECTO_PRECISION_F16X3;
     fc1_reduce<<<dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st>>>(
-        h->part, splits, count, count, h->fc1b, h->h1, act_fmt(), f16 ? h->cs[5] : nullptr, exp2i(h->sx[6]), h->ovf);
+        h->part, splits, part_rows * kHidLd, count, h->fc1b, h->h1, act_fmt(), f16 ? h->cs[5] : nullptr, exp2i(h->sx[6]), h->ovf);
     if ((rc = check_launch("fc1_reduce"))) return rc;
   }
   {
@@ -981,13 +1008,14 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
   for (int w = n_win - 1; w >= 0; --w) first[win_seg[w]] = w;
   for (int sg = n_seg - 1; sg >= 0; --sg) first[sg] = std::min(first[sg], first[sg + 1]);
   if (n_win > h->win_cap) {
-    for (int** b : {&h->win_seg_d, &h->win_off_d, &h->win_row_d, &h->alt_w_d, &h->copy_w_d}) {
+    for (int** b : {&h->win_seg_d, &h->win_off_d, &h->win_row_d, &h->alt_w_d, &h->copy_w_d, &h->fc_perm_d}) {
       if (*b) EXPECTO_HIP_CHECK(hipFree(*b));
       *b = nullptr;
     }
     h->win_cap = 0;
     for (int** b : {&h->win_seg_d, &h->win_off_d, &h->win_row_d, &h->alt_w_d, &h->copy_w_d})
       EXPECTO_HIP_CHECK(hipMalloc(b, n_win * sizeof(int)));
+    EXPECTO_HIP_CHECK(hipMalloc(&h->fc_perm_d, 2 * n_win * sizeof(int)));
     h->win_cap = n_win;
   }
   std::vector<int> alt_w, copy_w;
@@ -1018,24 +1046,60 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
   }
   EXPECTO_HIP_CHECK(hipMemcpyAsync(h->win_seg_d, win_seg, n_win * sizeof(int), hipMemcpyHostToDevice, st));
   EXPECTO_HIP_CHECK(hipMemcpyAsync(h->win_off_d, win_off, n_win * sizeof(int), hipMemcpyHostToDevice, st));
-  // the tables are caller-owned pageable host memory: finish the copies before returning
-  EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
   const int strands = mode == EXPECTO_STRAND_BOTH ? 2 : 1;
   // alt runs: one block per segment (conv1..4) or per (segment, phase) (pool2, conv5, conv6)
   const int blk_per_seg = pr ? std::max(n_ph, 1) : 0;
+  // chunks of whole segments: grow while the segment buffers, the FC workspace (<= max_batch
+  // windows) and the alt-run buffers (<= max_batch blocks) fit
+  std::vector<std::pair<int, int>> chunks;
+  for (int s0 = 0; s0 < n_seg;) {
+    int s1 = s0 + 1;
+    while (s1 < n_seg && s1 - s0 < seg_cap && first[s1 + 1] - first[s0] <= h->max_batch &&
+           (long long)(s1 + 1 - s0) * blk_per_seg <= h->max_batch)
+      ++s1;
+    chunks.push_back({s0, s1});
+    s0 = s1;
+  }
+  // Segment pairs: the FC rows of a chunk are its alt windows sorted by the SNV's position in
+  // the window, then the other windows.  The ref FC1 runs in that order, and the alt FC1 over
+  // the first rows recomputes only the split-K slabs its changed conv6 rows touch (a 256-row
+  // tile then holds windows with nearly the same changed rows), reusing the ref partials.
+  std::vector<int> fc_perm;
+  if (pr) {
+    fc_perm.resize((size_t)strands * n_win);
+    std::vector<char> is_alt(n_win, 0);
+    for (int w : alt_w) is_alt[w] = 1;
+    for (int sd = 0; sd < strands; ++sd) {
+      const bool rcs = (mode == EXPECTO_STRAND_RC) || sd == 1;
+      int* out = fc_perm.data() + (size_t)sd * n_win;
+      for (const auto& c : chunks) {
+        const int w0 = first[c.first], w1 = first[c.second];
+        int k = w0;
+        std::vector<int> a;
+        for (int w = w0; w < w1; ++w)
+          if (is_alt[w]) a.push_back(w);
+        std::stable_sort(a.begin(), a.end(), [&](int x, int y) {
+          const int px = pr->var_pos[win_seg[x]] - win_off[x], py = pr->var_pos[win_seg[y]] - win_off[y];
+          return rcs ? px > py : px < py;
+        });
+        for (int w : a) out[k++] = w;
+        for (int w = w0; w < w1; ++w)
+          if (!is_alt[w]) out[k++] = w;
+      }
+    }
+    EXPECTO_HIP_CHECK(hipMemcpyAsync(h->fc_perm_d, fc_perm.data(), fc_perm.size() * sizeof(int),
+                                     hipMemcpyHostToDevice, st));
+  }
+  // the tables are caller-owned pageable host memory: finish the copies before returning
+  EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
   const long long strand_rows = pr ? pr->strand_stride : n_win;
   const int eb = act_bytes();
   const SegDims gd{L, g.T1, g.P1, g.T3, g.T4, g.S5, g.T5, g.T6};
   const int4 ph4 = make_int4(ph[0], ph[1], ph[2], ph[3]);
   for (int sd = 0; sd < strands; ++sd) {
     const bool is_rc = (mode == EXPECTO_STRAND_RC) || sd == 1;
-    for (int s0 = 0; s0 < n_seg;) {
-      // grow the chunk while the segment buffers, the FC workspace (<= max_batch windows) and
-      // the alt-run buffers (<= max_batch blocks) fit
-      int s1 = s0 + 1;
-      while (s1 < n_seg && s1 - s0 < seg_cap && first[s1 + 1] - first[s0] <= h->max_batch &&
-             (long long)(s1 + 1 - s0) * blk_per_seg <= h->max_batch)
-        ++s1;
+    for (const auto& chunk : chunks) {
+      const int s0 = chunk.first, s1 = chunk.second;
       const int w0 = first[s0], nw = first[s1] - first[s0];
       EXPECTO_REQUIRE(nw <= h->max_batch, "more windows in one segment than max_batch");
       const int ns = s1 - s0;
@@ -1095,8 +1159,9 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
       if (nw > 0) {
         const int4 phi = make_int4(ph_idx[0], ph_idx[1], ph_idx[2], ph_idx[3]);
         const long long row_base = (long long)sd * strand_rows;
+        const int* widx = pr ? h->fc_perm_d + (size_t)sd * n_win + w0 : nullptr;   // FC row order
         seg_a_rows<<<dim3((nw + 255) / 256), dim3(256), 0, st>>>(h->win_seg_d, h->win_off_d,
-                                                                 win_row ? h->win_row_d : nullptr, nullptr, w0, nw, s0,
+                                                                 win_row ? h->win_row_d : nullptr, widx, w0, nw, s0,
                                                                  is_rc ? 1 : 0, L, n_ph, phi, g.T6, row_base,
                                                                  h->a_rows, h->c_rows);
         if ((rc = check_launch("seg_a_rows"))) return rc;
@@ -1111,12 +1176,33 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
             seg_alt_blocks<<<dim3(g.T6, (unsigned)nb), dim3(64), 0, st>>>(h->P, h->D0, n_ph, g.T6, h->seg_tab,
                                                                          640 * eb / 16, h->Q);
             if ((rc = check_launch("seg_alt_blocks"))) return rc;
-            seg_a_rows<<<dim3((ia1 - ia0 + 255) / 256), dim3(256), 0, st>>>(
-                h->win_seg_d, h->win_off_d, win_row ? h->win_row_d : nullptr, h->alt_w_d + ia0, 0, ia1 - ia0, s0,
+            const int n_alt = ia1 - ia0;   // the first n_alt FC rows of the chunk (widx)
+            seg_a_rows<<<dim3((n_alt + 255) / 256), dim3(256), 0, st>>>(
+                h->win_seg_d, h->win_off_d, win_row ? h->win_row_d : nullptr, widx, 0, n_alt, s0,
                 is_rc ? 1 : 0, L, n_ph, phi, g.T6, row_base, h->a_rows, h->c_rows);
             if ((rc = check_launch("seg_a_rows"))) return rc;
+            const unsigned* mask = nullptr;
+            double frac = 1.0;
+            if (planes_gemm()) {
+              const int tiles = (int)((n_alt + gemm_bm() - 1) / gemm_bm());
+              unsigned* md = reinterpret_cast<unsigned*>(h->slab_mask);
+              EXPECTO_HIP_CHECK(hipMemsetAsync(md, 0, tiles * sizeof(unsigned), st));
+              fc1_slab_mask_seg<<<dim3((n_alt + 255) / 256), dim3(256), 0, st>>>(
+                  widx, n_alt, h->win_seg_d, h->win_off_d, s0, is_rc ? 1 : 0, L, phi, h->seg_tab, (int)gemm_bm(),
+                  kFc1In / h->fc_splits, md);
+              if ((rc = check_launch("fc1_slab_mask_seg"))) return rc;
+              mask = md;
+              if (h->profiling) {   // executed share of the slabs, for the MAC count
+                std::vector<unsigned> hm(tiles);
+                EXPECTO_HIP_CHECK(hipMemcpyAsync(hm.data(), md, tiles * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+                EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
+                int bits = 0;
+                for (unsigned x : hm) bits += __builtin_popcount(x);
+                frac = (double)bits / (tiles * h->fc_splits);
+              }
+            }
             DeltaScope ds(h);
-            if ((rc = run_fc(h, h->Q, h->a_rows, ia1 - ia0, pr->y_alt, st, h->c_rows))) return rc;
+            if ((rc = run_fc(h, h->Q, h->a_rows, n_alt, pr->y_alt, st, h->c_rows, mask, frac, nw))) return rc;
           }
           if (ic1 > ic0) {
             copy_rows<<<dim3(ic1 - ic0), dim3(256), 0, st>>>(y, pr->y_alt, h->copy_w_d + ic0,
@@ -1125,7 +1211,6 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
           }
         }
       }
-      s0 = s1;
     }
   }
   return EXPECTO_OK;
@@ -1421,6 +1506,7 @@ void expecto_beluga_destroy(expecto_beluga_t h) {
   if (h->win_seg_d) (void)hipFree(h->win_seg_d);
   if (h->alt_w_d) (void)hipFree(h->alt_w_d);
   if (h->copy_w_d) (void)hipFree(h->copy_w_d);
+  if (h->fc_perm_d) (void)hipFree(h->fc_perm_d);
   if (h->seg_var_d) (void)hipFree(h->seg_var_d);
   if (h->win_off_d) (void)hipFree(h->win_off_d);
   if (h->win_row_d) (void)hipFree(h->win_row_d);
