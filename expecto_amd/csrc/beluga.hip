@@ -593,7 +593,7 @@ struct expecto_beluga {
   int* win_row_d = nullptr;
   int* fc_perm_d = nullptr;      // segment pairs: FC row order per strand (2 x win_cap)
   hipStream_t st2 = nullptr;     // pair path: alt-delta launches overlap the ref launches
-  hipEvent_t pev[12] = {};       //   (ordering events, no timing)
+  hipEvent_t pev[16] = {};       //   (ordering events, no timing)
   bool overlap = true;           //   EXPECTO_OVERLAP=0: one stream (same bits either way)
   float* DA = nullptr;           // alt-delta buffers (pair path), lazily allocated:
   float* D0 = nullptr;           //   DA = assembled input patch, D0/D1 = alternating W_l-row runs
@@ -1094,6 +1094,7 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
   EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
   const long long strand_rows = pr ? pr->strand_stride : n_win;
   const int eb = act_bytes();
+  hipStream_t sa = (pr && h->st2) ? h->st2 : st;     // alt runs of segment pairs
   const SegDims gd{L, g.T1, g.P1, g.T3, g.T4, g.S5, g.T5, g.T6};
   const int4 ph4 = make_int4(ph[0], ph[1], ph[2], ph[3]);
   for (int sd = 0; sd < strands; ++sd) {
@@ -1104,58 +1105,90 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
       EXPECTO_REQUIRE(nw <= h->max_batch, "more windows in one segment than max_batch");
       const int ns = s1 - s0;
       const long long nb = (long long)ns * n_ph;
-      // alt input patch of a layer from the ref input `ref` (ref_rows per block) and the
-      // previous alt run, then the layer's GEMM on it (same kernel, K order and weights)
-      auto alt_layer = [&](int l, const float* ref, int ref_rows, const float* dprev, int wprev, int nbk, int ib,
-                           int mult, int irp, int arows, int w, bool pool, float* dnext) -> int {
+      // Alt runs (segment pairs) on the handle's second stream `sa`: the alt input patch of
+      // layer l is assembled from the ref input of layer l (`ref`, ref_rows per block; the
+      // ref layer l reads it concurrently) and the previous alt run, then the layer's GEMM runs
+      // on it beside the next ref layers.  The ref launch that next overwrites `ref` (ping-
+      // pong) waits for the assembly (event `done`).  Same kernels, K order and weights.
+      auto alt_asm = [&](int l, const float* ref, int ref_rows, const float* dprev, int wprev, int nbk, int ib,
+                         int mult, int irp, int arows, hipEvent_t ready, hipEvent_t done) -> int {
+        if (sa != st) {
+          EXPECTO_HIP_CHECK(hipEventRecord(ready, st));
+          EXPECTO_HIP_CHECK(hipStreamWaitEvent(sa, ready, 0));
+        }
         const int row16 = kConv[l].cin * eb / 16;
-        seg_delta_assemble<<<dim3(ns * nbk), dim3(256), 0, st>>>(ref, ref_rows, dprev, wprev, h->seg_tab, nbk,
+        seg_delta_assemble<<<dim3(ns * nbk), dim3(256), 0, sa>>>(ref, ref_rows, dprev, wprev, h->seg_tab, nbk,
                                                                       ib, mult, irp, arows, row16, h->DA);
         int r = check_launch("seg_delta_assemble");
-        DeltaScope ds(h);
-        return r ? r : run_conv(h, l, h->DA, dnext, (long long)ns * nbk, arows, w, w, pool, st);
+        if (!r && sa != st) EXPECTO_HIP_CHECK(hipEventRecord(done, sa));
+        return r;
       };
+      auto alt_gemm = [&](int l, int nbk, int arows, int w, bool pool, float* dnext) -> int {
+        DeltaScope ds(h);
+        return run_conv(h, l, h->DA, dnext, (long long)ns * nbk, arows, w, w, pool, sa);
+      };
+      auto st_wait = [&](hipEvent_t e) -> int {   // st: the alt work recorded in e is done
+        if (sa != st) EXPECTO_HIP_CHECK(hipStreamWaitEvent(st, e, 0));
+        return EXPECTO_OK;
+      };
+      if (pr && sa != st) {   // sa: the previous chunk's use of the alt buffers on st is done
+        EXPECTO_HIP_CHECK(hipEventRecord(h->pev[0], st));
+        EXPECTO_HIP_CHECK(hipStreamWaitEvent(sa, h->pev[0], 0));
+      }
       // conv1 from codes: virtual rows = segments; rc mode mirrors inside the kernel
       if ((rc = run_conv1(h, nullptr, codes + (long long)s0 * code_stride, code_stride, ns,
                           is_rc ? EXPECTO_STRAND_RC : EXPECTO_STRAND_FWD, 0, ns, L, g.S1, st)))
         return rc;
       if (pr) {
-        seg_delta_table<<<dim3((ns + 255) / 256), dim3(256), 0, st>>>(h->seg_var_d, s0, ns, is_rc ? 1 : 0, gd, n_ph,
+        seg_delta_table<<<dim3((ns + 255) / 256), dim3(256), 0, sa>>>(h->seg_var_d, s0, ns, is_rc ? 1 : 0, gd, n_ph,
                                                                      ph4, h->seg_tab);
         if ((rc = check_launch("seg_delta_table"))) return rc;
-        seg_delta_codes<<<dim3((ns + 15) / 16), dim3(256), 0, st>>>(codes, code_stride, pr->alt_code, s0, ns,
+        seg_delta_codes<<<dim3((ns + 15) / 16), dim3(256), 0, sa>>>(codes, code_stride, pr->alt_code, s0, ns,
                                                                    is_rc ? 1 : 0, L, h->seg_tab, h->delta_codes);
         if ((rc = check_launch("seg_delta_codes"))) return rc;
         DeltaScope ds(h);
-        if ((rc = run_conv1(h, nullptr, h->delta_codes, 16, ns, EXPECTO_STRAND_FWD, 0, ns, kDA[1], kDW[1], st,
+        if ((rc = run_conv1(h, nullptr, h->delta_codes, 16, ns, EXPECTO_STRAND_FWD, 0, ns, kDA[1], kDW[1], sa,
                             h->D0)))
           return rc;
       }
       // conv2 + pool1 (P -> Q), conv3 (Q -> P), conv4 unpooled (P -> Q); alt runs D0 <-> D1
+      if (pr && (rc = alt_asm(0, h->P, g.S1, h->D0, kDW[1], 1, 2, 4, 1, kDA[2], h->pev[1], h->pev[2]))) return rc;
       if ((rc = run_conv(h, 0, h->P, h->Q, ns, g.S1, g.P1, g.P1, true, st))) return rc;
-      if (pr && (rc = alt_layer(0, h->P, g.S1, h->D0, kDW[1], 1, 2, 4, 1, kDA[2], kDW[2], true, h->D1))) return rc;
+      if (pr && ((rc = st_wait(h->pev[2])) || (rc = alt_gemm(0, 1, kDA[2], kDW[2], true, h->D1)))) return rc;
+      if (pr && (rc = alt_asm(1, h->Q, g.P1, h->D1, kDW[2], 1, 3, 1, 2, kDA[3], h->pev[3], h->pev[4]))) return rc;
       if ((rc = run_conv(h, 1, h->Q, h->P, ns, g.P1, g.T3, g.T3, false, st))) return rc;
-      if (pr && (rc = alt_layer(1, h->Q, g.P1, h->D1, kDW[2], 1, 3, 1, 2, kDA[3], kDW[3], false, h->D0))) return rc;
+      if (pr && ((rc = st_wait(h->pev[4])) || (rc = alt_gemm(1, 1, kDA[3], kDW[3], false, h->D0)))) return rc;
+      if (pr && (rc = alt_asm(2, h->P, g.T3, h->D0, kDW[3], 1, 4, 1, 3, kA4u, h->pev[5], h->pev[6]))) return rc;
       if ((rc = run_conv(h, 2, h->P, h->Q, ns, g.T3, g.T4, g.T4, false, st))) return rc;
-      if (pr && (rc = alt_layer(2, h->P, g.T3, h->D0, kDW[3], 1, 4, 1, 3, kA4u, kW4u, false, h->D1))) return rc;
+      if (pr && ((rc = st_wait(h->pev[6])) || (rc = alt_gemm(2, 1, kA4u, kW4u, false, h->D1)))) return rc;
       {  // pool2 phases (Q -> P)
         LayerTimer lt(h, 3, st);
         dim3 grid(g.S5, ns * n_ph);
         pool4_phases<<<grid, dim3(480), 0, st>>>(h->Q, ns, g.T4, g.T4, 480, n_ph, ph4, g.S5, h->P, act_fmt());
         if ((rc = check_launch("pool4_phases"))) return rc;
-        if (pr) {
-          seg_delta_pool<<<dim3(kDW[4], (unsigned)nb), dim3(480), 0, st>>>(h->Q, g.T4, h->D1, n_ph, ph4, h->seg_tab,
-                                                                           act_fmt(), h->D0);
-          if ((rc = check_launch("seg_delta_pool"))) return rc;
+      }
+      if (pr) {   // alt pool2 phases from the unpooled conv4 rows (Q) and the alt conv4 run
+        if (sa != st) {
+          EXPECTO_HIP_CHECK(hipEventRecord(h->pev[7], st));
+          EXPECTO_HIP_CHECK(hipStreamWaitEvent(sa, h->pev[7], 0));
         }
+        seg_delta_pool<<<dim3(kDW[4], (unsigned)nb), dim3(480), 0, sa>>>(h->Q, g.T4, h->D1, n_ph, ph4, h->seg_tab,
+                                                                         act_fmt(), h->D0);
+        if ((rc = check_launch("seg_delta_pool"))) return rc;
+        if (sa != st) EXPECTO_HIP_CHECK(hipEventRecord(h->pev[8], sa));
+        if ((rc = alt_asm(3, h->P, g.S5, h->D0, kDW[4], n_ph, 9, 1, 5, kDA[5], h->pev[9], h->pev[10]))) return rc;
+        if ((rc = st_wait(h->pev[8]))) return rc;    // conv5 overwrites Q
       }
       // conv5 (P -> Q), conv6 (Q -> P) over (segment, phase) blocks
       if ((rc = run_conv(h, 3, h->P, h->Q, nb, g.S5, g.T5, g.T5, false, st))) return rc;
-      if (pr && (rc = alt_layer(3, h->P, g.S5, h->D0, kDW[4], n_ph, 9, 1, 5, kDA[5], kDW[5], false, h->D1)))
+      if (pr && ((rc = st_wait(h->pev[10])) || (rc = alt_gemm(3, n_ph, kDA[5], kDW[5], false, h->D1)))) return rc;
+      if (pr && (rc = alt_asm(4, h->Q, g.T5, h->D1, kDW[5], n_ph, 13, 1, 9, kDA[6], h->pev[11], h->pev[12])))
         return rc;
       if ((rc = run_conv(h, 4, h->Q, h->P, nb, g.T5, g.T6, g.T6, false, st))) return rc;
-      if (pr && (rc = alt_layer(4, h->Q, g.T5, h->D1, kDW[5], n_ph, 13, 1, 9, kDA[6], kDW[6], false, h->D0)))
-        return rc;
+      if (pr) {
+        if ((rc = alt_gemm(4, n_ph, kDA[6], kDW[6], false, h->D0))) return rc;
+        if (sa != st) EXPECTO_HIP_CHECK(hipEventRecord(h->pev[13], sa));   // all alt runs of the chunk
+      }
       if (nw > 0) {
         const int4 phi = make_int4(ph_idx[0], ph_idx[1], ph_idx[2], ph_idx[3]);
         const long long row_base = (long long)sd * strand_rows;
@@ -1172,6 +1205,7 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
           const int ia1 = (int)(std::lower_bound(alt_w.begin(), alt_w.end(), w0 + nw) - alt_w.begin());
           const int ic0 = (int)(std::lower_bound(copy_w.begin(), copy_w.end(), w0) - copy_w.begin());
           const int ic1 = (int)(std::lower_bound(copy_w.begin(), copy_w.end(), w0 + nw) - copy_w.begin());
+          if ((rc = st_wait(h->pev[13]))) return rc;   // alt conv6 runs (and the Q reads of their patches)
           if (ia1 > ia0) {  // alt conv6 blocks into Q (conv5 rows are dead), then their FC
             seg_alt_blocks<<<dim3(g.T6, (unsigned)nb), dim3(64), 0, st>>>(h->P, h->D0, n_ph, g.T6, h->seg_tab,
                                                                          640 * eb / 16, h->Q);
@@ -1211,6 +1245,7 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
           }
         }
       }
+      if (pr && (rc = st_wait(h->pev[13]))) return rc;   // every alt run of the chunk joined
     }
   }
   return EXPECTO_OK;
