@@ -46,7 +46,7 @@ LAYER_MACS = {
     "fc1": 67840 * 2003, "fc1_reduce": 0, "fc2": 2003 * 2002,
 }
 GEMM_LAYER_EPI = {"conv2": (2, 1), "conv3": (3, 0), "conv4": (4, 1), "conv5": (5, 0), "conv6": (6, 0),
-                  "fc1": (7, 3), "fc2": (8, 2)}
+                  "fc1": (7, 3), "fc2": (8, 3)}
 
 
 DTYPES = {

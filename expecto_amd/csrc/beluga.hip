@@ -122,6 +122,21 @@ __global__ void fc1_reduce(const float* __restrict__ part, int splits, long long
   store_act_rt(fmt, h1, row, kHidLd, n, v, osc, ovf);
 }
 
+// FC2 output: y[c_rows[m] or m][n] = sigmoid(sum_k part[k][m][n] * col_scale[n] + bias[n]) (Beluga.py:46-48)
+__global__ void fc2_reduce(const float* __restrict__ part, int splits, long long split_stride, int M,
+                           const float* __restrict__ bias, const float* __restrict__ col_scale,
+                           const long long* __restrict__ c_rows, float* __restrict__ y) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)M * kNFeat) return;
+  const int m = (int)(i / kNFeat), n = (int)(i - (long long)m * kNFeat);
+  const long long src = (long long)m * kHidLd + n;
+  float s = 0.f;
+  for (int k = 0; k < splits; ++k) s += part[k * split_stride + src];
+  if (col_scale) s *= col_scale[n];   // f16x3: exact power-of-2 unscaling of the split-K sum
+  const float v = s + bias[n];
+  y[(c_rows ? c_rows[m] : m) * kNFeat + n] = 1.0f / (1.0f + expf(-v));
+}
+
 // MaxPool(1,4) floor mode at pool phases p (segment path, SURVEY.md 5 "trunk sharing"):
 // out[(seg*n_ph + i)*s_out + g][c] = max_{j<4} in[seg*s_in + ph[i] + 4g + j][c],
 // g < (t_in - ph[i]) / 4.  ReLU was applied by the producing conv (Beluga.py:32-34 order).
@@ -548,6 +563,8 @@ constexpr ConvGeo kConv[5] = {
 // FC1 split-K: a fixed number of slabs per handle (default 20 of 3392; a divisor of
 // 67840/32 = 2120 K blocks), whatever the batch, so an FC1 output never depends on how many
 // windows shared the launch.
+constexpr int kFc2Splits = 7;          // FC2 K = 63 blocks of 32 -> 7 slabs of 9: a 2000-row FC2 fills
+                                        // 728 workgroups instead of 104 (fixed: sums never depend on M)
 constexpr int kFcSplitsDefault = 20;   // 2080 workgroups for 2000 rows: 8.1 rounds of 256 CUs (10: 4.1)
 }  // namespace
 
@@ -581,6 +598,7 @@ struct expecto_beluga {
   float* P = nullptr;
   float* Q = nullptr;
   float* part = nullptr;
+  float* part2 = nullptr;        // FC2 split-K partials (kFc2Splits slabs; FC1's stay in `part`)
   float* h1 = nullptr;
   long long* a_rows = nullptr;  // FC1 row table (segment path), max_batch entries
   long long* c_rows = nullptr;  // FC2 output-row table (segment path), max_batch entries
@@ -876,22 +894,22 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     a.Bp = g_precision == EXPECTO_PRECISION_F16X3 ? h->wh[6] : h->fc2p;
     a.col_scale = g_precision == EXPECTO_PRECISION_F16X3 ? h->cs[6] : nullptr;
     a.ldb = kHidLd;
-    a.kper = kHidLd;
+    a.kper = kHidLd / kFc2Splits;
     a.taps = 1;
     a.n_tiles = npad_of(kNFeat) / GBN;
     a.m_tiles = m_tiles;
     a.m_fastest = 1;
-    a.bias = h->fc2b;
-    a.c_rows = c_rows;
-    a.C = y;
-    a.ldc = kNFeat;
+    a.C = h->part2;
+    a.ldc = kHidLd;
     a.n_store = kNFeat;
-    a.s_in = 1;
-    a.t_valid = 1;
-    a.s_out = 1;
+    a.split_stride = (long long)nb * kHidLd;
     LayerTimer lt(h, 8, st);
     if (h->profiling) h->macs[h->timer_base + 8] += (double)nb * kNFeat * kFc1Out;
-    if ((rc = launch_gemm<8, EPI_SIGMOID>(a, 1, st))) return rc;
+    if ((rc = launch_gemm<8, EPI_PARTIAL>(a, kFc2Splits, st))) return rc;
+    const long long count = (long long)nb * kNFeat;
+    fc2_reduce<<<dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st>>>(
+        h->part2, kFc2Splits, (long long)nb * kHidLd, nb, h->fc2b, a.col_scale, c_rows, y);
+    if ((rc = check_launch("fc2_reduce"))) return rc;
   }
   return EXPECTO_OK;
 }
@@ -1518,7 +1536,8 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   }
   const size_t partf = (size_t)h->fc_splits * max_batch * kHidLd;
   if ((rc = dalloc(h, &h->P, act_alloc(pf))) || (rc = dalloc(h, &h->Q, act_alloc(qf))) ||
-      (rc = dalloc(h, &h->part, partf)) || (rc = dalloc(h, &h->h1, act_alloc((size_t)max_batch * kHidLd))))
+      (rc = dalloc(h, &h->part, partf)) || (rc = dalloc(h, &h->h1, act_alloc((size_t)max_batch * kHidLd))) ||
+      (rc = dalloc(h, &h->part2, (size_t)kFc2Splits * max_batch * kHidLd)))
     return fail(rc);
   {
     float* rows = nullptr;
