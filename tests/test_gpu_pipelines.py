@@ -230,3 +230,43 @@ def test_segment_pairs_alt_runs_are_bitwise_equal(precision):
         want = eng.forward_codes(wins, 2).view(2, S * n, 2002)
         d = (y[:, a] - want).abs().amax(-1).view(2, S, n).cpu().numpy()
         assert (d == 0).all(), f"allele {a}: strand x offset x variant max|diff| {d} (q={q}, offsets={offs})"
+
+
+def test_second_stream_overlap_is_bitwise_equal(monkeypatch):
+    """The alt-delta launches on the handle's second stream (pair and segment-pair paths,
+    EXPECTO_OVERLAP=1, the default) give exactly the single-stream results, on batches large
+    enough that the ref launches run many rounds beside them."""
+    import math
+    import torch
+    from expecto_amd import beluga
+    rng = np.random.default_rng(21)
+    n = 1200
+    pos = rng.integers(0, 2000, n).astype(np.int32)
+    ref = torch.from_numpy(rng.integers(0, 5, (n, 2000)).astype(np.uint8)).cuda()
+    alt = ref.clone()
+    newb = torch.from_numpy(((ref.cpu().numpy()[np.arange(n), pos] + 1) % 4).astype(np.uint8)).cuda()
+    alt[torch.arange(n), torch.from_numpy(pos).long()] = newb
+    L, ns = 3600, 150
+    q = rng.integers(0, L, ns).astype(np.int32)
+    seg = torch.from_numpy(rng.integers(0, 5, (ns, L)).astype(np.uint8)).cuda()
+    alt_code = torch.from_numpy(((seg.cpu().numpy()[np.arange(ns), q] + 2) % 4).astype(np.uint8)).cuda()
+    offs = np.arange(0, 1601, 200, dtype=np.int32)
+    v_i, j_i = np.meshgrid(np.arange(ns), np.arange(offs.size), indexing="ij")
+    win_seg, win_off = v_i.ravel().astype(np.int32), offs[j_i.ravel()]
+    win_row = (j_i * ns + v_i).ravel().astype(np.int32)
+    W = win_seg.size
+    out = {}
+    for ov in ("0", "1"):
+        monkeypatch.setenv("EXPECTO_OVERLAP", ov)
+        eng = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=2400).cuda().engine()
+        y = torch.empty((2, 2, n, 2002), device="cuda")
+        yv = y.view(4 * n, 2002)
+        eng.forward_pairs(ref, alt, pos, yv[0:], yv[n:], 2 * n, 2)
+        ys = torch.empty((2, 2, W, 2002), device="cuda")
+        yf = ys.view(4 * W, 2002)
+        eng.forward_segment_pairs(seg, L, q, alt_code, win_seg, win_off, win_row, yf[0:], yf[W:], 2 * W)
+        torch.cuda.synchronize()
+        out[ov] = (y.cpu(), ys.cpu())
+        del eng
+    assert torch.equal(out["0"][0], out["1"][0])
+    assert torch.equal(out["0"][1], out["1"][1])
