@@ -36,6 +36,7 @@ FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 
 # bf16 dense MFMA peak: 256 CU x 4 SIMD x 1024 FLOP/clk (v_mfma_f32_32x32x16_bf16: 32768 FLOP
 # per 32 cycles) x 2.4 GHz = 2516.6 TFLOP/s (MI355X_MICROARCH.md "~2.5 PF dense")
 BF16_MFMA_PEAK_TFLOPS = 256 * 4 * 1024 * 2.4e9 / 1e12
+HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 BF16X6_PRODUCTS = 6               # bf16 MFMA products per fp32 multiply-add in the bf16x6 kernel
 F16X3_PRODUCTS = 3                # fp16 MFMA products per multiply-add in the f16x3 kernel (fp16 peak = bf16 peak)
 
@@ -94,6 +95,53 @@ def cpu_baseline(sd_cpu, codes: np.ndarray, seconds: float, threads: int, window
             "windows_per_s": wps,
             "sample": f"{done} windows of the same workload (seeded SNV ref windows), batch 32, "
                       f"oracle/beluga_np.forward_torch_cpu (torch CPU fp32, oneDNN), {el:.1f} s"}
+
+
+def hbm_reductions(dev):
+    """The metric's "HBM GB/s vs peak": the HBM-bound spatial reductions timed
+    with HIP events on synthetic inputs resident in HBM; algorithmic bytes = every input read
+    once + every output written once.
+      TSS (compute_expecto_features.py:91-124): 1000 genes x 200 shifts x 2002, fwd + rc fp32 ->
+        [1000, 20020] fp64 (3.2 MB read + 160 KB written per gene);
+      variant (predict.py:87-136): 20000 variants x 9 shifts x 2002 fp32 -> [20000, 20020] fp64
+        (write-dominated: "fp64_fill_ceiling" times torch's zero_ of the same output, the
+        practical write rate on this box)."""
+    from expecto_amd import features
+    g = torch.Generator(device=dev).manual_seed(3)
+    res = {}
+    G, S, F = 1000, 200, 2002
+    fwd = torch.rand((G, S, F), device=dev, generator=g)
+    rc = torch.rand((G, S, F), device=dev, generator=g)
+    w = torch.from_numpy(features.tss_pos_weights()).to(dev)
+    out = torch.empty((G, 10 * F), dtype=torch.float64, device=dev)
+    n_var, S9 = 20000, 9
+    eff = torch.rand((S9, n_var, F), device=dev, generator=g)
+    rng = np.random.default_rng(4)
+    dist = rng.integers(-20000, 20000, n_var)
+    plus = rng.integers(0, 2, n_var).astype(bool)
+    from expecto_amd.pipeline import shift_order
+    sh = shift_order(800)
+    vout = torch.empty((n_var, 10 * F), dtype=torch.float64, device=dev)
+    for name, fn, nbytes in (
+            ("fp64_fill_ceiling", lambda: vout.zero_(), n_var * 10 * F * 8),   # write-only reference
+            ("tss_reduce", lambda: features.tss_reduce(fwd, rc, w, out), 2 * G * S * F * 4 + G * 10 * F * 8),
+            ("variant_reduce", lambda: features.variant_features(eff, dist, plus, sh, vout),
+             S9 * n_var * F * 4 + n_var * 10 * F * 8)):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 5
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        res[name] = {"ms": ms, "bytes": nbytes, "GB_per_s": gbs, "peak_GB_per_s": HBM_PEAK_GBS,
+                     "frac": gbs / HBM_PEAK_GBS}
+    del fwd, rc, eff, out, vout
+    torch.cuda.empty_cache()
+    return res
 
 
 def make_variants(genome, n, seed):
@@ -286,6 +334,7 @@ def main():
             alt_prec[prec] = {"variants_per_s": n * 3 / elp, "ms_per_step": elp / 3 * 1e3,
                               "dominant": {k: rp[k] for k in ("kernel", "layer", "achieved", "peak", "frac")}}
         extras["headline_other_precisions"] = alt_prec
+        extras["hbm_reductions"] = hbm_reductions(dev)
         rec["extra_workloads"] = extras
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from expecto_amd.encode import seqs_to_codes

@@ -167,6 +167,48 @@ __global__ void tss_reduce_kernel(const float* __restrict__ fwd, const float* __
   for (int k = 0; k < 10; ++k) o[(long long)k * nfeat] = acc[k];
 }
 
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+// Streaming 16-byte store: outputs are written once and never re-read by the kernel.
+__device__ __forceinline__ void store_nt2(double* p, double a, double b) {
+  f64x2 v = {a, b};
+  __builtin_nontemporal_store(v, reinterpret_cast<f64x2*>(p));
+}
+
+// The same with 2 features per thread (nfeat even, 8-byte aligned inputs, 16-byte aligned
+// output): float2 loads and double2 stores, so each wave moves 512 B per load instruction and
+// 1 KB per store, and half as many workgroups redo the per-gene weight staging.  Per output the
+// same shift-sequential products and sums: bitwise equal to tss_reduce_kernel.
+__global__ void tss_reduce2_kernel(const float* __restrict__ fwd, const float* __restrict__ rc,
+                                   const double* __restrict__ weights, int n_shift, int nfeat,
+                                   double* __restrict__ out) {
+  extern __shared__ double wsh[];  // [10][n_shift]
+  for (int i = threadIdx.x; i < 10 * n_shift; i += blockDim.x) wsh[i] = weights[i];
+  __syncthreads();
+  const int f = 2 * (blockIdx.x * blockDim.x + threadIdx.x);
+  const long long g = blockIdx.y;
+  if (f >= nfeat) return;
+  double a0[10], a1[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) a0[k] = a1[k] = 0.0;
+  const long long h2 = nfeat / 2;
+  const float2* pf = reinterpret_cast<const float2*>(fwd + g * n_shift * nfeat + f);
+  const float2* pr = reinterpret_cast<const float2*>(rc + g * n_shift * nfeat + f);
+#pragma unroll 4
+  for (int s = 0; s < n_shift; ++s) {
+    const float2 x = pf[s * h2], y = pr[s * h2];
+    const double p0 = (double)(0.5f * (x.x + y.x)), p1 = (double)(0.5f * (x.y + y.y));  // f32 like numpy
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      const double w = wsh[k * n_shift + s];
+      a0[k] += w * p0;
+      a1[k] += w * p1;
+    }
+  }
+  double* o = out + g * 10LL * nfeat + f;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) store_nt2(o + (long long)k * nfeat, a0[k], a1[k]);
+}
+
 // grid: (ceil(nfeat/256), n); weights W_j[k] computed per variant in f64.
 __global__ void variant_reduce_kernel(const float* __restrict__ eff, const long long* __restrict__ dist,
                                       const uint8_t* __restrict__ strand_plus, const int* __restrict__ shifts,
@@ -200,6 +242,46 @@ __global__ void variant_reduce_kernel(const float* __restrict__ eff, const long 
   double* o = out + v * 10LL * nfeat + f;
 #pragma unroll
   for (int k = 0; k < 10; ++k) o[(long long)k * nfeat] = acc[k];
+}
+
+// 2 features per thread (as tss_reduce2_kernel): 4 instead of 8 workgroups per variant compute
+// the 9 x 10 weights, float2 loads and double2 stores; bitwise equal to variant_reduce_kernel.
+__global__ void variant_reduce2_kernel(const float* __restrict__ eff, const long long* __restrict__ dist,
+                                       const uint8_t* __restrict__ strand_plus, const int* __restrict__ shifts,
+                                       int n_shift, int n, int nfeat, double* __restrict__ out) {
+  __shared__ double wsh[32 * 10];
+  const long long v = blockIdx.y;
+  const double decay[5] = {0.01, 0.02, 0.05, 0.1, 0.2};
+  if ((int)threadIdx.x < n_shift) {
+    const int j = threadIdx.x;
+    const long long sgn = strand_plus[v] ? 1 : -1;
+    const long long d = dist[v] * sgn + (long long)shifts[j] * sgn;
+    const double fl = floor(fabs((double)d) / 200.0);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const double e = exp(-decay[k] * fl);
+      wsh[j * 10 + k] = d <= 0 ? e : 0.0;
+      wsh[j * 10 + 5 + k] = d >= 0 ? e : 0.0;
+    }
+  }
+  __syncthreads();
+  const int f = 2 * (blockIdx.x * blockDim.x + threadIdx.x);
+  if (f >= nfeat) return;
+  double a0[10], a1[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) a0[k] = a1[k] = 0.0;
+  for (int j = 0; j < n_shift; ++j) {
+    const float2 e2 = *reinterpret_cast<const float2*>(eff + ((long long)j * n + v) * nfeat + f);
+    const double e0 = (double)e2.x, e1 = (double)e2.y;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      a0[k] += e0 * wsh[j * 10 + k];
+      a1[k] += e1 * wsh[j * 10 + k];
+    }
+  }
+  double* o = out + v * 10LL * nfeat + f;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) store_nt2(o + (long long)k * nfeat, a0[k], a1[k]);
 }
 
 }  // namespace expecto
@@ -315,9 +397,17 @@ int expecto_tss_reduce(const float* fwd, const float* rc, const double* weights,
   if (n_genes == 0) return EXPECTO_OK;
   EXPECTO_REQUIRE(n_genes <= 65535, "at most 65535 genes per call");
   EXPECTO_REQUIRE(fwd && rc && weights && out, "null argument");
-  dim3 grid((nfeat + 255) / 256, n_genes);
-  tss_reduce_kernel<<<grid, dim3(256), 10 * n_shift * sizeof(double), as_stream(stream)>>>(fwd, rc, weights, n_shift,
-                                                                                          nfeat, out);
+  const bool v2 = nfeat % 2 == 0 && ((reinterpret_cast<uintptr_t>(fwd) | reinterpret_cast<uintptr_t>(rc)) & 7) == 0 &&
+                  (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+  if (v2) {
+    dim3 grid((nfeat / 2 + 255) / 256, n_genes);
+    tss_reduce2_kernel<<<grid, dim3(256), 10 * n_shift * sizeof(double), as_stream(stream)>>>(fwd, rc, weights,
+                                                                                             n_shift, nfeat, out);
+  } else {
+    dim3 grid((nfeat + 255) / 256, n_genes);
+    tss_reduce_kernel<<<grid, dim3(256), 10 * n_shift * sizeof(double), as_stream(stream)>>>(fwd, rc, weights, n_shift,
+                                                                                            nfeat, out);
+  }
   return check_launch("tss_reduce");
 }
 
@@ -327,9 +417,15 @@ int expecto_variant_reduce(const float* effects, const long long* dist, const ui
   if (n == 0) return EXPECTO_OK;
   EXPECTO_REQUIRE(n <= 65535, "at most 65535 variants per call");
   EXPECTO_REQUIRE(effects && dist && strand_plus && shifts && out, "null argument");
-  dim3 grid((nfeat + 255) / 256, n);
-  variant_reduce_kernel<<<grid, dim3(256), 0, as_stream(stream)>>>(effects, dist, strand_plus, shifts, n_shift, n,
-                                                                   nfeat, out);
+  if (nfeat % 2 == 0 && (reinterpret_cast<uintptr_t>(effects) & 7) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+    dim3 grid((nfeat / 2 + 255) / 256, n);
+    variant_reduce2_kernel<<<grid, dim3(256), 0, as_stream(stream)>>>(effects, dist, strand_plus, shifts, n_shift, n,
+                                                                      nfeat, out);
+  } else {
+    dim3 grid((nfeat + 255) / 256, n);
+    variant_reduce_kernel<<<grid, dim3(256), 0, as_stream(stream)>>>(effects, dist, strand_plus, shifts, n_shift, n,
+                                                                     nfeat, out);
+  }
   return check_launch("variant_reduce");
 }
 
