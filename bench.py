@@ -152,6 +152,36 @@ def hbm_reductions(dev):
     return res
 
 
+def time_final_gather(S, n, dev, rank, world):
+    """configs[3]'s exchange step, outside the timed steps: one step's outputs of every rank
+    (y [2, 2, S, n, 2002] and diff [2, S, n, 2002] fp32) gathered to rank 0 per shift, as the
+    chromatin CLI does before rank 0 writes the .diff.h5 files (RCCL gather over xGMI)."""
+    y = torch.rand((2, 2, S, n, 2002), device=dev)
+    d = torch.rand((2, S, n, 2002), device=dev)
+    total = world * n
+
+    def gather():
+        for j in range(S):
+            edist.gather_rows_to(y[:, :, j:j + 1], 3, total, world, rank)
+            edist.gather_rows_to(d[:, j:j + 1], 2, total, world, rank)
+
+    gather()                                   # warm the communicator
+    torch.cuda.synchronize()
+    torch.distributed.barrier()
+    t0 = time.perf_counter()
+    gather()
+    torch.cuda.synchronize()
+    torch.distributed.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if torch.distributed.get_backend() == "nccl":
+        el = el.to(dev)
+    torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+    nbytes = (world - 1) * (y.numel() + d.numel()) * 4        # bytes arriving at rank 0
+    ms = float(el.item()) * 1e3
+    return {"ms": ms, "bytes_into_rank0": nbytes, "GB_per_s": nbytes / (ms * 1e-3) / 1e9,
+            "what": "one step's y + diff of every rank to rank 0, per shift (not part of value)"}
+
+
 def make_variants(genome, n, seed):
     snvs = synthetic.snvs(genome, n, seed=seed)
     return VariantSet([v[0] for v in snvs], np.array([v[1] for v in snvs]), [v[2] for v in snvs],
@@ -353,6 +383,8 @@ def main():
         rec["cpu_baseline"] = cpu_baseline(sd_cpu, seqs_to_codes(sample), args.cpu_seconds,
                                            min(args.cpu_threads, os.cpu_count() or 1), 4 * S)
         rec["speedup_vs_cpu_baseline"] = value / rec["cpu_baseline"]["value"]
+    if world > 1:
+        rec["final_gather"] = time_final_gather(S, n, dev, rank, world)
     if rank == 0:
         print(json.dumps(rec))
     if world > 1:

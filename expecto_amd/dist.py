@@ -18,13 +18,14 @@ def env_rank():
 
 
 def init(backend: str | None = None):
-    """Initialise the process group when launched with WORLD_SIZE > 1; returns (rank, world, local)."""
+    """Initialise the process group when launched with WORLD_SIZE > 1; returns (rank, world, local).
+    Backend: the argument, else $EXPECTO_DIST_BACKEND, else "nccl" (RCCL) on a GPU, "gloo" on CPU."""
     import torch.distributed as dist
 
     rank, world, local = env_rank()
     if world > 1 and not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("EXPECTO_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
@@ -38,23 +39,51 @@ def shard_range(n: int, rank: int, world: int):
     return lo, lo + q + (1 if rank < r else 0)
 
 
-def gather_rows(t: torch.Tensor, dim: int, n_total: int, world: int):
-    """Gather the shards of `t` along `dim` (contiguous rank ranges of shard_range) to every rank.
-
-    Returns the full tensor (rank order = global order).  Uses one all_gather of
-    equally padded shards (RCCL ring over xGMI on the GPU)."""
-    import torch.distributed as dist
-
-    if world == 1:
-        return t
+def _padded(t: torch.Tensor, dim: int, n_total: int, world: int):
     x = t.movedim(dim, 0).contiguous()
     max_n = max(shard_range(n_total, r, world)[1] - shard_range(n_total, r, world)[0] for r in range(world))
+    if x.shape[0] == max_n:
+        return x
     pad = torch.zeros((max_n,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     pad[: x.shape[0]] = x
-    parts = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(parts, pad)
+    return pad
+
+
+def _unpad(parts, dim: int, n_total: int, world: int):
     pieces = []
     for r in range(world):
         lo, hi = shard_range(n_total, r, world)
         pieces.append(parts[r][: hi - lo])
     return torch.cat(pieces, 0).movedim(0, dim)
+
+
+def gather_rows(t: torch.Tensor, dim: int, n_total: int, world: int):
+    """Gather the shards of `t` along `dim` (contiguous rank ranges of shard_range) to every rank.
+
+    Returns the full tensor (rank order = global order).  One all_gather of equally padded
+    shards (RCCL ring over xGMI on the GPU)."""
+    import torch.distributed as dist
+
+    if world == 1:
+        return t
+    pad = _padded(t, dim, n_total, world)
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad)
+    return _unpad(parts, dim, n_total, world)
+
+
+def gather_rows_to(t: torch.Tensor, dim: int, n_total: int, world: int, rank: int, dst: int = 0):
+    """Gather the shards of `t` along `dim` to rank `dst` only (None on the other ranks).
+
+    The file-writing rank is the only one that needs the full tensor: one RCCL gather moves
+    each shard once over xGMI into `dst`, and no other rank allocates the full size."""
+    import torch.distributed as dist
+
+    if world == 1:
+        return t
+    pad = _padded(t, dim, n_total, world)
+    if pad.is_cuda and dist.get_backend() == "gloo":
+        pad = pad.cpu()       # gloo gathers host tensors only (CPU tests, one-GPU rehearsals)
+    parts = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
+    dist.gather(pad, parts, dst=dst)
+    return _unpad(parts, dim, n_total, world) if rank == dst else None

@@ -1,4 +1,4 @@
-"""CPU, world_size 2 over gloo: variant sharding and the gather to rank 0 (dist.py)."""
+"""CPU, world_size 2 over gloo: variant sharding, the all-gather and the gather to rank 0 (dist.py)."""
 import os
 import socket
 
@@ -25,7 +25,10 @@ def _worker(rank, world, port, n_total, q):
     v = torch.arange(lo, hi, dtype=torch.float32)
     y = v.view(1, 1, 1, -1, 1).expand(2, 2, 3, hi - lo, 5).contiguous() + torch.arange(5.0)
     full = edist.gather_rows(y, 3, n_total, w)
-    q.put((r, lo, hi, full.shape, bool(torch.equal(full[0, 1, 2, :, 0], torch.arange(n_total, dtype=torch.float32)))))
+    to0 = edist.gather_rows_to(y, 3, n_total, w, r)
+    ok_to0 = torch.equal(to0, full) if r == 0 else to0 is None
+    q.put((r, lo, hi, full.shape,
+           bool(torch.equal(full[0, 1, 2, :, 0], torch.arange(n_total, dtype=torch.float32))) and ok_to0))
     torch.distributed.destroy_process_group()
 
 

@@ -270,3 +270,39 @@ def test_second_stream_overlap_is_bitwise_equal(monkeypatch):
         del eng
     assert torch.equal(out["0"][0], out["1"][0])
     assert torch.equal(out["0"][1], out["1"][1])
+
+
+def test_chromatin_cli_two_ranks_equals_one(workdir):
+    """The CLI sharded over 2 ranks (torch.distributed.run; gloo, both ranks on this one GPU:
+    the 8-GPU RCCL run is the driver's) writes the same .diff.h5 files, bit for bit, as one
+    rank: shards are contiguous variant ranges and the per-shift gather to rank 0 restores
+    the global order."""
+    import socket
+    import subprocess
+    import sys
+    from expecto_amd import chromatin, h5
+    vcf = workdir / "in2.vcf"
+    with open(vcf, "w") as f:
+        f.write("##fileformat=VCFv4.1\n")
+        f.write(open(os.path.join(GOLDEN, "chromatin_vcf.txt")).read())
+    common = ["--maxshift", "200", "--genome", str(workdir / "hg19.fa"), "--synthetic-weights", "0",
+              "--max-batch", "40"]
+    one = workdir / "out_1rank"
+    chromatin.main([str(vcf), "--output_dir", str(one)] + common)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    two = workdir / "out_2rank"
+    env = dict(os.environ, EXPECTO_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "expecto_amd.chromatin",
+                        str(vcf), "--output_dir", str(two)] + common,
+                       env=env, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    for sh in (0, -200, 200):
+        a = h5.read(str(one / f"snps.shift_{sh}.diff.h5"))
+        b = h5.read(str(two / f"snps.shift_{sh}.diff.h5"))
+        for k in ("ref", "alt", "diff"):
+            np.testing.assert_array_equal(a[k], b[k])
