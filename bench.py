@@ -152,6 +152,32 @@ def hbm_reductions(dev):
     return res
 
 
+def tss_workload(eng, genome, dg, dev, genes=96, steps=2):
+    """configs[4]'s per-GPU work (compute_expecto_features.py:88-128): per gene, 200 windows
+    x fwd/rc through the segment path, then the 10 x 200 exp-decay reduction to 20020 f64
+    features; seeded TSS positions and strands on the synthetic genome."""
+    from expecto_amd.tss import TSSPipeline
+    rng = np.random.default_rng(55)
+    names = sorted(genome)
+    chroms = [names[i] for i in rng.integers(0, len(names), genes)]
+    tss = [int(rng.integers(30000, len(genome[c]) - 30000)) for c in chroms]
+    strands = rng.choice([-1, 1], genes)
+    pipe = TSSPipeline(eng, dg)
+    pipe.features(chroms, tss, strands)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        pipe.features(chroms, tss, strands)
+    e1.record()
+    torch.cuda.synchronize()
+    el = e0.elapsed_time(e1) * 1e-3
+    gps = genes * steps / el
+    return {"genes_per_s": gps, "genes_per_step": genes, "windows_per_gene": 400,
+            "dense_windows_per_s": gps * 400, "ms_per_step": el / steps * 1e3,
+            "projected_20k_genes_s_1gpu": 20000 / gps, "projected_20k_genes_s_8gpu_weak": 20000 / gps / 8}
+
+
 def time_final_gather(S, n, dev, rank, world):
     """configs[3]'s exchange step, outside the timed steps: one step's outputs of every rank
     (y [2, 2, S, n, 2002] and diff [2, S, n, 2002] fp32) gathered to rank 0 per shift, as the
@@ -373,6 +399,7 @@ def main():
             alt_prec[prec] = {"variants_per_s": n * 3 / elp, "ms_per_step": elp / 3 * 1e3,
                               "dominant": {k: rp[k] for k in ("kernel", "layer", "achieved", "peak", "frac")}}
         extras["headline_other_precisions"] = alt_prec
+        extras["cfg5_tss_features"] = tss_workload(eng, genome, pipe.dg, dev)
         extras["hbm_reductions"] = hbm_reductions(dev)
         rec["extra_workloads"] = extras
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
