@@ -410,6 +410,10 @@ def main():
         rec["cpu_baseline"] = cpu_baseline(sd_cpu, seqs_to_codes(sample), args.cpu_seconds,
                                            min(args.cpu_threads, os.cpu_count() or 1), 4 * S)
         rec["speedup_vs_cpu_baseline"] = value / rec["cpu_baseline"]["value"]
+        if args.cpu_threads != 8:
+            # SURVEY.md 8(d) asks for P = 8 beside the box's full share (a shorter sample)
+            p8 = cpu_baseline(sd_cpu, seqs_to_codes(sample), args.cpu_seconds / 2, 8, 4 * S)
+            rec["cpu_baseline_8_threads"] = {k: p8[k] for k in ("value", "unit", "cores", "windows_per_s", "sample")}
     if world > 1:
         rec["final_gather"] = time_final_gather(S, n, dev, rank, world)
     if rank == 0:
