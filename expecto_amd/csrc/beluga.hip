@@ -157,6 +157,44 @@ __global__ void pool4_phases(const float* __restrict__ in, int n_seg, int s_in, 
   store_act_rt(fmt, out, orow, C, c, m);   // fmt 2: values stay in the (shared) scaled domain
 }
 
+// pool4_phases for f16x3 rows (fmt 2), 16-byte accesses: a row of C channels is C/32 groups of
+// [32 hi | 32 lo] fp16, so one thread takes 8 channels (16 B of hi + the matching 16 B of lo)
+// of 4 input rows and writes 8 pooled channels; 4 pooled rows per 256-thread block.  The same
+// decode (hi + lo), fmaxf order and canonical re-split as pool4_phases: bitwise equal.
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+__global__ __launch_bounds__(256) void pool4_phases_h2(const float* __restrict__ in, int s_in, int t_in, int C,
+                                                        int n_ph, int4 ph, int s_out, float* __restrict__ out) {
+  const int c8 = threadIdx.x & 63;
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int i = blockIdx.y % n_ph;
+  const long long seg = blockIdx.y / n_ph;
+  const int p = i == 0 ? ph.x : i == 1 ? ph.y : i == 2 ? ph.z : ph.w;
+  if (c8 >= C / 8 || g >= (t_in - p) / 4) return;
+  const long long rb = (long long)C * 4;   // bytes per row
+  const int cofs = (c8 >> 2) * 128 + (c8 & 3) * 16;
+  const char* src = reinterpret_cast<const char*>(in) + (seg * s_in + p + 4LL * g) * rb + cofs;
+  halfx8 hi[4], lo[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    hi[j] = *reinterpret_cast<const halfx8*>(src + j * rb);
+    lo[j] = *reinterpret_cast<const halfx8*>(src + j * rb + 64);
+  }
+  halfx8 oh, ol;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float m = (float)hi[0][e] + (float)lo[0][e];
+#pragma unroll
+    for (int j = 1; j < 4; ++j) m = fmaxf(m, (float)hi[j][e] + (float)lo[j][e]);
+    _Float16 h, l;
+    split_h2(m, h, l);
+    oh[e] = h;
+    ol[e] = l;
+  }
+  char* dst = reinterpret_cast<char*>(out) + ((seg * n_ph + i) * s_out + g) * rb + cofs;
+  *reinterpret_cast<halfx8*>(dst) = oh;
+  *reinterpret_cast<halfx8*>(dst + 64) = ol;
+}
+
 // FC1 row table of the windows of one segment chunk: window m of the chunk reads conv6
 // rows [off6, off6+106) of block (segment, pool2 phase).
 // (widx: optional list of window indices; row m then serves window widx[m].)
@@ -1181,8 +1219,13 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
       if (pr && ((rc = st_wait(h->pev[6])) || (rc = alt_gemm(2, 1, kA4u, kW4u, false, h->D1)))) return rc;
       {  // pool2 phases (Q -> P)
         LayerTimer lt(h, 3, st);
-        dim3 grid(g.S5, ns * n_ph);
-        pool4_phases<<<grid, dim3(480), 0, st>>>(h->Q, ns, g.T4, g.T4, 480, n_ph, ph4, g.S5, h->P, act_fmt());
+        if (act_fmt() == 2) {
+          dim3 grid((g.S5 + 3) / 4, ns * n_ph);
+          pool4_phases_h2<<<grid, dim3(256), 0, st>>>(h->Q, g.T4, g.T4, 480, n_ph, ph4, g.S5, h->P);
+        } else {
+          dim3 grid(g.S5, ns * n_ph);
+          pool4_phases<<<grid, dim3(480), 0, st>>>(h->Q, ns, g.T4, g.T4, 480, n_ph, ph4, g.S5, h->P, act_fmt());
+        }
         if ((rc = check_launch("pool4_phases"))) return rc;
       }
       if (pr) {   // alt pool2 phases from the unpooled conv4 rows (Q) and the alt conv4 run
