@@ -122,6 +122,44 @@ __global__ void fc1_reduce(const float* __restrict__ part, int splits, long long
   store_act_rt(fmt, h1, row, kHidLd, n, v, osc, ovf);
 }
 
+// fc1_reduce for f16x3 hidden rows, 4 columns per thread: float4 loads of the split-K slabs,
+// 8-byte stores of the 4 hi and 4 lo halves (4 columns never straddle a 32-column plane group).
+// Same per-element sum order, unscaling, bias, ReLU and split: bitwise equal to fc1_reduce.
+typedef _Float16 halfx4 __attribute__((ext_vector_type(4)));
+__global__ void fc1_reduce_h2(const float* __restrict__ part, int splits, long long split_stride, long long count4,
+                              const float* __restrict__ bias, float* __restrict__ h1,
+                              const float* __restrict__ col_scale, float osc, int* __restrict__ ovf) {
+  const long long i4 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i4 >= count4) return;
+  const long long i = i4 * 4;
+  const long long row = i / kHidLd;
+  const int n = (int)(i - row * kHidLd);
+  floatx4 s = {0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < splits; ++k) {
+    const floatx4 v = *reinterpret_cast<const floatx4*>(part + k * split_stride + i);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s[e] += v[e];
+  }
+  halfx4 hv, lv;
+  bool bad = false;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float t = s[e];
+    if (col_scale) t *= col_scale[n + e];
+    const float v = n + e < kFc1Out ? fmaxf(t + bias[min(n + e, kFc1Out - 1)], 0.f) : 0.f;
+    const float x = v * osc;
+    bad |= !(fabsf(x) < 65504.f);
+    _Float16 hh, ll;
+    split_h2(x, hh, ll);
+    hv[e] = hh;
+    lv[e] = ll;
+  }
+  if (bad && ovf) *ovf = 1;
+  _Float16* d = reinterpret_cast<_Float16*>(h1) + act_index<2>(row, kHidLd, n);
+  *reinterpret_cast<halfx4*>(d) = hv;
+  *reinterpret_cast<halfx4*>(d + 32) = lv;
+}
+
 // FC2 output: y[c_rows[m] or m][n] = sigmoid(sum_k part[k][m][n] * col_scale[n] + bias[n]) (Beluga.py:46-48)
 __global__ void fc2_reduce(const float* __restrict__ part, int splits, long long split_stride, int M,
                            const float* __restrict__ bias, const float* __restrict__ col_scale,
@@ -919,8 +957,12 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     LayerTimer lt(h, 7, st);
     const long long count = (long long)nb * kHidLd;
     const bool f16 = g_precision == EXPECTO_PRECISION_F16X3;
-    fc1_reduce<<<dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st>>>(
-        h->part, splits, part_rows * kHidLd, count, h->fc1b, h->h1, act_fmt(), f16 ? h->cs[5] : nullptr, exp2i(h->sx[6]), h->ovf);
+    if (act_fmt() == 2)
+      fc1_reduce_h2<<<dim3((unsigned)((count / 4 + 255) / 256)), dim3(256), 0, st>>>(
+          h->part, splits, part_rows * kHidLd, count / 4, h->fc1b, h->h1, h->cs[5], exp2i(h->sx[6]), h->ovf);
+    else
+      fc1_reduce<<<dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st>>>(
+          h->part, splits, part_rows * kHidLd, count, h->fc1b, h->h1, act_fmt(), f16 ? h->cs[5] : nullptr, exp2i(h->sx[6]), h->ovf);
     if ((rc = check_launch("fc1_reduce"))) return rc;
   }
   {
