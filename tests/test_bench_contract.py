@@ -1,0 +1,39 @@
+"""bench.py's bookkeeping against the committed profiles (CPU): the dominant kernel name it
+reports is one rocprofv3 saw, the roofline's per-window MACs are the oracle's, and the HBM
+traffic of the committed PMC summary is found for the default workload key."""
+import csv
+import glob
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _latest_profile():
+    tags = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")))
+    assert tags, "no profiles/<round> directory"
+    return tags[-1]
+
+
+def test_layer_macs_are_the_oracle_count():
+    import bench
+    from oracle.beluga_np import macs_per_window
+    assert bench.WINDOW_MACS == macs_per_window()
+
+
+def test_reported_kernel_names_exist_in_the_committed_kernel_trace():
+    import bench
+    names = [r["Name"] for r in csv.DictReader(open(os.path.join(_latest_profile(), "kernel_stats.csv")))]
+    for layer in ("conv1", "conv2", "conv3", "conv4", "conv5", "conv6", "fc1", "fc2"):
+        k = bench.kernel_name(layer, "f16x3")
+        assert any(k in n for n in names), (layer, k)
+
+
+def test_committed_traffic_matches_the_default_workload_key():
+    import bench
+    from expecto_amd.pipeline import shift_order
+    key = {"variants": 1000, "shifts": shift_order(0), "precision": "f16x3", "max_batch": bench.MAX_BATCH}
+    traffic, src = bench.pmc_traffic(key, bench.kernel_name("conv2", "f16x3"))
+    assert traffic is not None and traffic > 0, "re-take profiles: tools/profile_round.sh + collect_profiles.py"
+    assert src.startswith("profiles/")
