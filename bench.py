@@ -3,14 +3,20 @@
 Workload (BASELINE.json configs[1], per GPU): 1k synthetic biallelic SNVs, shift 0, ref+alt
 alleles x fwd+rc strands = 4000 Beluga windows per step.  One step = device window
 generation from the HBM-resident genome (expecto_variant_windows) + the Beluga forward over
-all 4000 windows (conv1 .. fc2+sigmoid, fp32) + diff = alt - ref: exactly the device work of
+all 4000 windows (conv1 .. fc2+sigmoid, fp32 in/out) + diff = alt - ref: exactly the device work of
 one chromatin.py shift for 1k variants, inputs already resident in HBM.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 N>1: weak scaling, each rank its own 1k SNVs, no collective in the step (variants are
-independent; the RCCL gather belongs to file output).  Rank 0 prints ONE JSON line.
+independent; the RCCL gather belongs to file output and is timed after the steps as
+"final_gather").  Rank 0 prints ONE JSON line.
+
+The "f16x3" arithmetic computes fp32 products from 22-bit fp16 planes (DTYPES below).
+N=1 extras, outside `value`: configs[2] (+-800 sweep), the 200-window variant unit,
+configs[4] TSS genes, the other two precisions, the HBM-bound reductions in GB/s, and the
+CPU port timed on host cores (16 and 8 threads).
 """
 from __future__ import annotations
 
