@@ -1,22 +1,27 @@
 """Benchmark of the ExPecto hot path on MI355X (contract: see task / DESIGN.md "Measurement").
 
-Workload (BASELINE.json configs[1], per GPU): 1k synthetic biallelic SNVs, shift 0, ref+alt
-alleles x fwd+rc strands = 4000 Beluga windows per step.  One step = device window
-generation from the HBM-resident genome (expecto_variant_windows) + the Beluga forward over
-all 4000 windows (conv1 .. fc2+sigmoid, fp32 in/out) + diff = alt - ref: exactly the device work of
-one chromatin.py shift for 1k variants, inputs already resident in HBM.
+Headline workload = BASELINE.json's metric unit, the "200-window variant" (per GPU and step):
+96 seeded SNVs, each scored with 200 windows (shifts -20000..19800 step 200,
+geuvadis_sed_for_top_eqtls.py:61) x ref/alt allele x fwd/rc strand = 800 Beluga windows per
+variant.  One step = window generation from the HBM-resident genome + the Beluga forward of
+all 76,800 windows (segment path: conv trunk shared across the shifts, alt allele through
+its SNV cone, bit-identical to per-window forwards) + the float64 fwd/rc mean and 10 x 200
+exp-decay reduction to 20030 features per allele (geuvadis_sed_for_top_eqtls.py:83-121).
+`value` is timed with layer profiling OFF; the f16x3 overflow flag is checked at the end of
+every step (the release point of a batch) and a flagged step is recomputed in bf16x6 inside
+the timed region.  Layer times and the roofline come from a separate profiled pass.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-N>1: weak scaling, each rank its own 1k SNVs, no collective in the step (variants are
-independent; the RCCL gather belongs to file output and is timed after the steps as
-"final_gather").  Rank 0 prints ONE JSON line.
+N>1: weak scaling, each rank its own 96 variants per step, no collective in the step (variants
+are independent).  N>1 extra, outside `value`: configs[3]'s per-rank shape (100k SNVs over 8
+ranks = 12.5k SNVs x 9 shifts per rank) computed once and its outputs gathered to rank 0 per
+shift over RCCL (the file-output exchange), both timed.  Rank 0 prints ONE JSON line.
 
-The "f16x3" arithmetic computes fp32 products from 22-bit fp16 planes (DTYPES below).
-N=1 extras, outside `value`: configs[2] (+-800 sweep), the 200-window variant unit,
-configs[4] TSS genes, the other two precisions, the HBM-bound reductions in GB/s, and the
-CPU port timed on host cores (16 and 8 threads).
+N=1 extras, outside `value`: the headline in bf16x6 (fp32-faithful split), configs[1]
+(1k SNVs, shift 0), configs[2] (+-800 sweep), configs[4] TSS genes, the HBM-bound reductions
+in GB/s, and the CPU port timed on host cores (P = 8 and 16 threads, batch 32 and 512).
 """
 from __future__ import annotations
 
@@ -35,7 +40,7 @@ sys.path.insert(0, REPO)
 
 from expecto_amd import beluga, dist as edist, synthetic  # noqa: E402
 from expecto_amd.genome import DeviceGenome, Fasta  # noqa: E402
-from expecto_amd.pipeline import VariantPipeline, VariantSet  # noqa: E402
+from expecto_amd.pipeline import VariantPipeline, VariantSet, shift_order  # noqa: E402
 
 METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
@@ -54,7 +59,13 @@ LAYER_MACS = {
 }
 GEMM_LAYER_EPI = {"conv2": (2, 1), "conv3": (3, 0), "conv4": (4, 1), "conv5": (5, 0), "conv6": (6, 0),
                   "fc1": (7, 3), "fc2": (8, 3)}
+WINDOW_MACS = sum(LAYER_MACS.values())
 
+SHIFTS_200 = list(range(-20000, 20000, 200))     # geuvadis_sed_for_top_eqtls.py:61, compute_expecto_features.py:88
+N200 = 96                                        # 200-window variants per GPU and step
+WIN_PER_VARIANT_200 = 2 * 2 * len(SHIFTS_200)    # ref/alt x fwd/rc x 200 shifts = 800
+SNV_MARGIN_200 = 25_000                          # every window of the +-20 kb sweep inside its contig
+CFG3_PER_RANK = 12_500                           # configs[3]: 100k SNVs over 8 ranks
 
 DTYPES = {
     "bf16x6": "fp32 (bf16x6: exact 3-way bf16 split, 6 MFMA products, fp32 accumulate)",
@@ -64,11 +75,14 @@ DTYPES = {
 }
 
 
-def kernel_name(layer: str, precision: str) -> str:
-    """rocprofv3 kernel name of a layer's launch (per-window path)."""
+def kernel_name(layer: str, precision: str, segments: bool = True) -> str:
+    """rocprofv3 kernel name of a layer's launch.  On the segment path (the headline, configs[2]
+    and [4]) conv4 runs unpooled (its pool2 is a separate per-phase kernel)."""
     if layer not in GEMM_LAYER_EPI:
         return {"conv1": "beluga_conv1", "fc1_reduce": "fc1_reduce"}[layer]
     l, e = GEMM_LAYER_EPI[layer]
+    if segments and layer == "conv4":
+        e = 0
     if precision == "bf16x6":
         return f"beluga_gemm_x6q<{l}, {e}, 0>"
     if precision == "f16x3":
@@ -78,39 +92,45 @@ def kernel_name(layer: str, precision: str) -> str:
             return f"beluga_conv_h3r<{l}, {e}, 0>"
         return f"beluga_conv_h3p<{l}, {e}, 0, 3>"
     return f"beluga_gemm<{l}, {e}, 4, 2, 32, 1>"
-WINDOW_MACS = sum(LAYER_MACS.values())
 
 
-def cpu_baseline(sd_cpu, codes: np.ndarray, seconds: float, threads: int, windows_per_variant: int):
-    """Oracle torch-CPU forward (the reference's CPU arithmetic) on a bounded sample."""
+# ---- CPU baseline ---------------------------------------------------------------------------
+def cpu_baseline(sd_cpu, codes: np.ndarray, seconds: float, windows_per_variant: int):
+    """Oracle torch-CPU forward (the reference's CPU arithmetic, oneDNN fp32) on a bounded sample
+    of the headline's windows, at P = 8 and 16 host threads (16 = this job's CPU share of the
+    box; os.cpu_count() reports the whole machine) and batch 32 and 512.  Per
+    window the cost is linear, so windows/s extrapolates; variants/s = windows/s / 800 (the
+    reference forwards every window of a 200-window variant, geuvadis_sed_for_top_eqtls.py:80-98)."""
     from oracle.beluga_np import forward_torch_cpu
     from expecto_amd.encode import codes_to_onehot
 
-    torch.set_num_threads(threads)
-    x = torch.from_numpy(codes_to_onehot(codes[:32], with_rc=False).astype(np.float32)).unsqueeze(2)
-    forward_torch_cpu(sd_cpu, x[:4])                     # warm-up
-    done, t0 = 0, time.perf_counter()
-    while True:
-        forward_torch_cpu(sd_cpu, x)
-        done += x.shape[0]
-        el = time.perf_counter() - t0
-        if el >= seconds or el >= 30.0:
-            break
-    wps = done / el
-    return {"value": wps / windows_per_variant, "unit": "variants/s", "cores": threads, "kind": "port",
-            "windows_per_s": wps,
-            "sample": f"{done} windows of the same workload (seeded SNV ref windows), batch 32, "
-                      f"oracle/beluga_np.forward_torch_cpu (torch CPU fp32, oneDNN), {el:.1f} s"}
+    x_all = torch.from_numpy(codes_to_onehot(codes, with_rc=False).astype(np.float32)).unsqueeze(2)
+    runs = {}
+    for threads in (16, 8):
+        torch.set_num_threads(threads)
+        forward_torch_cpu(sd_cpu, x_all[:4])                     # warm-up
+        for batch in (32, 512):
+            x = x_all[:batch]
+            done, t0 = 0, time.perf_counter()
+            while True:
+                forward_torch_cpu(sd_cpu, x)
+                done += x.shape[0]
+                el = time.perf_counter() - t0
+                if el >= seconds:
+                    break
+            runs[f"p{threads}_b{batch}"] = {"windows_per_s": done / el, "windows": done, "s": el}
+    best16 = max((v for k, v in runs.items() if k.startswith("p16")), key=lambda v: v["windows_per_s"])
+    b16 = max((k for k in runs if k.startswith("p16")), key=lambda k: runs[k]["windows_per_s"])
+    return {"value": best16["windows_per_s"] / windows_per_variant, "unit": "variants/s", "cores": 16,
+            "kind": "port", "windows_per_s": best16["windows_per_s"], "host_cpu_count": os.cpu_count(),
+            "per_setting": {k: dict(v, variants_per_s=v["windows_per_s"] / windows_per_variant)
+                            for k, v in runs.items()},
+            "sample": f"seeded SNV ref windows of the headline workload; oracle/beluga_np.forward_torch_cpu "
+                      f"(torch CPU fp32, oneDNN) at 16 and 8 threads x batch 32 and 512, ~{seconds:.0f} s each; "
+                      f"value = best 16-thread setting ({b16}) / {windows_per_variant} windows per variant"}
 
 
-# Handle workspace (windows per launch chunk): 8192 lets the segment path put ~40 variants'
-# 200-window segments in one chunk (tools/seg200_sweep.py: 4000 -> 8192 windows and 24 -> 96
-# variants per step take the 200-window workload from 799 to 881 variants/s); the headline's
-# 4000 windows stay one chunk either way.
-MAX_BATCH = 8192
-N200 = 96
-
-
+# ---- HBM-bound reductions -----------------------------------------------------------------
 def hbm_reductions(dev):
     """The metric's "HBM GB/s vs peak": the HBM-bound spatial reductions timed
     with HIP events on synthetic inputs resident in HBM; algorithmic bytes = every input read
@@ -133,7 +153,6 @@ def hbm_reductions(dev):
     rng = np.random.default_rng(4)
     dist = rng.integers(-20000, 20000, n_var)
     plus = rng.integers(0, 2, n_var).astype(bool)
-    from expecto_amd.pipeline import shift_order
     sh = shift_order(800)
     vout = torch.empty((n_var, 10 * F), dtype=torch.float64, device=dev)
     for name, fn, nbytes in (
@@ -158,118 +177,111 @@ def hbm_reductions(dev):
     return res
 
 
-def tss_workload(eng, genome, dg, dev, genes=96, steps=2):
-    """configs[4]'s per-GPU work (compute_expecto_features.py:88-128): per gene, 200 windows
-    x fwd/rc through the segment path, then the 10 x 200 exp-decay reduction to 20020 f64
-    features; seeded TSS positions and strands on the synthetic genome."""
-    from expecto_amd.tss import TSSPipeline
-    rng = np.random.default_rng(55)
-    names = sorted(genome)
-    chroms = [names[i] for i in rng.integers(0, len(names), genes)]
-    tss = [int(rng.integers(30000, len(genome[c]) - 30000)) for c in chroms]
-    strands = rng.choice([-1, 1], genes)
-    pipe = TSSPipeline(eng, dg)
-    pipe.features(chroms, tss, strands)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(steps):
-        pipe.features(chroms, tss, strands)
-    e1.record()
-    torch.cuda.synchronize()
-    el = e0.elapsed_time(e1) * 1e-3
-    gps = genes * steps / el
-    return {"genes_per_s": gps, "genes_per_step": genes, "windows_per_gene": 400,
-            "dense_windows_per_s": gps * 400, "ms_per_step": el / steps * 1e3,
-            "projected_20k_genes_s_1gpu": 20000 / gps, "projected_20k_genes_s_8gpu_weak": 20000 / gps / 8}
-
-
-def time_final_gather(S, n, dev, rank, world):
-    """configs[3]'s exchange step, outside the timed steps: one step's outputs of every rank
-    (y [2, 2, S, n, 2002] and diff [2, S, n, 2002] fp32) gathered to rank 0 per shift, as the
-    chromatin CLI does before rank 0 writes the .diff.h5 files (RCCL gather over xGMI)."""
-    y = torch.rand((2, 2, S, n, 2002), device=dev)
-    d = torch.rand((2, S, n, 2002), device=dev)
-    total = world * n
-
-    def gather():
-        for j in range(S):
-            edist.gather_rows_to(y[:, :, j:j + 1], 3, total, world, rank)
-            edist.gather_rows_to(d[:, j:j + 1], 2, total, world, rank)
-
-    gather()                                   # warm the communicator
-    torch.cuda.synchronize()
-    torch.distributed.barrier()
-    t0 = time.perf_counter()
-    gather()
-    torch.cuda.synchronize()
-    torch.distributed.barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-    if torch.distributed.get_backend() == "nccl":
-        el = el.to(dev)
-    torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
-    nbytes = (world - 1) * (y.numel() + d.numel()) * 4        # bytes arriving at rank 0
-    ms = float(el.item()) * 1e3
-    return {"ms": ms, "bytes_into_rank0": nbytes, "GB_per_s": nbytes / (ms * 1e-3) / 1e9,
-            "what": "one step's y + diff of every rank to rank 0, per shift (not part of value)"}
-
-
-def make_variants(genome, n, seed):
-    snvs = synthetic.snvs(genome, n, seed=seed)
+# ---- workloads ------------------------------------------------------------------------------
+def make_variants(genome, n, seed, margin=5000):
+    snvs = synthetic.snvs(genome, n, seed=seed, margin=margin)
     return VariantSet([v[0] for v in snvs], np.array([v[1] for v in snvs]), [v[2] for v in snvs],
                       [v[3] for v in snvs])
 
 
-def time_workload(pipe, eng, prep, shifts, n, steps, warmup, dev, world):
-    """Time `steps` steps (window generation + forward + diff) with HIP-event layer timing."""
-    S = len(shifts)
-    y = torch.empty((2, 2, S, n, 2002), dtype=torch.float32, device=dev)
+class Sed200:
+    """The headline step: 200-window variants (geuvadis_sed_for_top_eqtls.py:61-121)."""
 
-    def step():
-        pipe.predict(prep, out=y)
-        return pipe.diff(y)
+    def __init__(self, pipe, genome, n, seed, dev):
+        from expecto_amd.features import tss_pos_weights
+        self.pipe, self.n = pipe, n
+        self.prep = pipe.prepare(make_variants(genome, n, seed, margin=SNV_MARGIN_200), SHIFTS_200, rows="variant")
+        S = len(SHIFTS_200)
+        self.y = torch.empty((2, 2, n, S, 2002), dtype=torch.float32, device=dev)
+        self.w = torch.from_numpy(tss_pos_weights(np.asarray(SHIFTS_200))).to(dev)
+        self.feat = torch.empty((2, n, 20030), dtype=torch.float64, device=dev)
+
+    def __call__(self):
+        self.pipe.predict(self.prep, out=self.y)
+        self.pipe.sed_features(self.y, self.w, out=self.feat)
+
+
+class ShiftSweep:
+    """chromatin.py's device work for one variant batch: every shift's ref/alt x fwd/rc windows
+    + diff = alt - ref (configs[1]: shift 0; configs[2]/[3]: +-800)."""
+
+    def __init__(self, pipe, genome, n, seed, shifts, dev):
+        self.pipe, self.n, self.S = pipe, n, len(shifts)
+        self.prep = pipe.prepare(make_variants(genome, n, seed), shifts)
+        self.y = torch.empty((2, 2, self.S, n, 2002), dtype=torch.float32, device=dev)
+        self.d = None
+
+    def __call__(self):
+        self.pipe.predict(self.prep, out=self.y)
+        self.d = self.pipe.diff(self.y)
+
+
+def time_steps(step, eng, steps, warmup, world, dev):
+    """Wall time of `steps` steps between barriers + syncs (max over ranks), profiling off.
+    Each step ends at its release point: the f16x3 overflow flag is read (a stream sync) and a
+    flagged step is recomputed in bf16x6, inside the timed region."""
+    fallbacks = 0
+
+    def one():
+        nonlocal fallbacks
+        step()
+        if eng.precision == "f16x3" and eng.overflow_pending():
+            fallbacks += 1
+            with eng.precision_override("bf16x6"):
+                step()
 
     for _ in range(warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    eng.set_profiling(True)
+        one()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        step()
+        one()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     el = time.perf_counter() - t0
-    layers = eng.layer_times()
-    eng.set_profiling(False)
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         el = float(t.item())
-    return el, layers
+    return el, fallbacks
 
 
-def roofline(layers, precision):
+def profile_layers(step, eng, steps):
+    """Per-layer HIP-event times / launches / executed MACs over `steps` profiled steps (a pass
+    apart from the timed one)."""
+    torch.cuda.synchronize()
+    eng.set_profiling(True)
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    layers = eng.layer_times()
+    eng.set_profiling(False)
+    eng.overflow_pending()
+    return layers
+
+
+def products_and_peak(precision):
+    if precision == "bf16x6":
+        return BF16X6_PRODUCTS, BF16_MFMA_PEAK_TFLOPS
+    if precision == "f16x3":
+        return F16X3_PRODUCTS, BF16_MFMA_PEAK_TFLOPS
+    return 1, FP32_MFMA_PEAK_TFLOPS
+
+
+def roofline(layers, precision, segments=True):
     """MFMA roofline of the dominant GEMM kernel from executed work per launch (library counts)
     and its average launch duration (HIP events on the launch stream)."""
     dom = max((k for k in GEMM_LAYER_EPI), key=lambda k: layers[k][0])
     ms, calls, macs = layers[dom]
     fp32_flops_launch = 2.0 * macs / calls
     fp32_tflops = fp32_flops_launch / (ms / calls / 1e3) / 1e12
-    if precision == "bf16x6":
-        mult, peak = BF16X6_PRODUCTS, BF16_MFMA_PEAK_TFLOPS
-    elif precision == "f16x3":
-        mult, peak = F16X3_PRODUCTS, BF16_MFMA_PEAK_TFLOPS
-    else:
-        mult, peak = 1, FP32_MFMA_PEAK_TFLOPS
+    mult, peak = products_and_peak(precision)
     achieved = mult * fp32_tflops
-    return {"bound": "mfma", "kernel": kernel_name(dom, precision), "layer": dom, "achieved": achieved,
+    return {"bound": "mfma", "kernel": kernel_name(dom, precision, segments), "layer": dom, "achieved": achieved,
             "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
             "avg_launch_ms": ms / calls, "launches": calls, "mfma_flops_per_launch": mult * fp32_flops_launch,
             "fp32_flops_per_launch": fp32_flops_launch, "fp32_tflops": fp32_tflops, "precision": precision}
@@ -279,11 +291,9 @@ def pmc_traffic(key, kernel):
     """HBM bytes per launch of ``kernel`` from the newest committed rocprofv3 --pmc summary
     (profiles/<tag>/traffic.json, written by tools/collect_profiles.py from FETCH_SIZE and
     WRITE_SIZE passes of this same bench command).  None unless that profile was taken on the
-    same workload key (variants, shifts, precision, max_batch): PMC counters cannot be read
-    live next to the HIP-event timing."""
+    same workload key: PMC counters cannot be read live next to the HIP-event timing."""
     import glob
-    for path in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*",
-                                              "traffic.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "traffic.json")), reverse=True):
         try:
             t = json.load(open(path))
         except (OSError, ValueError):
@@ -296,17 +306,94 @@ def pmc_traffic(key, kernel):
     return None, None
 
 
+def layer_summary(layers, el_steps):
+    return ({k: ms / el_steps for k, (ms, c, m) in layers.items()},
+            {k: 2.0 * m / (ms * 1e-3) / 1e12 for k, (ms, c, m) in layers.items() if ms > 0})
+
+
+def measure(step, eng, n_units, steps, warmup, world, dev, prof_steps=2, segments=True):
+    """(units/s, ms/step, fallbacks, layers, roofline, executed MACs per step)."""
+    el, fb = time_steps(step, eng, steps, warmup, world, dev)
+    layers = profile_layers(step, eng, prof_steps)
+    exec_macs = sum(m for _, _, m in layers.values()) / prof_steps
+    return {"units_per_s": world * n_units * steps / el, "ms_per_step": el / steps * 1e3, "fallbacks": fb,
+            "layers": layers, "roofline": roofline(layers, eng.precision, segments), "exec_macs_step": exec_macs,
+            "prof_steps": prof_steps}
+
+
+def extra_record(m, unit, n_units, windows_per_unit, precision):
+    ms_l, tf_l = layer_summary(m["layers"], m["prof_steps"])
+    mult, peak = products_and_peak(precision)
+    step_s = m["ms_per_step"] * 1e-3
+    return {unit: m["units_per_s"], f"{unit.split('_')[0]}_per_step": n_units, "ms_per_step": m["ms_per_step"],
+            "windows_per_unit": windows_per_unit, "dense_windows_per_s": m["units_per_s"] * windows_per_unit,
+            "executed_fp32_tflops": 2.0 * m["exec_macs_step"] / step_s / 1e12,
+            "step_mfma_frac": mult * 2.0 * m["exec_macs_step"] / step_s / 1e12 / peak,
+            "f16_fallback_steps": m["fallbacks"], "layer_ms_per_step": ms_l, "layer_tflops": tf_l,
+            "roofline": m["roofline"], "precision": precision}
+
+
+def tss_workload(eng, genome, dg, dev, genes=96, steps=2):
+    """configs[4]'s per-GPU work (compute_expecto_features.py:88-128): per gene, 200 windows
+    x fwd/rc through the segment path, then the 10 x 200 exp-decay reduction to 20020 f64
+    features; seeded TSS positions and strands on the synthetic genome."""
+    from expecto_amd.tss import TSSPipeline
+    rng = np.random.default_rng(55)
+    names = sorted(genome)
+    chroms = [names[i] for i in rng.integers(0, len(names), genes)]
+    tss = [int(rng.integers(30000, len(genome[c]) - 30000)) for c in chroms]
+    strands = rng.choice([-1, 1], genes)
+    pipe = TSSPipeline(eng, dg)
+    step = lambda: pipe.features(chroms, tss, strands)   # noqa: E731
+    el, fb = time_steps(step, eng, steps, 1, 1, dev)
+    gps = genes * steps / el
+    return {"genes_per_s": gps, "genes_per_step": genes, "windows_per_gene": 400, "f16_fallback_steps": fb,
+            "dense_windows_per_s": gps * 400, "ms_per_step": el / steps * 1e3,
+            "projected_20k_genes_s_1gpu": 20000 / gps, "projected_20k_genes_s_8gpu_weak": 20000 / gps / 8}
+
+
+def cfg3_rank_shard(pipe, eng, genome, rank, world, dev):
+    """configs[3] per rank (100k SNVs over 8 GPUs = 12.5k SNVs x 9 shifts, +-800), computed once
+    (timed, max over ranks), then its y + diff gathered to rank 0 one shift at a time (RCCL gather
+    over xGMI, as the chromatin CLI does before rank 0 writes each .diff.h5).  Not part of value."""
+    sh9 = shift_order(800)
+    work = ShiftSweep(pipe, genome, CFG3_PER_RANK, 1000 + rank, sh9, dev)
+    el, fb = time_steps(work, eng, 1, 1, world, dev)
+    y, d, n, total = work.y, work.d, CFG3_PER_RANK, world * CFG3_PER_RANK
+
+    def gather():
+        for j in range(len(sh9)):
+            edist.gather_rows_to(y[:, :, j:j + 1], 3, total, world, rank)
+            edist.gather_rows_to(d[:, j:j + 1], 2, total, world, rank)
+
+    gather()                                   # warm the communicator
+    torch.cuda.synchronize()
+    torch.distributed.barrier()
+    t0 = time.perf_counter()
+    gather()
+    torch.cuda.synchronize()
+    torch.distributed.barrier()
+    gl = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if torch.distributed.get_backend() == "nccl":
+        gl = gl.to(dev)
+    torch.distributed.all_reduce(gl, op=torch.distributed.ReduceOp.MAX)
+    nbytes = (world - 1) * (y.numel() + d.numel()) * 4        # bytes arriving at rank 0
+    gms = float(gl.item()) * 1e3
+    return {"snvs_per_rank": n, "shifts": sh9, "compute_s": el, "variants_per_s": world * n / el,
+            "f16_fallback_steps": fb,
+            "gather": {"ms": gms, "bytes_into_rank0": nbytes, "GB_per_s": nbytes / (gms * 1e-3) / 1e9,
+                       "what": "every rank's y + diff to rank 0, one shift at a time (RCCL gather)"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--variants", type=int, default=1000, help="SNVs per GPU per step")
-    ap.add_argument("--maxshift", type=int, default=0, help="0 = configs[1] (shift 0 only)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--variants", type=int, default=N200, help="200-window variants per GPU per step")
+    ap.add_argument("--cpu-seconds", type=float, default=7.0, help="per CPU-baseline setting (4 settings)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="skip the cfg3 / 200-window extra workloads")
+    ap.add_argument("--no-extras", action="store_true", help="skip the extra workloads")
     ap.add_argument("--precision", default=None, help="GEMM arithmetic (default: the engine default)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for the scaling runs; gloo to "
                     "rehearse several ranks on one GPU")
@@ -317,116 +404,101 @@ def main():
     local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    from expecto_amd.pipeline import shift_order
-    shifts = shift_order(args.maxshift)
-    S, n = len(shifts), args.variants
-    rows = 4 * S * n
+    n = args.variants
 
     genome = synthetic.genome_bytes(n_contigs=24, contig_len=2_000_000, seed=0)
     fasta = Fasta.from_dict(genome)
-    vs = make_variants(genome, n, 1 + rank)
     model = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=MAX_BATCH)
     sd_cpu = {k: v.detach().clone() for k, v in model.state_dict().items()} if (rank == 0 and world == 1) else None
     model = model.cuda()
     eng = model.engine()
     if args.precision:
         eng.set_precision(args.precision)
+    eng.set_overflow_check(deferred=True)              # checked at each step's release point
     pipe = VariantPipeline(eng, fasta, DeviceGenome(fasta, device=dev))
-    prep = pipe.prepare(vs, shifts)                          # variant table resident in HBM
+    head = Sed200(pipe, genome, n, 202 + rank, dev)    # variant tables resident in HBM
 
-    el, layers = time_workload(pipe, eng, prep, shifts, n, args.steps, args.warmup, dev, world)
-    total_rows = rows * args.steps
-    value = world * n * args.steps / el
-    exec_macs = sum(m for _, _, m in layers.values())
-    key = {"variants": n, "shifts": shifts, "precision": eng.precision, "max_batch": MAX_BATCH}
-    roof = roofline(layers, eng.precision)
+    m = measure(head, eng, n, args.steps, args.warmup, world, dev)
+    ms_l, tf_l = layer_summary(m["layers"], m["prof_steps"])
+    mult, peak = products_and_peak(eng.precision)
+    step_s = m["ms_per_step"] * 1e-3
+    key = {"workload": "sed200", "variants": n, "precision": eng.precision, "max_batch": MAX_BATCH}
+    roof = m["roofline"]
     roof["traffic"], src = pmc_traffic(key, roof["kernel"])
     if roof["traffic"] is not None:
         roof["traffic_unit"] = "bytes/launch (HBM read+write)"
         roof["traffic_source"] = src
     rec = {
-        "metric": METRIC, "value": value, "unit": "variants/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "metric": METRIC, "value": m["units_per_s"], "unit": "variants/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": m["ms_per_step"], "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None,
         "dtype": DTYPES[eng.precision],
         "data": "synthetic: seeded genome (24 x 2 Mbp), seeded SNVs, seeded Beluga weights x sqrt(6)",
-        "config": {"workload": f"configs[1]: {n} SNVs/GPU, shifts {shifts}, ref+alt x fwd+rc = "
-                               f"{rows} Beluga windows/step/GPU (window gen + forward + diff)",
-                   "variants_per_gpu": n, "windows_per_variant": 4 * S, "parallelism": f"dp{world} (variant shards)"},
-        "windows_per_s": world * total_rows / el,
-        "dense_equivalent_tflops": 2.0 * WINDOW_MACS * world * total_rows / el / 1e12,
-        "executed_fp32_tflops": 2.0 * exec_macs * world / el / 1e12,
+        "config": {"workload": f"200-window variants (BASELINE metric unit): {n} SNVs/GPU/step x 200 shifts "
+                               f"(-20000..19800 step 200) x ref/alt x fwd/rc = {n * WIN_PER_VARIANT_200} Beluga "
+                               f"windows/step/GPU; window gen + forward + float64 fwd/rc mean + 10x200 exp-decay "
+                               f"reduction to 20030 features per allele (geuvadis_sed_for_top_eqtls.py:61-121)",
+                   "variants_per_gpu_step": n, "windows_per_variant": WIN_PER_VARIANT_200,
+                   "parallelism": f"dp{world} (variant shards)"},
+        "windows_per_s": m["units_per_s"] * WIN_PER_VARIANT_200,
+        "dense_equivalent_tflops": 2.0 * WINDOW_MACS * m["units_per_s"] * WIN_PER_VARIANT_200 / 1e12,
+        "executed_fp32_tflops": 2.0 * m["exec_macs_step"] * world / step_s / 1e12,
+        "step_mfma_frac": mult * 2.0 * m["exec_macs_step"] / step_s / 1e12 / peak,
         "roofline": roof,
-        "layer_ms_per_step": {k: ms / args.steps for k, (ms, c, m) in layers.items()},
-        "layer_tflops": {k: 2.0 * m / (ms * 1e-3) / 1e12 for k, (ms, c, m) in layers.items() if ms > 0},
+        "layer_ms_per_step": ms_l,
+        "layer_tflops": tf_l,
+        "layer_timing": f"separate profiled pass of {m['prof_steps']} steps (HIP events per launch); the "
+                        f"*_delta slots run on the second stream beside the ref launches (upper bounds)",
+        "f16_fallback_steps": m["fallbacks"],
         "profile_key": key,
-        "reuse": "alt-cone (SNV alt windows recompute <=20 of 106 conv6 rows; bit-identical)" if S == 1 else
-                 "segments (trunk shared across shifts; bit-identical)",
+        "reuse": "segments (conv trunk shared by the 200 shifts) + alt-cone (the alt allele recomputes only the "
+                 "rows its SNV changes; windows without it copy the ref row); bit-identical to per-window forwards",
     }
     if eng.precision == "f16x3":
         fb, sx = eng.f16_state()
         rec["f16x3"] = {"fallback_calls": fb, "activation_scale_exp": sx}
     if world == 1 and not args.no_extras:
         extras = {}
-        # configs[2]: the +-800 shift sweep (9 shifts) -- segment path (trunk shared across shifts)
-        sh9 = shift_order(800)
-        v3 = make_variants(genome, 400, 101)
-        p3 = pipe.prepare(v3, sh9)
-        el3, l3 = time_workload(pipe, eng, p3, sh9, 400, 2, 1, dev, 1)
-        extras["cfg3_shift_sweep_800"] = {
-            "variants_per_s": 400 * 2 / el3, "windows_per_variant": 36, "dense_windows_per_s": 400 * 36 * 2 / el3,
-            "executed_fp32_tflops": 2.0 * sum(m for _, _, m in l3.values()) / el3 / 1e12,
-            "layer_ms_per_step": {k: ms / 2 for k, (ms, c, m) in l3.items()},
-            "layer_tflops": {k: 2.0 * m / (ms * 1e-3) / 1e12 for k, (ms, c, m) in l3.items() if ms > 0},
-            "roofline": roofline(l3, eng.precision)}
-        # the metric's literal unit: a variant scored with 200 windows (+-20 kb, stride 200) x ref/alt x fwd/rc
-        sh200 = list(range(-20000, 20000, 200))
-        v200 = make_variants(genome, N200, 202)
-        p200 = pipe.prepare(v200, sh200)
-        el2, l2 = time_workload(pipe, eng, p200, sh200, N200, 2, 1, dev, 1)
-        extras["variant_200_windows"] = {
-            "variants_per_s": N200 * 2 / el2, "variants_per_step": N200, "windows_per_variant": 800,
-            "dense_windows_per_s": N200 * 800 * 2 / el2,
-            "executed_fp32_tflops": 2.0 * sum(m for _, _, m in l2.values()) / el2 / 1e12,
-            "layer_ms_per_step": {k: ms / 2 for k, (ms, c, m) in l2.items()},
-            "layer_tflops": {k: 2.0 * m / (ms * 1e-3) / 1e12 for k, (ms, c, m) in l2.items() if ms > 0},
-            "roofline": roofline(l2, eng.precision)}
-        # the same headline workload under the other two arithmetics (all three pass the same
-        # parity bar; DESIGN.md accuracy table): exact fp32 MFMA and fp32-faithful bf16x6
-        alt_prec = {}
-        for prec in ("bf16x6", "fp32"):
-            if prec == eng.precision:
-                continue
-            base = eng.precision
-            eng.set_precision(prec)
-            elp, lp = time_workload(pipe, eng, prep, shifts, n, 3, 1, dev, 1)
-            eng.set_precision(base)
-            rp = roofline(lp, prec)
-            alt_prec[prec] = {"variants_per_s": n * 3 / elp, "ms_per_step": elp / 3 * 1e3,
-                              "dominant": {k: rp[k] for k in ("kernel", "layer", "achieved", "peak", "frac")}}
-        extras["headline_other_precisions"] = alt_prec
-        extras["cfg5_tss_features"] = tss_workload(eng, genome, pipe.dg, dev)
+        # the same headline workload in the fp32-faithful bf16x6 split
+        other = "bf16x6" if eng.precision != "bf16x6" else "f16x3"
+        with eng.precision_override(other):
+            mo = measure(head, eng, n, 3, 1, 1, dev)
+        extras[f"headline_{other}"] = extra_record(mo, "variants_per_s", n, WIN_PER_VARIANT_200, other)
+        # configs[1]: 1k SNVs, shift 0 (per-window pair path)
+        c1 = ShiftSweep(pipe, genome, 1000, 1, shift_order(0), dev)
+        extras["cfg1_1k_snv_shift0"] = extra_record(measure(c1, eng, 1000, 10, 3, 1, dev, segments=False), "variants_per_s",
+                                                    1000, 4, eng.precision)
+        del c1
+        # configs[2]: +-800 sweep (9 shifts, segment path)
+        c2 = ShiftSweep(pipe, genome, 400, 101, shift_order(800), dev)
+        extras["cfg2_shift_sweep_800"] = extra_record(measure(c2, eng, 400, 2, 1, 1, dev), "variants_per_s",
+                                                      400, 36, eng.precision)
+        del c2
+        extras["cfg4_tss_features"] = tss_workload(eng, genome, pipe.dg, dev)
         extras["hbm_reductions"] = hbm_reductions(dev)
         rec["extra_workloads"] = extras
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from expecto_amd.encode import seqs_to_codes
-        g1 = genome["chr1"]
         rng = np.random.default_rng(5)
-        sample = [g1[p - 1000:p + 1000] for p in rng.integers(5000, len(g1) - 5000, 32)]
-        rec["cpu_baseline"] = cpu_baseline(sd_cpu, seqs_to_codes(sample), args.cpu_seconds,
-                                           min(args.cpu_threads, os.cpu_count() or 1), 4 * S)
-        rec["speedup_vs_cpu_baseline"] = value / rec["cpu_baseline"]["value"]
-        if args.cpu_threads != 8:
-            # SURVEY.md 8(d) asks for P = 8 beside the box's full share (a shorter sample)
-            p8 = cpu_baseline(sd_cpu, seqs_to_codes(sample), args.cpu_seconds / 2, 8, 4 * S)
-            rec["cpu_baseline_8_threads"] = {k: p8[k] for k in ("value", "unit", "cores", "windows_per_s", "sample")}
+        sample = []
+        for _ in range(512):
+            c = sorted(genome)[int(rng.integers(0, len(genome)))]
+            p = int(rng.integers(30000, len(genome[c]) - 30000)) + int(rng.choice(SHIFTS_200))
+            sample.append(genome[c][p - 1000:p + 1000].decode())
+        rec["cpu_baseline"] = cpu_baseline(sd_cpu, seqs_to_codes(sample), args.cpu_seconds, WIN_PER_VARIANT_200)
+        rec["speedup_vs_cpu_baseline"] = rec["value"] / rec["cpu_baseline"]["value"]
     if world > 1:
-        rec["final_gather"] = time_final_gather(S, n, dev, rank, world)
+        rec["cfg3_rank_shard"] = cfg3_rank_shard(pipe, eng, genome, rank, world, dev)
     if rank == 0:
         print(json.dumps(rec))
     if world > 1:
         torch.distributed.destroy_process_group()
 
+
+# Handle workspace (windows per launch chunk): 8192 lets the segment path put ~40 variants'
+# 200-window segments in one chunk (tools/seg200_sweep.py: 4000 -> 8192 windows and 24 -> 96
+# variants per step take the 200-window workload from 799 to 881 variants/s).
+MAX_BATCH = 8192
 
 if __name__ == "__main__":
     main()

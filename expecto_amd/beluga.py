@@ -84,6 +84,35 @@ class BelugaEngine:
             _lib.check(int(n), "f16_fallbacks")
         return int(n), list(sx)
 
+    def set_overflow_check(self, deferred: bool):
+        """f16x3 overflow check: per call (default; one stream sync per forward call) or deferred
+        to ``overflow_pending()`` at the caller's release point (no sync inside a forward)."""
+        _lib.check(self.lib.expecto_beluga_set_overflow_check(self.handle, int(bool(deferred))), "set_overflow_check")
+        self.deferred = bool(deferred)
+
+    def overflow_pending(self, stream=None) -> bool:
+        """Deferred mode: sync the stream; True if an f16x3 activation overflowed since the last
+        check (the flag is cleared; recompute those calls under ``precision_override('bf16x6')``)."""
+        with torch.cuda.device(self.device):
+            r = self.lib.expecto_beluga_overflow_pending(self.handle, _lib.stream_ptr(stream))
+        if r < 0:
+            _lib.check(int(r), "overflow_pending")
+        return bool(r)
+
+    def precision_override(self, precision: str):
+        """Context manager: run the enclosed calls in another arithmetic, then restore."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            base = self.precision
+            self.set_precision(precision)
+            try:
+                yield self
+            finally:
+                self.set_precision(base)
+        return cm()
+
     def __del__(self):
         h = getattr(self, "handle", None)
         if h is not None and h.value:

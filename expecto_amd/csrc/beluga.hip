@@ -366,6 +366,16 @@ __global__ void fc1_slab_mask(const int* __restrict__ var_pos, int nv, int v0, i
   atomicOr(mask + m / tile_rows, bits);
 }
 
+// profiling: executed MACs of a masked FC1 = set slab bits x MACs per (tile, slab), summed into
+// acc on the device (one wave; the host reads acc when the layer times are collected)
+__global__ __launch_bounds__(64) void slab_macs(const unsigned* __restrict__ mask, int tiles, double per_bit,
+                                                double* __restrict__ acc) {
+  int bits = 0;
+  for (int i = threadIdx.x; i < tiles; i += 64) bits += __popc(mask[i]);
+  for (int o = 32; o > 0; o >>= 1) bits += __shfl_down(bits, o);
+  if (threadIdx.x == 0) atomicAdd(acc, bits * per_bit);
+}
+
 // alt conv6 = ref conv6 (act6, 106 rows per window) with rows [r6, r6+20) from the alt run
 __global__ __launch_bounds__(256) void pair_patch_apply(const float* __restrict__ d6, float* __restrict__ act6, int nv,
                                                         int v0, const int* __restrict__ var_pos, int row16) {
@@ -669,8 +679,16 @@ struct expecto_beluga {
   int f16_target = 10;
   bool f16_ready = false;
   int* ovf = nullptr;
+  bool ovf_deferred = false;     // leave the flag for expecto_beluga_overflow_pending (no sync per call)
   float* calib = nullptr;        // calibration windows' codes, outputs and maxima
   long long fallbacks = 0;
+  // Host tables of a segment call go through pinned staging (two slots, each reused once the
+  // event after its copies has fired), so the call returns without a host sync.
+  void* stage_buf[2] = {};
+  size_t stage_cap[2] = {};
+  hipEvent_t stage_ev[2] = {};
+  int stage_next = 0;
+  double* macs_d = nullptr;      // executed-MAC counters summed on the device (alt FC1 slab share)
   float* P = nullptr;
   float* Q = nullptr;
   float* part = nullptr;
@@ -729,6 +747,43 @@ int dalloc(expecto_beluga* h, float** p, size_t nfloat) {
 }
 
 int npad_of(int n) { return (n + GBN - 1) / GBN * GBN; }
+
+// Host -> device copies of one call's tables through a pinned staging slot.  The slot was last
+// filled two calls ago; its event fires once those copies ran (they precede that call's kernels
+// on the stream), so the wait is normally already satisfied.
+struct HostCopy {
+  void* dst;
+  const void* src;
+  size_t bytes;
+};
+int stage_copies(expecto_beluga* h, const std::vector<HostCopy>& cp, hipStream_t st) {
+  size_t total = 0;
+  for (const HostCopy& c : cp) total += (c.bytes + 15) / 16 * 16;
+  if (total == 0) return EXPECTO_OK;
+  const int s = h->stage_next;
+  h->stage_next ^= 1;
+  if (h->stage_ev[s])
+    EXPECTO_HIP_CHECK(hipEventSynchronize(h->stage_ev[s]));
+  else
+    EXPECTO_HIP_CHECK(hipEventCreateWithFlags(&h->stage_ev[s], hipEventDisableTiming));
+  if (h->stage_cap[s] < total) {
+    if (h->stage_buf[s]) EXPECTO_HIP_CHECK(hipHostFree(h->stage_buf[s]));
+    h->stage_buf[s] = nullptr;
+    h->stage_cap[s] = 0;
+    const size_t cap = std::max<size_t>(total + total / 4, 1 << 16);
+    EXPECTO_HIP_CHECK(hipHostMalloc(&h->stage_buf[s], cap, hipHostMallocDefault));
+    h->stage_cap[s] = cap;
+  }
+  char* p = static_cast<char*>(h->stage_buf[s]);
+  for (const HostCopy& c : cp) {
+    if (c.bytes == 0) continue;
+    std::memcpy(p, c.src, c.bytes);
+    EXPECTO_HIP_CHECK(hipMemcpyAsync(c.dst, p, c.bytes, hipMemcpyHostToDevice, st));
+    p += (c.bytes + 15) / 16 * 16;
+  }
+  EXPECTO_HIP_CHECK(hipEventRecord(h->stage_ev[s], st));
+  return EXPECTO_OK;
+}
 
 // floats to allocate for `elements` activation elements in either format (6 B per bf16x6 element)
 size_t act_alloc(size_t elements) { return elements + (elements + 1) / 2; }
@@ -994,6 +1049,21 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
   return EXPECTO_OK;
 }
 
+// Profiling: the executed MACs of an alt FC1 that runs only the masked split-K slabs of its
+// `tiles` M tiles (nb rows) go to the device counter of the fc1_delta slot.
+int count_slab_macs(expecto_beluga* h, const unsigned* mask, int tiles, long long nb, hipStream_t st) {
+  if (!h->macs_d) {
+    float* f = nullptr;
+    int rc = dalloc(h, &f, 4 * kNumLayers);
+    if (rc) return rc;
+    h->macs_d = reinterpret_cast<double*>(f);
+    EXPECTO_HIP_CHECK(hipMemsetAsync(h->macs_d, 0, 2 * kNumLayers * sizeof(double), st));
+  }
+  const double per_bit = (double)nb * kFc1Out * kFc1In / ((double)tiles * h->fc_splits);
+  slab_macs<<<dim3(1), dim3(64), 0, st>>>(mask, tiles, per_bit, h->macs_d + kNumLayers + 6);   // fc1_delta
+  return check_launch("slab_macs");
+}
+
 // One chunk of nb independent windows; conv1 input from x (one-hot) or codes.
 int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long long code_stride, int n_src,
                   int mode, long long row0, int nb, float* y, hipStream_t st) {
@@ -1131,19 +1201,19 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
       EXPECTO_HIP_CHECK(hipMalloc(&h->seg_var_d, n_seg * sizeof(int)));
       h->seg_var_cap = n_seg;
     }
-    EXPECTO_HIP_CHECK(hipMemcpyAsync(h->seg_var_d, pr->var_pos, n_seg * sizeof(int), hipMemcpyHostToDevice, st));
-    if (!alt_w.empty())
-      EXPECTO_HIP_CHECK(hipMemcpyAsync(h->alt_w_d, alt_w.data(), alt_w.size() * sizeof(int), hipMemcpyHostToDevice, st));
-    if (!copy_w.empty())
-      EXPECTO_HIP_CHECK(
-          hipMemcpyAsync(h->copy_w_d, copy_w.data(), copy_w.size() * sizeof(int), hipMemcpyHostToDevice, st));
+  }
+  std::vector<HostCopy> copies;   // staged once the FC row order is known (below)
+  if (pr) {
+    copies.push_back({h->seg_var_d, pr->var_pos, n_seg * sizeof(int)});
+    copies.push_back({h->alt_w_d, alt_w.data(), alt_w.size() * sizeof(int)});
+    copies.push_back({h->copy_w_d, copy_w.data(), copy_w.size() * sizeof(int)});
   }
   if (win_row) {
     for (int w = 0; w < n_win; ++w) EXPECTO_REQUIRE(win_row[w] >= 0 && win_row[w] < n_win, "window row out of range");
-    EXPECTO_HIP_CHECK(hipMemcpyAsync(h->win_row_d, win_row, n_win * sizeof(int), hipMemcpyHostToDevice, st));
+    copies.push_back({h->win_row_d, win_row, n_win * sizeof(int)});
   }
-  EXPECTO_HIP_CHECK(hipMemcpyAsync(h->win_seg_d, win_seg, n_win * sizeof(int), hipMemcpyHostToDevice, st));
-  EXPECTO_HIP_CHECK(hipMemcpyAsync(h->win_off_d, win_off, n_win * sizeof(int), hipMemcpyHostToDevice, st));
+  copies.push_back({h->win_seg_d, win_seg, n_win * sizeof(int)});
+  copies.push_back({h->win_off_d, win_off, n_win * sizeof(int)});
   const int strands = mode == EXPECTO_STRAND_BOTH ? 2 : 1;
   // alt runs: one block per segment (conv1..4) or per (segment, phase) (pool2, conv5, conv6)
   const int blk_per_seg = pr ? std::max(n_ph, 1) : 0;
@@ -1185,11 +1255,10 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
           if (!is_alt[w]) out[k++] = w;
       }
     }
-    EXPECTO_HIP_CHECK(hipMemcpyAsync(h->fc_perm_d, fc_perm.data(), fc_perm.size() * sizeof(int),
-                                     hipMemcpyHostToDevice, st));
+    copies.push_back({h->fc_perm_d, fc_perm.data(), fc_perm.size() * sizeof(int)});
   }
-  // the tables are caller-owned pageable host memory: finish the copies before returning
-  EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
+  // the tables are caller-owned (and local) host memory: stage them through pinned memory
+  if ((rc = stage_copies(h, copies, st))) return rc;
   const long long strand_rows = pr ? pr->strand_stride : n_win;
   const int eb = act_bytes();
   hipStream_t sa = (pr && h->st2) ? h->st2 : st;     // alt runs of segment pairs
@@ -1329,13 +1398,9 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
                   kFc1In / h->fc_splits, md);
               if ((rc = check_launch("fc1_slab_mask_seg"))) return rc;
               mask = md;
-              if (h->profiling) {   // executed share of the slabs, for the MAC count
-                std::vector<unsigned> hm(tiles);
-                EXPECTO_HIP_CHECK(hipMemcpyAsync(hm.data(), md, tiles * sizeof(unsigned), hipMemcpyDeviceToHost, st));
-                EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
-                int bits = 0;
-                for (unsigned x : hm) bits += __builtin_popcount(x);
-                frac = (double)bits / (tiles * h->fc_splits);
+              if (h->profiling) {   // executed share of the slabs, counted on the device (no sync)
+                if ((rc = count_slab_macs(h, md, tiles, n_alt, st))) return rc;
+                frac = 0.0;
               }
             }
             DeltaScope ds(h);
@@ -1420,13 +1485,9 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
                                                                   kFc1In / h->fc_splits, md);
       if ((rc = check_launch("fc1_slab_mask"))) return rc;
       mask = md;
-      if (h->profiling) {   // executed share of the slabs, for the MAC count
-        std::vector<unsigned> hm(tiles);
-        EXPECTO_HIP_CHECK(hipMemcpyAsync(hm.data(), md, tiles * sizeof(unsigned), hipMemcpyDeviceToHost, st));
-        EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
-        int bits = 0;
-        for (unsigned x : hm) bits += __builtin_popcount(x);
-        frac = (double)bits / (tiles * h->fc_splits);
+      if (h->profiling) {   // executed share of the slabs, counted on the device (no sync)
+        if ((rc = count_slab_macs(h, md, tiles, R, st))) return rc;
+        frac = 0.0;
       }
     }
     DeltaScope ds(h);
@@ -1540,10 +1601,11 @@ int f16_prepare(expecto_beluga* h, hipStream_t st) {
 }
 
 // Run one public call; on the f16x3 path check the overflow flag afterwards and, if an
-// activation did not fit fp16, recompute the whole call with bf16x6.
+// activation did not fit fp16, recompute the whole call with bf16x6.  In deferred mode the
+// flag stays on the device for expecto_beluga_overflow_pending (the caller's release point).
 template <class F>
 int run_checked(expecto_beluga* h, hipStream_t st, F&& fn) {
-  if (h->precision != EXPECTO_PRECISION_F16X3) return fn();
+  if (h->precision != EXPECTO_PRECISION_F16X3 || h->ovf_deferred) return fn();
   int rc = fn();
   if (rc) return rc;
   int flag = 0;
@@ -1654,6 +1716,11 @@ void expecto_beluga_destroy(expecto_beluga_t h) {
   for (hipEvent_t e : h->pev)
     if (e) (void)hipEventDestroy(e);
   if (h->st2) (void)hipStreamDestroy(h->st2);
+  for (int s = 0; s < 2; ++s) {
+    if (h->stage_ev[s]) (void)hipEventSynchronize(h->stage_ev[s]);
+    if (h->stage_buf[s]) (void)hipHostFree(h->stage_buf[s]);
+    if (h->stage_ev[s]) (void)hipEventDestroy(h->stage_ev[s]);
+  }
   delete h;
 }
 
@@ -1802,6 +1869,10 @@ int expecto_beluga_set_profiling(expecto_beluga_t h, int on) {
   }
   h->profiling = on != 0;
   if (on) {
+    if (h->macs_d) {
+      EXPECTO_HIP_CHECK(hipDeviceSynchronize());
+      EXPECTO_HIP_CHECK(hipMemset(h->macs_d, 0, 2 * kNumLayers * sizeof(double)));
+    }
     std::fill(h->ms, h->ms + 2 * kNumLayers, 0.0);
     std::fill(h->calls, h->calls + 2 * kNumLayers, 0LL);
     std::fill(h->macs, h->macs + 2 * kNumLayers, 0.0);
@@ -1813,13 +1884,40 @@ int expecto_beluga_layer_times(expecto_beluga_t h, double* ms, long long* calls,
   EXPECTO_REQUIRE(h != nullptr, "null handle");
   int rc = resolve_events(h);
   if (rc) return rc;
+  double dm[2 * kNumLayers] = {};
+  if (h->macs_d) {   // device-side counts (alt FC1 slab share); the events above are resolved
+    EXPECTO_HIP_CHECK(hipDeviceSynchronize());
+    EXPECTO_HIP_CHECK(hipMemcpy(dm, h->macs_d, sizeof(dm), hipMemcpyDeviceToHost));
+  }
   const int n = std::min(max_layers, 2 * kNumLayers);
   for (int i = 0; i < n; ++i) {
     if (ms) ms[i] = h->ms[i];
     if (calls) calls[i] = h->calls[i];
-    if (macs) macs[i] = h->macs[i];
+    if (macs) macs[i] = h->macs[i] + dm[i];
   }
   return 2 * kNumLayers;
+}
+
+int expecto_beluga_set_overflow_check(expecto_beluga_t h, int deferred) {
+  EXPECTO_REQUIRE(h != nullptr, "null handle");
+  EXPECTO_REQUIRE(deferred == 0 || deferred == 1, "deferred must be 0 or 1");
+  h->ovf_deferred = deferred != 0;
+  return EXPECTO_OK;
+}
+
+int expecto_beluga_overflow_pending(expecto_beluga_t h, void* stream) {
+  EXPECTO_REQUIRE(h != nullptr, "null handle");
+  if (!h->ovf) return 0;
+  EXPECTO_HIP_CHECK(hipSetDevice(h->device));
+  hipStream_t st = as_stream(stream);
+  int flag = 0;
+  EXPECTO_HIP_CHECK(hipMemcpyAsync(&flag, h->ovf, sizeof(int), hipMemcpyDeviceToHost, st));
+  EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
+  if (!flag) return 0;
+  EXPECTO_HIP_CHECK(hipMemsetAsync(h->ovf, 0, sizeof(int), st));
+  EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
+  h->fallbacks += 1;   // the caller recomputes the flagged calls with BF16X6
+  return 1;
 }
 
 }  // extern "C"

@@ -117,6 +117,7 @@ template <bool F64AVG, bool LEGACY>
 __global__ void shift_reduce_kernel(const float* __restrict__ fwd, const float* __restrict__ rc,
                                     const double* __restrict__ weights, int n_shift, int nfeat,
                                     double* __restrict__ out) {
+#pragma clang fp contract(off)   // products rounded before the sum, as numpy
   extern __shared__ double wsx[];  // [10][n_shift]
   for (int i = threadIdx.x; i < 10 * n_shift; i += blockDim.x) wsx[i] = weights[i];
   __syncthreads();
@@ -145,6 +146,7 @@ __global__ void shift_reduce_kernel(const float* __restrict__ fwd, const float* 
 __global__ void tss_reduce_kernel(const float* __restrict__ fwd, const float* __restrict__ rc,
                                   const double* __restrict__ weights, int n_shift, int nfeat,
                                   double* __restrict__ out) {
+#pragma clang fp contract(off)   // products rounded before the sum, as numpy
   extern __shared__ double wsh[];  // [10][n_shift]
   for (int i = threadIdx.x; i < 10 * n_shift; i += blockDim.x) wsh[i] = weights[i];
   __syncthreads();
@@ -181,6 +183,7 @@ __device__ __forceinline__ void store_nt2(double* p, double a, double b) {
 __global__ void tss_reduce2_kernel(const float* __restrict__ fwd, const float* __restrict__ rc,
                                    const double* __restrict__ weights, int n_shift, int nfeat,
                                    double* __restrict__ out) {
+#pragma clang fp contract(off)   // products rounded before the sum, as numpy
   extern __shared__ double wsh[];  // [10][n_shift]
   for (int i = threadIdx.x; i < 10 * n_shift; i += blockDim.x) wsh[i] = weights[i];
   __syncthreads();
@@ -213,11 +216,11 @@ __global__ void tss_reduce2_kernel(const float* __restrict__ fwd, const float* _
 __global__ void variant_reduce_kernel(const float* __restrict__ eff, const long long* __restrict__ dist,
                                       const uint8_t* __restrict__ strand_plus, const int* __restrict__ shifts,
                                       int n_shift, int n, int nfeat, double* __restrict__ out) {
-  __shared__ double wsh[32 * 10];
+#pragma clang fp contract(off)   // products rounded before the sum, as numpy
+  extern __shared__ double wsh[];   // [n_shift][10]
   const long long v = blockIdx.y;
   const double decay[5] = {0.01, 0.02, 0.05, 0.1, 0.2};
-  if ((int)threadIdx.x < n_shift) {
-    const int j = threadIdx.x;
+  for (int j = threadIdx.x; j < n_shift; j += blockDim.x) {
     const long long sgn = strand_plus[v] ? 1 : -1;
     const long long d = dist[v] * sgn + (long long)shifts[j] * sgn;
     const double fl = floor(fabs((double)d) / 200.0);
@@ -249,11 +252,11 @@ __global__ void variant_reduce_kernel(const float* __restrict__ eff, const long 
 __global__ void variant_reduce2_kernel(const float* __restrict__ eff, const long long* __restrict__ dist,
                                        const uint8_t* __restrict__ strand_plus, const int* __restrict__ shifts,
                                        int n_shift, int n, int nfeat, double* __restrict__ out) {
-  __shared__ double wsh[32 * 10];
+#pragma clang fp contract(off)   // products rounded before the sum, as numpy
+  extern __shared__ double wsh[];   // [n_shift][10]
   const long long v = blockIdx.y;
   const double decay[5] = {0.01, 0.02, 0.05, 0.1, 0.2};
-  if ((int)threadIdx.x < n_shift) {
-    const int j = threadIdx.x;
+  for (int j = threadIdx.x; j < n_shift; j += blockDim.x) {
     const long long sgn = strand_plus[v] ? 1 : -1;
     const long long d = dist[v] * sgn + (long long)shifts[j] * sgn;
     const double fl = floor(fabs((double)d) / 200.0);
@@ -413,17 +416,18 @@ int expecto_tss_reduce(const float* fwd, const float* rc, const double* weights,
 
 int expecto_variant_reduce(const float* effects, const long long* dist, const uint8_t* strand_plus, const int* shifts,
                            int n_shift, int n, int nfeat, double* out, void* stream) {
-  EXPECTO_REQUIRE(n >= 0 && n_shift > 0 && n_shift <= 32 && nfeat > 0, "bad shape (n_shift <= 32)");
+  EXPECTO_REQUIRE(n >= 0 && n_shift > 0 && n_shift <= 4096 && nfeat > 0, "bad shape (n_shift <= 4096)");
   if (n == 0) return EXPECTO_OK;
   EXPECTO_REQUIRE(n <= 65535, "at most 65535 variants per call");
   EXPECTO_REQUIRE(effects && dist && strand_plus && shifts && out, "null argument");
+  const size_t shm = 10 * (size_t)n_shift * sizeof(double);
   if (nfeat % 2 == 0 && (reinterpret_cast<uintptr_t>(effects) & 7) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
     dim3 grid((nfeat / 2 + 255) / 256, n);
-    variant_reduce2_kernel<<<grid, dim3(256), 0, as_stream(stream)>>>(effects, dist, strand_plus, shifts, n_shift, n,
+    variant_reduce2_kernel<<<grid, dim3(256), shm, as_stream(stream)>>>(effects, dist, strand_plus, shifts, n_shift, n,
                                                                       nfeat, out);
   } else {
     dim3 grid((nfeat + 255) / 256, n);
-    variant_reduce_kernel<<<grid, dim3(256), 0, as_stream(stream)>>>(effects, dist, strand_plus, shifts, n_shift, n,
+    variant_reduce_kernel<<<grid, dim3(256), shm, as_stream(stream)>>>(effects, dist, strand_plus, shifts, n_shift, n,
                                                                      nfeat, out);
   }
   return check_launch("variant_reduce");

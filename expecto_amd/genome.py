@@ -7,9 +7,10 @@ Contig sequences are kept as bytes (case preserved, as pyfasta does).
 
 ``DeviceGenome`` concatenates every contig's uint8 base codes (0=A 1=G 2=C 3=T 4=zero)
 into one HBM tensor (hg19 is ~3.1 GB, a few % of 288 GB), with ``GUARD`` zero codes
-between contigs, so window generation never crosses into a neighbouring contig.
-Windows running past a contig end read zero columns: pyfasta's behaviour there is not
-pinned by any fixture ("Window-edge semantics"), see DESIGN.md.
+between contigs.  Windows running up to GUARD bases past a contig end read zero columns
+(pyfasta's behaviour there is not pinned by any fixture: SURVEY.md 7, "Window-edge
+semantics"); ``check_spans`` rejects any window reaching further, so the window
+kernels never read a neighbouring contig.
 """
 from __future__ import annotations
 
@@ -19,7 +20,7 @@ import numpy as np
 
 from .encode import CODE_ZERO, _LUT
 
-GUARD = 4096
+GUARD = 32768     # > the +-21 kb reach of a TSS segment (compute_expecto_features.py:88)
 
 
 class Fasta:
@@ -97,6 +98,21 @@ class CodeGenome:
         """Flat offset of the 1-based position ``pos1`` of ``chrom``."""
         return self.offsets[chrom] + pos1 - 1
 
+    def check_spans(self, chroms, lo, hi) -> None:
+        """Raise ValueError if a window span [lo[i], hi[i]] (flat offsets) of contig chroms[i]
+        reaches more than GUARD bases outside that contig (it would read the next one)."""
+        lo = np.asarray(lo, np.int64).reshape(-1)
+        hi = np.asarray(hi, np.int64).reshape(-1)
+        if lo.size == 0:
+            return
+        start = np.array([self.offsets[c] for c in chroms], np.int64)
+        end = start + np.array([self.lengths[c] for c in chroms], np.int64)
+        bad = np.nonzero((lo < start - GUARD) | (hi >= end + GUARD))[0]
+        if bad.size:
+            i = int(bad[0])
+            raise ValueError(f"window of {chroms[i]} reaches more than {GUARD} bp past the contig "
+                             f"(offsets {int(lo[i] - start[i])}..{int(hi[i] - start[i])} of {int(end[i] - start[i])})")
+
 
 class DeviceGenome:
     """CodeGenome resident in HBM as a torch uint8 tensor."""
@@ -111,6 +127,9 @@ class DeviceGenome:
 
     def offset(self, chrom: str, pos1: int) -> int:
         return self.host.offset(chrom, pos1)
+
+    def check_spans(self, chroms, lo, hi) -> None:
+        self.host.check_spans(chroms, lo, hi)
 
 
 def open_genome(path: str) -> Fasta:

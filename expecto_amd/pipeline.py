@@ -108,19 +108,28 @@ class VariantPipeline:
         self.use_segments = use_segments
         self.use_pairs = use_pairs
 
-    def prepare(self, vs: VariantSet, shifts) -> dict:
-        """Host checks + the device-resident variant tables (done once, outside the hot loop)."""
+    def prepare(self, vs: VariantSet, shifts, rows: str = "shift") -> dict:
+        """Host checks + the device-resident variant tables (done once, outside the hot loop).
+
+        rows="shift" (chromatin.py's per-shift files): ``y[strand][allele][shift][variant]``;
+        rows="variant" (the 200-shift eQTL scoring, geuvadis_sed_for_top_eqtls.py:61-98):
+        ``y[strand][allele][variant][shift]``, so each variant's [S, 2002] block is contiguous
+        for the shift reductions.  "variant" needs SNVs on 4-aligned shifts (segment path)."""
+        if rows not in ("shift", "variant"):
+            raise ValueError("rows must be 'shift' or 'variant'")
         n, S = len(vs), len(shifts)
         shifts = list(shifts)
         snv = np.array([len(r) == 1 and len(a) == 1 for r, a in zip(vs.ref, vs.alt)], bool).reshape(-1)
         off = np.array([self.dg.offset(c, int(p)) for c, p in zip(vs.chrom, vs.pos)], np.int64).reshape(-1)
         snv_idx, ind_idx = np.nonzero(snv)[0], np.nonzero(~snv)[0]
         self._check_window_chars(off[snv_idx], shifts)
+        if n:
+            self.dg.check_spans(vs.chrom, off + min(shifts) - 999, off + max(shifts) + 1000)
         rc = np.array([_allele_code(vs.ref[v]) for v in snv_idx], np.uint8).reshape(-1)
         ac = np.array([_allele_code(vs.alt[v]) for v in snv_idx], np.uint8).reshape(-1)
         ns = snv_idx.size
         dev = self.device
-        prep = {"n": n, "S": S, "shifts": shifts, "snv_idx": torch.from_numpy(snv_idx).to(dev),
+        prep = {"n": n, "S": S, "shifts": shifts, "rows": rows, "snv_idx": torch.from_numpy(snv_idx).to(dev),
                 "ind_idx": torch.from_numpy(ind_idx).to(dev), "n_snv": ns, "n_ind": ind_idx.size,
                 "seg": None, "win": None, "ind_codes": None}
         lo_s, hi_s = min(shifts), max(shifts)
@@ -139,7 +148,7 @@ class VariantPipeline:
                     "var_pos": np.full(ns, 999 - lo_s, np.int32),
                     "win_seg": v_i.ravel().astype(np.int32),
                     "win_off": (np.asarray(shifts)[j_i.ravel()] - lo_s).astype(np.int32),
-                    "win_row": (j_i * ns + v_i).ravel().astype(np.int32),
+                    "win_row": ((j_i * ns + v_i) if rows == "shift" else (v_i * S + j_i)).ravel().astype(np.int32),
                 }
             else:
                 # segment a*ns + v; window (a, v, j) at offset shifts[j] - lo_s -> row (a*S + j)*ns + v
@@ -151,12 +160,15 @@ class VariantPipeline:
                     "splice_code": torch.from_numpy(np.concatenate([rc, ac])).to(dev),
                     "win_seg": (a_i * ns + v_i).ravel().astype(np.int32),
                     "win_off": (np.asarray(shifts)[j_i.ravel()] - lo_s).astype(np.int32),
-                    "win_row": ((a_i * S + j_i) * ns + v_i).ravel().astype(np.int32),
+                    "win_row": (((a_i * S + j_i) * ns + v_i) if rows == "shift" else
+                                ((a_i * ns + v_i) * S + j_i)).ravel().astype(np.int32),
                 }
         elif ns:
             prep["win"] = {"off": torch.from_numpy(off[snv_idx]).to(dev), "rc": torch.from_numpy(rc).to(dev),
                            "ac": torch.from_numpy(ac).to(dev),
                            "sh": torch.tensor(shifts, dtype=torch.int32, device=dev)}
+        if rows == "variant" and (prep["seg"] is None or ind_idx.size):
+            raise ValueError('rows="variant" needs SNVs on 4-aligned shifts (the segment path)')
         if ind_idx.size:
             # indels / MNPs: length-changing splice + floor crop on the host (chromatin.py:164,209)
             host = np.empty((2, S, ind_idx.size, 2000), np.uint8)
@@ -205,7 +217,8 @@ class VariantPipeline:
         prep = vs if isinstance(vs, dict) else self.prepare(vs, shifts)
         n, S, ns, ni = prep["n"], prep["S"], prep["n_snv"], prep["n_ind"]
         if out is None:
-            out = torch.empty((2, 2, S, n, 2002), dtype=torch.float32, device=self.device)
+            shape = (2, 2, S, n, 2002) if prep.get("rows", "shift") == "shift" else (2, 2, n, S, 2002)
+            out = torch.empty(shape, dtype=torch.float32, device=self.device)
         if ns:
             y = out if ni == 0 else torch.empty((2, 2, S, ns, 2002), dtype=torch.float32, device=self.device)
             seg = prep["seg"]
@@ -241,6 +254,28 @@ class VariantPipeline:
             self.engine.forward_codes(prep["ind_codes"].view(2 * S * ni, 2000), _lib.STRAND_BOTH,
                                       out=yi.view(4 * S * ni, 2002))
             out.index_copy_(3, prep["ind_idx"], yi)
+        return out
+
+    def sed_features(self, y: torch.Tensor, weights: torch.Tensor, out: torch.Tensor | None = None,
+                     legacy: bool = True) -> torch.Tensor:
+        """Per-allele eQTL features of a rows="variant" prediction y[2, 2, n, S, 2002]:
+        float64 fwd/rc mean, then the 10 x S exp-decay shift reduction
+        (geuvadis_sed_for_top_eqtls.py:83-121); out [2 alleles, n, 20030] (legacy layout, a zero
+        column ahead of each decay block) or [2, n, 20020]."""
+        _, _, n, S, F = y.shape
+        width = 10 * (F + (1 if legacy else 0))
+        if out is None:
+            out = torch.empty((2, n, width), dtype=torch.float64, device=y.device)
+        if not (y.is_contiguous() and out.is_contiguous() and tuple(out.shape) == (2, n, width)):
+            raise RuntimeError("sed_features: y must be contiguous [2,2,n,S,2002], out [2,n,width]")
+        st = _lib.stream_ptr()
+        flags = 1 | (2 if legacy else 0)          # EXPECTO_REDUCE_F64AVG | EXPECTO_REDUCE_LEGACY20030
+        for a in range(2):
+            for v0 in range(0, n, 65535):
+                v1 = min(n, v0 + 65535)
+                _lib.check(self.lib.expecto_shift_reduce(_lib.dptr(y[0, a, v0:v1]), _lib.dptr(y[1, a, v0:v1]),
+                                                         _lib.dptr(weights), v1 - v0, S, F, flags,
+                                                         _lib.dptr(out[a, v0:v1]), st), "shift_reduce")
         return out
 
     def diff(self, y: torch.Tensor) -> torch.Tensor:

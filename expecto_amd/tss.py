@@ -40,9 +40,14 @@ class TSSPipeline:
         self.sh_d = torch.tensor(self.shifts, dtype=torch.int32, device=self.dev)
         self.w_d = torch.from_numpy(tss_pos_weights(self.shifts)).to(self.dev)
 
+    def _check(self, chroms, off, strands):
+        rel = np.asarray(self.shifts, np.int64)[None, :] * np.asarray(strands, np.int64).reshape(-1, 1)
+        self.dg.check_spans(list(chroms), off + rel.min(1) - 999, off + rel.max(1) + 1000)
+
     def window_codes(self, chroms, tss, strands) -> torch.Tensor:
         G, S = len(chroms), len(self.shifts)
         off = np.array([self.dg.offset(c, int(t)) for c, t in zip(chroms, tss)], np.int64)
+        self._check(chroms, off, strands)
         codes = torch.empty((G, S, 2000), dtype=torch.uint8, device=self.dev)
         if G:
             # keep the argument tensors referenced until the launch is queued (a temporary's
@@ -67,6 +72,7 @@ class TSSPipeline:
         if use_segments and all((x - sh.min()) % 4 == 0 for x in sh):
             strands = np.asarray(strands, np.int64)
             off = np.array([self.dg.offset(c, int(t)) for c, t in zip(chroms, tss)], np.int64)
+            self._check(chroms, off, strands)
             rel = sh[None, :] * strands[:, None]                  # window start - (tss_off - 999)
             lo = rel.min(1)
             L = 2000 + int((rel.max(1) - lo).max())

@@ -165,6 +165,17 @@ int expecto_beluga_set_f16_target(expecto_beluga_t h, int target_log2);
  * returns the number of calls recomputed with BF16X6 after an overflow (or < 0 on error). */
 long long expecto_beluga_f16_fallbacks(expecto_beluga_t h, int* sx);
 
+/* F16X3 overflow check mode.  deferred = 0 (default): every forward call reads the device
+ * overflow flag when its kernels are done (one stream sync per call) and recomputes itself with
+ * BF16X6 if an activation did not fit fp16, so outputs are final when the call returns.
+ * deferred = 1: calls only enqueue work (no host sync inside a forward); the flag stays set on
+ * the device until expecto_beluga_overflow_pending() is called at the caller's release point
+ * (before outputs are copied out), which syncs `stream`, returns 1 if any call since the last
+ * check overflowed (and clears the flag; the caller then recomputes those calls with BF16X6),
+ * else 0 (< 0 on error). */
+int expecto_beluga_set_overflow_check(expecto_beluga_t h, int deferred);
+int expecto_beluga_overflow_pending(expecto_beluga_t h, void* stream);
+
 /* Per-layer device time accumulated over forward calls while profiling is on (ms), launches
  * (`calls`) and executed multiply-adds (`macs`: GEMM M x N x K actually run, including the
  * few padding rows; reuse paths execute fewer than the dense per-window count).

@@ -32,8 +32,7 @@ def test_reported_kernel_names_exist_in_the_committed_kernel_trace():
 
 def test_committed_traffic_matches_the_default_workload_key():
     import bench
-    from expecto_amd.pipeline import shift_order
-    key = {"variants": 1000, "shifts": shift_order(0), "precision": "f16x3", "max_batch": bench.MAX_BATCH}
+    key = {"workload": "sed200", "variants": bench.N200, "precision": "f16x3", "max_batch": bench.MAX_BATCH}
     traffic, src = bench.pmc_traffic(key, bench.kernel_name("conv2", "f16x3"))
     assert traffic is not None and traffic > 0, "re-take profiles: tools/profile_round.sh + collect_profiles.py"
     assert src.startswith("profiles/")
