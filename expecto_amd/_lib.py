@@ -47,6 +47,7 @@ SIGNATURES = {
     "expecto_beluga_f16_fallbacks": (ctypes.c_longlong, [c_vp, c_i32p]),
     "expecto_beluga_set_overflow_check": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "expecto_beluga_overflow_pending": (ctypes.c_int, [c_vp, c_vp]),
+    "expecto_beluga_overflow_take": (ctypes.c_int, [c_vp, c_vp, c_vp]),
     "expecto_beluga_set_profiling": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "expecto_beluga_layer_times": (ctypes.c_int, [c_vp, c_f64p, c_i64p, c_f64p, ctypes.c_int]),
     "expecto_variant_windows": (ctypes.c_int, [c_vp, ctypes.c_longlong, c_vp, c_vp, c_vp, ctypes.c_int, c_vp,
@@ -58,6 +59,8 @@ SIGNATURES = {
     "expecto_tss_reduce": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp]),
     "expecto_variant_reduce": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                               c_vp, c_vp]),
+    "expecto_variant_reduce_lut": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                  c_vp, ctypes.c_int, c_vp, c_vp]),
     "expecto_gblinear_predict": (ctypes.c_int, [c_vp, ctypes.c_longlong, ctypes.c_longlong, c_vp, ctypes.c_int,
                                                 c_vp, ctypes.c_float, c_vp, c_vp]),
     "expecto_shift_reduce": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,

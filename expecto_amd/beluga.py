@@ -99,6 +99,15 @@ class BelugaEngine:
             _lib.check(int(r), "overflow_pending")
         return bool(r)
 
+    def overflow_take(self, dst: torch.Tensor, stream=None):
+        """Deferred mode: enqueue a copy of the overflow flag into ``dst`` (an int32 tensor of one
+        element, pinned host or device) and reset the flag, with no host sync."""
+        if dst.dtype != torch.int32 or dst.numel() != 1 or not (dst.is_cuda or dst.is_pinned()):
+            raise RuntimeError("overflow_take: dst must be a pinned-host or device int32 tensor of one element")
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.expecto_beluga_overflow_take(self.handle, ctypes.c_void_p(dst.data_ptr()),
+                                                             _lib.stream_ptr(stream)), "overflow_take")
+
     def precision_override(self, precision: str):
         """Context manager: run the enclosed calls in another arithmetic, then restore."""
         import contextlib

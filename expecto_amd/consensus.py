@@ -207,7 +207,10 @@ def _extra_args(p):
 
 
 # ---- geuvadis_sed_for_top_eqtls.py --------------------------------------------------------
-def sed_main(argv=None):
+def sed_main(argv=None, capture: dict | None = None):
+    """geuvadis_sed_for_top_eqtls.py main() (:21-135).  ``capture`` (a dict, for tests) receives
+    the per-batch window predictions ("y_ref"/"y_alt": [2 strands, n, 200, 2002] f32) and the
+    features ("x_ref"/"x_alt": [n, 20030] f64) the scores were computed from."""
     p = argparse.ArgumentParser(description='Predict expression for consensus sequences using ExPecto')
     p.add_argument('expecto_model')
     p.add_argument('consensus_dir')
@@ -244,9 +247,12 @@ def sed_main(argv=None):
             y_ref = scorer.predict(seqs, strands)
             alts = [s[:i] + a + s[i + 1:] for s, _, i, a in batch]
             y_alt = scorer.predict(alts, strands)
-        for y, dst in ((y_ref, ref_pred), (y_alt, alt_pred)):
+        for y, dst, tag in ((y_ref, ref_pred, "ref"), (y_alt, alt_pred, "alt")):
             x = scorer.features(y)
             dst.append(bst.predict(x).cpu().numpy())
+            if capture is not None:
+                capture.setdefault(f"y_{tag}", []).append(y.cpu().numpy())
+                capture.setdefault(f"x_{tag}", []).append(x.cpu().numpy())
         batch.clear()
 
     for i in range(eqtls_df.shape[0]):

@@ -1905,6 +1905,16 @@ int expecto_beluga_set_overflow_check(expecto_beluga_t h, int deferred) {
   return EXPECTO_OK;
 }
 
+int expecto_beluga_overflow_take(expecto_beluga_t h, int* dst, void* stream) {
+  EXPECTO_REQUIRE(h != nullptr && dst != nullptr, "null argument");
+  EXPECTO_HIP_CHECK(hipSetDevice(h->device));
+  hipStream_t st = as_stream(stream);
+  EXPECTO_REQUIRE(h->ovf != nullptr, "no overflow flag (f16x3 never prepared)");
+  EXPECTO_HIP_CHECK(hipMemcpyAsync(dst, h->ovf, sizeof(int), hipMemcpyDefault, st));
+  EXPECTO_HIP_CHECK(hipMemsetAsync(h->ovf, 0, sizeof(int), st));
+  return EXPECTO_OK;
+}
+
 int expecto_beluga_overflow_pending(expecto_beluga_t h, void* stream) {
   EXPECTO_REQUIRE(h != nullptr, "null handle");
   if (!h->ovf) return 0;

@@ -215,7 +215,8 @@ __global__ void tss_reduce2_kernel(const float* __restrict__ fwd, const float* _
 // grid: (ceil(nfeat/256), n); weights W_j[k] computed per variant in f64.
 __global__ void variant_reduce_kernel(const float* __restrict__ eff, const long long* __restrict__ dist,
                                       const uint8_t* __restrict__ strand_plus, const int* __restrict__ shifts,
-                                      int n_shift, int n, int nfeat, double* __restrict__ out) {
+                                      int n_shift, int n, int nfeat, const double* __restrict__ lut,
+                                      int lut_len, double* __restrict__ out) {
 #pragma clang fp contract(off)   // products rounded before the sum, as numpy
   extern __shared__ double wsh[];   // [n_shift][10]
   const long long v = blockIdx.y;
@@ -226,7 +227,8 @@ __global__ void variant_reduce_kernel(const float* __restrict__ eff, const long 
     const double fl = floor(fabs((double)d) / 200.0);
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-      const double e = exp(-decay[k] * fl);
+      // host table exp(-c_k * fl) (numpy's exp, as predict.py:88-107) when given, else the device exp
+      const double e = lut ? lut[k * lut_len + (long long)fl] : exp(-decay[k] * fl);
       wsh[j * 10 + k] = d <= 0 ? e : 0.0;
       wsh[j * 10 + 5 + k] = d >= 0 ? e : 0.0;
     }
@@ -251,7 +253,8 @@ __global__ void variant_reduce_kernel(const float* __restrict__ eff, const long 
 // the 9 x 10 weights, float2 loads and double2 stores; bitwise equal to variant_reduce_kernel.
 __global__ void variant_reduce2_kernel(const float* __restrict__ eff, const long long* __restrict__ dist,
                                        const uint8_t* __restrict__ strand_plus, const int* __restrict__ shifts,
-                                       int n_shift, int n, int nfeat, double* __restrict__ out) {
+                                       int n_shift, int n, int nfeat, const double* __restrict__ lut,
+                                       int lut_len, double* __restrict__ out) {
 #pragma clang fp contract(off)   // products rounded before the sum, as numpy
   extern __shared__ double wsh[];   // [n_shift][10]
   const long long v = blockIdx.y;
@@ -262,7 +265,8 @@ __global__ void variant_reduce2_kernel(const float* __restrict__ eff, const long
     const double fl = floor(fabs((double)d) / 200.0);
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-      const double e = exp(-decay[k] * fl);
+      // host table exp(-c_k * fl) (numpy's exp, as predict.py:88-107) when given, else the device exp
+      const double e = lut ? lut[k * lut_len + (long long)fl] : exp(-decay[k] * fl);
       wsh[j * 10 + k] = d <= 0 ? e : 0.0;
       wsh[j * 10 + 5 + k] = d >= 0 ? e : 0.0;
     }
@@ -414,23 +418,30 @@ int expecto_tss_reduce(const float* fwd, const float* rc, const double* weights,
   return check_launch("tss_reduce");
 }
 
-int expecto_variant_reduce(const float* effects, const long long* dist, const uint8_t* strand_plus, const int* shifts,
-                           int n_shift, int n, int nfeat, double* out, void* stream) {
+int expecto_variant_reduce_lut(const float* effects, const long long* dist, const uint8_t* strand_plus,
+                               const int* shifts, int n_shift, int n, int nfeat, const double* exp_lut, int lut_len,
+                               double* out, void* stream) {
   EXPECTO_REQUIRE(n >= 0 && n_shift > 0 && n_shift <= 4096 && nfeat > 0, "bad shape (n_shift <= 4096)");
   if (n == 0) return EXPECTO_OK;
   EXPECTO_REQUIRE(n <= 65535, "at most 65535 variants per call");
   EXPECTO_REQUIRE(effects && dist && strand_plus && shifts && out, "null argument");
+  EXPECTO_REQUIRE(!exp_lut || lut_len > 0, "empty exp table");
   const size_t shm = 10 * (size_t)n_shift * sizeof(double);
   if (nfeat % 2 == 0 && (reinterpret_cast<uintptr_t>(effects) & 7) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
     dim3 grid((nfeat / 2 + 255) / 256, n);
     variant_reduce2_kernel<<<grid, dim3(256), shm, as_stream(stream)>>>(effects, dist, strand_plus, shifts, n_shift, n,
-                                                                      nfeat, out);
+                                                                      nfeat, exp_lut, lut_len, out);
   } else {
     dim3 grid((nfeat + 255) / 256, n);
     variant_reduce_kernel<<<grid, dim3(256), shm, as_stream(stream)>>>(effects, dist, strand_plus, shifts, n_shift, n,
-                                                                     nfeat, out);
+                                                                     nfeat, exp_lut, lut_len, out);
   }
   return check_launch("variant_reduce");
+}
+
+int expecto_variant_reduce(const float* effects, const long long* dist, const uint8_t* strand_plus, const int* shifts,
+                           int n_shift, int n, int nfeat, double* out, void* stream) {
+  return expecto_variant_reduce_lut(effects, dist, strand_plus, shifts, n_shift, n, nfeat, nullptr, 0, out, stream);
 }
 
 int expecto_gblinear_predict(const double* X, long long n, long long ld, const int* cols, int ncols, const float* w,

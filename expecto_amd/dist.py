@@ -87,3 +87,27 @@ def gather_rows_to(t: torch.Tensor, dim: int, n_total: int, world: int, rank: in
     parts = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
     dist.gather(pad, parts, dst=dst)
     return _unpad(parts, dim, n_total, world) if rank == dst else None
+
+
+def gather_blocks_to(t: torch.Tensor, dim: int, counts, world: int, rank: int, dst: int = 0):
+    """Gather variable-size blocks along `dim` to rank `dst`: rank r holds counts[r] rows (a
+    streamed batch of its shard; 0 allowed).  Blocks are padded to max(counts) for one gather
+    (RCCL on the GPU, gloo on the host); returns the list of rank blocks (rank order) on `dst`,
+    None elsewhere."""
+    import torch.distributed as dist
+
+    if world == 1:
+        return [t]
+    m = max(counts)
+    x = t.movedim(dim, 0)
+    if x.shape[0] != counts[rank]:
+        raise ValueError(f"rank {rank} holds {x.shape[0]} rows, counts say {counts[rank]}")
+    pad = torch.zeros((m,) + tuple(x.shape[1:]), dtype=t.dtype, device=t.device)
+    pad[: x.shape[0]] = x
+    if pad.is_cuda and dist.get_backend() == "gloo":
+        pad = pad.cpu()       # gloo gathers host tensors only (CPU tests, one-GPU rehearsals)
+    parts = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
+    dist.gather(pad, parts, dst=dst)
+    if rank != dst:
+        return None
+    return [parts[r][: counts[r]].movedim(0, dim) for r in range(world)]

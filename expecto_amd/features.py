@@ -63,10 +63,23 @@ def variant_features(effects: torch.Tensor, dist, strand_plus, shifts, out: torc
     sh = torch.as_tensor(np.asarray(list(shifts), np.int32), device=dev)
     if out is None:
         out = torch.empty((n, 10 * F), dtype=torch.float64, device=dev)
+    lut = torch.from_numpy(decay_table(dist, strand_plus, shifts)).to(dev)
     for v0 in range(0, n, 65535):
         v1 = min(n, v0 + 65535)
         eff = effects[:, v0:v1].contiguous() if (v0 or v1 != n) else effects
-        _lib.check(lib.expecto_variant_reduce(_lib.dptr(eff), _lib.dptr(d[v0:v1]), _lib.dptr(sp[v0:v1]),
-                                              _lib.dptr(sh), S, v1 - v0, F, _lib.dptr(out[v0:v1]),
-                                              _lib.stream_ptr()), "variant_reduce")
+        _lib.check(lib.expecto_variant_reduce_lut(_lib.dptr(eff), _lib.dptr(d[v0:v1]), _lib.dptr(sp[v0:v1]),
+                                                  _lib.dptr(sh), S, v1 - v0, F, _lib.dptr(lut), lut.shape[1],
+                                                  _lib.dptr(out[v0:v1]), _lib.stream_ptr()), "variant_reduce")
     return out
+
+
+def decay_table(dist, strand_plus, shifts) -> np.ndarray:
+    """[5, K] float64 exp(-c_k * fl) for fl = 0..K-1, K covering every floor(|d|/200) of the
+    batch (d = dist*sgn + shift*sgn): numpy's exp of the arguments predict.py:88-107 passes it,
+    so the device reduction reproduces the reference's weights exactly."""
+    sgn = np.where(np.asarray(strand_plus, bool), 1, -1).astype(np.int64)
+    d = np.asarray(dist, np.int64) * sgn
+    sh = np.asarray(list(shifts), np.int64)
+    reach = int(np.abs(d).max(initial=0)) + int(np.abs(sh).max(initial=0))
+    fl = np.arange(int(np.floor(reach / 200.0)) + 1, dtype=np.float64)
+    return np.ascontiguousarray(np.stack([np.exp(-c * fl) for c in (0.01, 0.02, 0.05, 0.1, 0.2)]))

@@ -56,16 +56,12 @@ def _dataset_header(shape, dt, data_addr, nbytes) -> bytes:
     return struct.pack("<BBHII4x", 1, 0, len(msgs), 1, len(body)) + body
 
 
-def write(path: str, datasets: dict) -> None:
-    """Write ``{name: ndarray}`` (float32/float64, C-contiguous) as root datasets."""
-    names = sorted(datasets)                      # symbol-table entries are name-ordered
-    arrays = [np.array(datasets[n], order="C", copy=True) for n in names]   # 0-d arrays -> scalar dataspace
-    for a in arrays:
-        if a.dtype not in (np.float32, np.float64) and a.dtype.kind != "S":
-            raise TypeError(f"{a.dtype}: only float32/float64/'S' datasets are supported")
+def _layout(names, shapes, dtypes):
+    """(header bytes, data addresses, eof) of root datasets `names` (sorted) with the given shapes
+    and dtypes: everything ahead of the first data byte, and where each dataset's data goes."""
     if len(names) > 2 * _LEAF_K:
         raise ValueError("at most 8 datasets per file in this minimal writer")
-
+    nbytes = [int(np.prod(sh, dtype=np.int64)) * dt.itemsize for sh, dt in zip(shapes, dtypes)]
     # heap data segment: "" at 0 then each name, 8-byte padded
     heap = b"\0" * 8
     name_off = []
@@ -84,18 +80,17 @@ def write(path: str, datasets: dict) -> None:
     snod_size = 8 + 2 * _LEAF_K * 40
     ds_oh = []
     pos = snod + snod_size
-    dummy = [_dataset_header(a.shape, a.dtype, 0, 0) for a in arrays]
-    for d in dummy:
+    for sh, dt in zip(shapes, dtypes):
         ds_oh.append(pos)
-        pos += len(d)
+        pos += len(_dataset_header(sh, dt, 0, 0))
     data_addr = []
     pos = (pos + _DATA_ALIGN - 1) // _DATA_ALIGN * _DATA_ALIGN
-    for a in arrays:
+    for nb in nbytes:
         data_addr.append(pos)
-        pos += a.nbytes
+        pos += nb
     eof = pos
 
-    header_len = data_addr[0] if arrays else eof
+    header_len = data_addr[0] if names else eof
     out = bytearray(header_len)
     sb = _SIG + struct.pack("<BBBBBBBB", 0, 0, 0, 0, 0, 8, 8, 0) + struct.pack("<HHI", _LEAF_K, _INTERNAL_K, 0)
     sb += struct.pack("<QQQQ", 0, UNDEF, eof, UNDEF)
@@ -114,16 +109,78 @@ def write(path: str, datasets: dict) -> None:
     for i in range(len(names)):
         sn += struct.pack("<QQI4x16x", name_off[i], ds_oh[i], 0)
     out[snod:snod + len(sn)] = sn
-    for i, a in enumerate(arrays):
-        hdr = _dataset_header(a.shape, a.dtype, data_addr[i], a.nbytes)
+    for i in range(len(names)):
+        hdr = _dataset_header(shapes[i], dtypes[i], data_addr[i], nbytes[i])
         out[ds_oh[i]:ds_oh[i] + len(hdr)] = hdr
+    return bytes(out), data_addr, eof
+
+
+def _check_dtype(dt):
+    if dt not in (np.float32, np.float64) and dt.kind != "S":
+        raise TypeError(f"{dt}: only float32/float64/'S' datasets are supported")
+
+
+def write(path: str, datasets: dict) -> None:
+    """Write ``{name: ndarray}`` (float32/float64, C-contiguous) as root datasets."""
+    names = sorted(datasets)                      # symbol-table entries are name-ordered
+    arrays = [np.array(datasets[n], order="C", copy=True) for n in names]   # 0-d arrays -> scalar dataspace
+    for a in arrays:
+        _check_dtype(a.dtype)
+    head, data_addr, _ = _layout(names, [a.shape for a in arrays], [a.dtype for a in arrays])
     with open(path, "wb") as f:
-        f.write(out)
+        f.write(head)
         for i, a in enumerate(arrays):
             cur = f.tell()
             if cur < data_addr[i]:
                 f.write(b"\0" * (data_addr[i] - cur))
             f.write(a.tobytes() if a.dtype.kind == "S" else a.astype(a.dtype.newbyteorder("<"), copy=False).tobytes())
+
+
+class RowWriter:
+    """A file of fixed-shape root datasets filled row block by row block (streamed outputs).
+
+    ``RowWriter(path, {name: (shape, dtype)})`` writes the header and sizes the file (unwritten
+    data reads as zeros); ``write_rows(name, row0, block)`` stores ``block`` (C-contiguous, same
+    dtype, trailing dims of the dataset) at rows ``row0..`` in place.  Once every row is written
+    the file is byte-identical to ``write`` of the full arrays."""
+
+    def __init__(self, path: str, specs: dict):
+        import os
+        self.names = sorted(specs)
+        self.shapes = {n: tuple(int(x) for x in specs[n][0]) for n in self.names}
+        self.dtypes = {n: np.dtype(specs[n][1]) for n in self.names}
+        for n in self.names:
+            _check_dtype(self.dtypes[n])
+        head, addr, eof = _layout(self.names, [self.shapes[n] for n in self.names],
+                                  [self.dtypes[n] for n in self.names])
+        self.addr = dict(zip(self.names, addr))
+        self.fd = os.open(path, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o644)
+        os.pwrite(self.fd, head, 0)
+        os.ftruncate(self.fd, eof)
+
+    def write_rows(self, name: str, row0: int, block: np.ndarray) -> None:
+        import os
+        shape, dt = self.shapes[name], self.dtypes[name]
+        block = np.ascontiguousarray(block, dtype=dt.newbyteorder("<"))
+        if block.shape[1:] != shape[1:] or row0 < 0 or row0 + block.shape[0] > shape[0]:
+            raise ValueError(f"{name}: rows {row0}..{row0 + block.shape[0]} of {shape} do not fit {block.shape}")
+        row_bytes = int(np.prod(shape[1:], dtype=np.int64)) * dt.itemsize
+        mv = memoryview(block).cast("B")
+        off, done = self.addr[name] + row0 * row_bytes, 0
+        while done < len(mv):
+            done += os.pwrite(self.fd, mv[done:], off + done)
+
+    def close(self) -> None:
+        import os
+        if self.fd is not None:
+            os.close(self.fd)
+            self.fd = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 # ---------------------------------------------------------------------------- reader

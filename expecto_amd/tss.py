@@ -137,7 +137,8 @@ def _batches(items, size):
 
 
 def compute_main(argv=None):
-    """compute_expecto_features.py main() (:17-128)."""
+    """compute_expecto_features.py main() (:17-128).  Under torch.distributed.run the genes are
+    sharded by contiguous rank ranges and rank 0 gathers the features and writes the .npy."""
     p = argparse.ArgumentParser(description='Compute ExPecto chromatin features for TSS list')
     p.add_argument('annoFile')
     p.add_argument('tss_file')
@@ -148,6 +149,9 @@ def compute_main(argv=None):
     args = p.parse_args(argv)
     if args.windowsize != 2000:
         raise ValueError("--windowsize must be 2000 (Beluga.py:43)")
+    rank, world, local = edist.init()
+    if world > 1:
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     os.makedirs(args.out_dir, exist_ok=True)
     fasta = Fasta(args.genome)
     model = _load_model(args)
@@ -178,18 +182,23 @@ def compute_main(argv=None):
                                          f"position {tss38}"
                 chrom, tss, _ = coords[0]
         genes.append((gene_id, chrom, int(tss), 1 if strand == "+" else -1))
-    print(f"Found {found} genes in geneAnno file that match a TSS in provided TSS file...")
-    print(f"Failed to convert {no_map} hg38 positions to hg19 with liftover tool...")
     anno = pd.read_csv(args.annoFile, index_col=0)
     changed = sum(1 for g, c, t, s in genes if anno.loc[g, 'CAGE_representative_TSS'] != t)
-    print(f"Found {changed} altered TSSs out of {anno.shape[0]} total TSSs...")
+    if rank == 0:
+        print(f"Found {found} genes in geneAnno file that match a TSS in provided TSS file...")
+        print(f"Failed to convert {no_map} hg38 positions to hg19 with liftover tool...")
+        print(f"Found {changed} altered TSSs out of {anno.shape[0]} total TSSs...")
     dg = DeviceGenome(fasta)
     pipe = TSSPipeline(model.engine(), dg)
-    feats = []
-    for b in _batches(genes, args.gene_batch):
-        f = pipe.features([g[1] for g in b], [g[2] for g in b], [g[3] for g in b])
-        feats.append(f.cpu().numpy())
-    arr = np.concatenate(feats, 0) if feats else np.zeros((0, 20020))
+    # genes shard by contiguous rank ranges; rank 0 gathers the f64 [G_r, 20020] blocks (RCCL)
+    lo, hi = edist.shard_range(len(genes), rank, world)
+    feats = [pipe.features([g[1] for g in b], [g[2] for g in b], [g[3] for g in b])
+             for b in _batches(genes[lo:hi], args.gene_batch)]
+    mine = torch.cat(feats, 0) if feats else torch.zeros((0, 20020), dtype=torch.float64, device=dg.codes.device)
+    full = edist.gather_rows_to(mine, 0, len(genes), world, rank)
+    if rank != 0:
+        return None
+    arr = full.cpu().numpy()
     np.save(f'{args.out_dir}/Xreducedall.2002.representative_tss_top', arr)
     return arr
 

@@ -24,7 +24,7 @@
  *   expecto_fwd_rc_average         (x[:N] + x[N:]) / 2 (predict.py:186-190;
  *                                   0.5*(fwd+rc) of compute_expecto_features.py:123)
  *   expecto_tss_reduce             pos_weights x pred_fwd_rc (compute_expecto_features.py:91-124)
- *   expecto_variant_reduce         exp-decay shift weights x effects (predict.py:87-136)
+ *   expecto_variant_reduce(_lut)   exp-decay shift weights x effects (predict.py:87-136)
  *   expecto_gblinear_predict       xgboost gblinear scoring of feature rows (predict.py:150-166)
  *   expecto_shift_reduce           200-shift reduction of consensus / eQTL sequences
  *                                  (geuvadis_sed_for_top_eqtls.py:95-121, geuvadis_predict_consensus.py:110-128)
@@ -175,6 +175,11 @@ long long expecto_beluga_f16_fallbacks(expecto_beluga_t h, int* sx);
  * else 0 (< 0 on error). */
 int expecto_beluga_set_overflow_check(expecto_beluga_t h, int deferred);
 int expecto_beluga_overflow_pending(expecto_beluga_t h, void* stream);
+/* Deferred mode, streamed batches: enqueue on `stream` a copy of the flag into *dst (pinned host
+ * or device memory) followed by its reset, without a host sync.  Enqueued right after a batch's
+ * forward calls, *dst holds exactly that batch's overflow state once an event recorded after it
+ * has completed (the stream runs in order), while later batches are already queued. */
+int expecto_beluga_overflow_take(expecto_beluga_t h, int* dst, void* stream);
 
 /* Per-layer device time accumulated over forward calls while profiling is on (ms), launches
  * (`calls`) and executed multiply-adds (`macs`: GEMM M x N x K actually run, including the
@@ -218,6 +223,13 @@ int expecto_tss_reduce(const float* fwd, const float* rc, const double* weights,
  * shifts[n_shift]; out [n, 10*nfeat] fp64 (predict.py:87-124 feature layout). */
 int expecto_variant_reduce(const float* effects, const long long* dist, const uint8_t* strand_plus,
                            const int* shifts, int n_shift, int n, int nfeat, double* out, void* stream);
+/* The same with the decay factors from a table: exp_lut[k*lut_len + fl] = exp(-c_k * fl)
+ * (c = 0.01, 0.02, 0.05, 0.1, 0.2; every fl = floor(|d|/200) < lut_len; DEVICE array) computed
+ * by the caller with the reference's own exp (numpy, predict.py:88-107), so the features equal
+ * the reference's bit for bit; expecto_variant_reduce uses the device exp (within 1 ulp). */
+int expecto_variant_reduce_lut(const float* effects, const long long* dist, const uint8_t* strand_plus,
+                               const int* shifts, int n_shift, int n, int nfeat, const double* exp_lut, int lut_len,
+                               double* out, void* stream);
 
 /* Shift reduction of per-sequence window predictions (fwd and rc [n, n_shift, nfeat] f32, DEVICE)
  * with exp-decay weights [10, n_shift] f64 into float64 features, shifts summed in order.

@@ -9,6 +9,8 @@ Runs ``geuvadis_sed_for_top_eqtls.py`` (2 eQTLs, + and - strand, one SNV inside 
 synthetic 393,216-bp consensus FASTAs, with the seeded Beluga weights (make_golden.py) and a
 seeded gblinear model of 20030 features (xgboost 0.7 binary layout), stubs on PYTHONPATH
 (h5py -> .npz, Bio.SeqIO, natsort, seaborn, xgboost with a restated gblinear).
+The sed run goes through ``forward_capture.py``, which records the reference Beluga forwards
+(the per-window 200-shift chromatin predictions); the stub DMatrix records its features.
 Writes tests/golden/consensus.npz (+ consensus_model.save, consensus_stdout.txt).
 The inputs are regenerated at test time by ``write_inputs`` (same seed).
 """
@@ -98,14 +100,33 @@ def main():
     sd = oweights.seeded_state_dict(0)
     torch.save(sd, os.path.join(work, "beluga.pth"))
     env = dict(os.environ, PYTHONPATH=STUBS + ":" + REF, OMP_NUM_THREADS="8")
-    out1 = subprocess.run([sys.executable, os.path.join(REF, "geuvadis_sed_for_top_eqtls.py"), paths["model"],
+    out1 = subprocess.run([sys.executable, os.path.join(GOLD, "forward_capture.py"),
+                           os.path.join(REF, "geuvadis_sed_for_top_eqtls.py"), paths["model"],
                            paths["consensus"], paths["genes_csv"], paths["eqtls_csv"], "--beluga_model",
                            os.path.join(work, "beluga.pth"), "-o", "sed_out"], cwd=work, env=env,
                           capture_output=True, text=True, check=True)
+    # the sed run's per-window forwards (one [400, 2002] call per eQTL and allele: 200 shifts fwd
+    # then rc) and its two feature matrices (stub DMatrix: ref then alt, [n_eqtl, 20030] f64)
+    with np.load(os.path.join(work, "captured_forward.npz")) as z:
+        fw = [z[f"arr_{i}"] for i in range(len(z.files))]
+    assert len(fw) == 2 * len(GENES) and all(a.shape == (400, 2002) for a in fw), [a.shape for a in fw]
+    sed_feats = [np.load(os.path.join(work, f"captured_dmatrix_{i}.npy")) for i in range(2)]
     out2 = subprocess.run([sys.executable, os.path.join(REF, "geuvadis_predict_consensus.py"), paths["model"],
                            paths["consensus"], paths["genes_csv"], "--beluga_model", os.path.join(work, "beluga.pth"),
                            "-o", "cons_out"], cwd=work, env=env, capture_output=True, text=True, check=True)
     res = {}
+    for gi, (gene, *_) in enumerate(GENES):
+        # chromatin predictions of the 200-shift sed path: every window whose alt differs from its
+        # ref (the SNV's cone) and every 8th window, every 5th feature; full-row f64 sums of all
+        ref_w, alt_w = fw[2 * gi], fw[2 * gi + 1]
+        rows = np.union1d(np.nonzero((ref_w != alt_w).any(1))[0], np.arange(0, 400, 8))
+        res[f"sed_win_rows_{gene}"] = rows
+        res[f"sed_win_ref_{gene}"] = ref_w[rows, ::5]
+        res[f"sed_win_alt_{gene}"] = alt_w[rows, ::5]
+        res[f"sed_win_refsum_{gene}"] = ref_w.astype(np.float64).sum(1)
+        res[f"sed_win_altsum_{gene}"] = alt_w.astype(np.float64).sum(1)
+        res[f"sed_feat_ref_{gene}"] = sed_feats[0][gi, ::4]
+        res[f"sed_feat_alt_{gene}"] = sed_feats[1][gi, ::4]
     for gene, *_ in GENES:
         g = gene
         with np.load(os.path.join(work, "sed_out", g, f"{g}.h5.npz")) as z:

@@ -65,3 +65,29 @@ def test_no_cpu_fallback_without_library(tmp_path, monkeypatch):
     monkeypatch.setattr(_lib, "_lib", None)
     with pytest.raises(RuntimeError, match="not built"):
         _lib.load(str(tmp_path / "missing.so"))
+
+
+def _function_body(src: str, name: str) -> str:
+    """Text of the C++ function `name` (first definition) by brace matching."""
+    m = re.search(r"\n[\w:<>,\s\*&]*\b" + name + r"\s*\([^;{]*\)\s*\{", src)
+    assert m, name
+    i, depth = m.end(), 1
+    while depth:
+        depth += {"{": 1, "}": -1}.get(src[i], 0)
+        i += 1
+    return src[m.start():i]
+
+
+def test_production_forward_has_no_host_sync():
+    """The forward paths only enqueue work: no stream/device sync and no blocking copy in the
+    functions a forward call runs (forward_chunk, forward_segments, forward_pairs, run_fc,
+    run_conv, run_conv1, stage_copies); the f16x3 overflow check syncs only in its per-call
+    mode (run_checked) and the deferred release point (expecto_beluga_overflow_pending)."""
+    src = open(os.path.join(REPO, "expecto_amd", "csrc", "beluga.hip")).read()
+    for fn in ("forward_chunk", "forward_segments", "forward_pairs", "run_fc", "run_conv", "run_conv1",
+               "stage_copies", "count_slab_macs"):
+        body = _function_body(src, fn)
+        for bad in ("hipStreamSynchronize", "hipDeviceSynchronize", "hipMemcpy(", "hipMemcpyDeviceToHost"):
+            assert bad not in body, (fn, bad)
+    rc = _function_body(src, "run_checked")
+    assert rc.index("h->ovf_deferred") < rc.index("hipStreamSynchronize")

@@ -25,8 +25,21 @@ def _worker(rank, world, port, n_total, q):
     v = torch.arange(lo, hi, dtype=torch.float32)
     y = v.view(1, 1, 1, -1, 1).expand(2, 2, 3, hi - lo, 5).contiguous() + torch.arange(5.0)
     full = edist.gather_rows(y, 3, n_total, w)
+    # streamed batches: variable block sizes per rank (batch 0 of 2 rows, as the chromatin CLI does)
+    counts = [min(2, edist.shard_range(n_total, k, w)[1] - edist.shard_range(n_total, k, w)[0]) for k in range(w)]
+    blocks = edist.gather_blocks_to(y[:, :, :, :counts[r]], 3, counts, w, r)
+    if r == 0:
+        ok_blocks = all(torch.equal(b, full[:, :, :, edist.shard_range(n_total, k, w)[0]:][:, :, :, :counts[k]])
+                        for k, b in enumerate(blocks))
+    else:
+        ok_blocks = blocks is None
     to0 = edist.gather_rows_to(y, 3, n_total, w, r)
-    ok_to0 = torch.equal(to0, full) if r == 0 else to0 is None
+    # compute_expecto_features' features: f64 [G_r, 20020]-shaped blocks along dim 0 to rank 0
+    f = torch.arange(lo, hi, dtype=torch.float64).view(-1, 1) * 10 + torch.arange(3, dtype=torch.float64)
+    f0 = edist.gather_rows_to(f, 0, n_total, w, r)
+    ok_f = (torch.equal(f0[:, 0], torch.arange(n_total, dtype=torch.float64) * 10) and f0.dtype == torch.float64
+            if r == 0 else f0 is None)
+    ok_to0 = (torch.equal(to0, full) if r == 0 else to0 is None) and ok_blocks and ok_f
     q.put((r, lo, hi, full.shape,
            bool(torch.equal(full[0, 1, 2, :, 0], torch.arange(n_total, dtype=torch.float32))) and ok_to0))
     torch.distributed.destroy_process_group()

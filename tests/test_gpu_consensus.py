@@ -27,20 +27,75 @@ def _score_close(got, want, what):
                                err_msg=what)
 
 
+def _score_bound(m, x, pbar, weights, rows=None):
+    """Bound on |score(ours) - score(reference)| for the gblinear score psum = f32(bias + base),
+    psum = f32(psum + f32(f32(x_j) w_j)) over the 20030 features (xgboost 0.7 GBLinear::Pred),
+    when our features x come from window predictions pbar [S, 2002] each within the parity bar
+    1e-4|p| + 1e-5 of the reference's: feature (k, f) of the legacy layout may differ by
+    dx = sum_s W[k,s] (1e-4 |pbar[s,f]| + 1e-5) (only over the windows `rows` that can differ;
+    all by default), moving the exact sum by sum_j |w_j| dx_j; each side's float32 evaluation
+    then deviates from its exact sum by at most (n+1) u max_j |psum_j| (one rounding of the
+    product and one of the sum per feature, u = 2^-24)."""
+    W = weights if rows is None else weights[:, rows]
+    p = pbar if rows is None else pbar[rows]
+    dx = W @ (1e-4 * np.abs(p) + 1e-5)                                 # [10, 2002]
+    dx = np.concatenate([np.zeros((10, 1)), dx], 1).reshape(-1)        # legacy zero column per block
+    w = m.weights[:, 0].astype(np.float64)
+    psum = float(m.bias[0]) + float(m.base_score) + np.cumsum(w * x)
+    return float(np.abs(w) @ dx + 2 * (x.size + 1) * 2.0 ** -24 * np.abs(psum).max())
+
+
 def test_sed_for_top_eqtls_matches_reference(inputs):
+    """The 200-shift SNV path (forward_segment_pairs) against geuvadis_sed_for_top_eqtls.py:
+    per-window chromatin predictions of both alleles (the SNV's windows and every 8th window,
+    captured from the reference Beluga forwards) at the parity bar, the 20030 features at the
+    same bar, our scoring bit for bit equal to the restated GBLinear::Pred on our features, and
+    the scores (and alt - ref) within the bound _score_bound derives from the parity bar and
+    the float32 accumulation of the score sum."""
     from expecto_amd import consensus, h5
+    from expecto_amd.features import tss_pos_weights
+    from expecto_amd.xgblinear import GBLinear
     d, p, genes = inputs
     gold = np.load(os.path.join(GOLDEN, "consensus.npz"))
     out = d / "sed_out"
+    cap = {}
     consensus.sed_main([p["model"], p["consensus"], p["genes_csv"], p["eqtls_csv"], "--synthetic-weights", "0",
-                        "-o", str(out), "--seq-batch", "1"])
-    for gene, *_ in genes:
+                        "-o", str(out), "--seq-batch", "1"], capture=cap)
+    y = {a: np.concatenate(cap[f"y_{a}"], axis=1) for a in ("ref", "alt")}     # [2, n, 200, 2002]
+    x = {a: np.concatenate(cap[f"x_{a}"], axis=0) for a in ("ref", "alt")}     # [n, 20030]
+    from oracle.gblinear_np import predict as gblinear_ref
+    m = GBLinear.load(p["model"])
+    weights = tss_pos_weights()
+    for gi, (gene, *_) in enumerate(genes):
+        win = {a: y[a][:, gi].reshape(400, 2002) for a in y}                     # rows: 200 fwd then 200 rc
+        rows = gold[f"sed_win_rows_{gene}"]
+        for a in ("ref", "alt"):
+            assert_close(win[a][rows, ::5], gold[f"sed_win_{a}_{gene}"], what=f"{gene} {a} window predictions")
+            np.testing.assert_allclose(win[a].astype(np.float64).sum(1), gold[f"sed_win_{a}sum_{gene}"], rtol=2e-6,
+                                       atol=0, err_msg=f"{gene} {a} row sums")
+            assert_close(x[a][gi, ::4], gold[f"sed_feat_{a}_{gene}"], what=f"{gene} {a} features")
+        gd = gold[f"sed_win_alt_{gene}"].astype(np.float64) - gold[f"sed_win_ref_{gene}"]
+        assert_close(win["alt"][rows, ::5].astype(np.float64) - win["ref"][rows, ::5], gd,
+                     what=f"{gene} alt-ref window predictions")
+        # windows without the SNV are bitwise the ref ones, as in the reference
+        same = ~(gold[f"sed_win_alt_{gene}"] != gold[f"sed_win_ref_{gene}"]).any(1)
+        assert (win["alt"][rows[same]] == win["ref"][rows[same]]).all()
         r = h5.read(str(out / gene / f"{gene}.h5"))
         assert r["ref_preds"].shape == () and r["ref_preds"].dtype == np.float32
-        _score_close(r["ref_preds"], gold[f"sed_ref_{gene}"], f"{gene} ref")
-        _score_close(r["alt_preds"], gold[f"sed_alt_{gene}"], f"{gene} alt")
-        _score_close(r["alt_preds"] - r["ref_preds"], gold[f"sed_alt_{gene}"] - gold[f"sed_ref_{gene}"],
-                     f"{gene} alt-ref")
+        pbar = {a: (win[a][:200].astype(np.float64) + win[a][200:]) / 2 for a in win}
+        b = {a: _score_bound(m, x[a][gi], pbar[a], weights) for a in ("ref", "alt")}
+        for a in ("ref", "alt"):
+            got, want = float(r[f"{a}_preds"]), float(gold[f"sed_{a}_{gene}"])
+            # the scoring itself is exact: our score of our features == the restated GBLinear::Pred
+            assert np.float32(got) == gblinear_ref(x[a][gi][None], m.weights[:, 0], m.bias[0], m.base_score)[0]
+            assert abs(got - want) <= b[a], (gene, a, got, want, b[a])
+        # alt - ref: only the windows holding the SNV can move the features apart
+        snv = np.nonzero((win["alt"][:200] != win["ref"][:200]).any(1) | (win["alt"][200:] != win["ref"][200:]).any(1))[0]
+        bd = _score_bound(m, x["alt"][gi], pbar["alt"], weights, snv) + _score_bound(m, x["ref"][gi], pbar["ref"],
+                                                                                      weights, snv)
+        got = float(r["alt_preds"]) - float(r["ref_preds"])
+        want = float(gold[f"sed_alt_{gene}"]) - float(gold[f"sed_ref_{gene}"])
+        assert abs(got - want) <= bd, (gene, "alt-ref", got, want, bd)
     # the SNV 24 kb from the TSS lies outside every window: alt == ref exactly, like the reference
     r = h5.read(str(out / "geneb" / "geneb.h5"))
     assert r["ref_preds"] == r["alt_preds"]

@@ -274,9 +274,10 @@ def test_second_stream_overlap_is_bitwise_equal(monkeypatch):
 
 def test_chromatin_cli_two_ranks_equals_one(workdir):
     """The CLI sharded over 2 ranks (torch.distributed.run; gloo, both ranks on this one GPU:
-    the 8-GPU RCCL run is the driver's) writes the same .diff.h5 files, bit for bit, as one
-    rank: shards are contiguous variant ranges and the per-shift gather to rank 0 restores
-    the global order."""
+    the 8-GPU RCCL run is the driver's) and streamed in batches of 2 variants (uneven last
+    batches) writes the same files byte for byte as one rank in one batch: shards are contiguous
+    variant ranges, each batch is gathered to rank 0 and written at its rows; only rank 0 writes
+    snps_hg19.vcf.  One rank streaming 2-variant batches writes the same bytes too."""
     import socket
     import subprocess
     import sys
@@ -289,6 +290,8 @@ def test_chromatin_cli_two_ranks_equals_one(workdir):
               "--max-batch", "40"]
     one = workdir / "out_1rank"
     chromatin.main([str(vcf), "--output_dir", str(one)] + common)
+    one_b2 = workdir / "out_1rank_b2"
+    chromatin.main([str(vcf), "--output_dir", str(one_b2), "--variant-batch", "2"] + common)
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -297,12 +300,50 @@ def test_chromatin_cli_two_ranks_equals_one(workdir):
     env = dict(os.environ, EXPECTO_DIST_BACKEND="gloo")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "expecto_amd.chromatin",
-                        str(vcf), "--output_dir", str(two)] + common,
+                        str(vcf), "--output_dir", str(two), "--variant-batch", "2"] + common,
                        env=env, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
-    for sh in (0, -200, 200):
-        a = h5.read(str(one / f"snps.shift_{sh}.diff.h5"))
-        b = h5.read(str(two / f"snps.shift_{sh}.diff.h5"))
-        for k in ("ref", "alt", "diff"):
-            np.testing.assert_array_equal(a[k], b[k])
+    for name in ["snps_hg19.vcf"] + [f"snps.shift_{sh}.diff.h5" for sh in (0, -200, 200)]:
+        want = open(one / name, "rb").read()
+        assert open(two / name, "rb").read() == want, name
+        assert open(one_b2 / name, "rb").read() == want, name
+    a = h5.read(str(two / "snps.shift_200.diff.h5"))
+    assert a["ref"].shape == (12, 2002) and float(np.abs(a["ref"]).min()) > 0
+
+
+def test_tss_compute_two_ranks_equals_one(workdir):
+    """compute_expecto_features over 2 ranks (torch.distributed.run, gloo on this one GPU): genes
+    shard by rank ranges and rank 0 gathers the f64 [G_r, 20020] blocks; the .npy equals the
+    one-rank file bit for bit."""
+    import socket
+    import subprocess
+    import sys
+    from expecto_amd import tss
+    anno = workdir / "anno3.csv"
+    anno.write_text("id,symbol,seqnames,strand,TSS,CAGE_representative_TSS,type\n"
+                    "ENSGT0001,G1,chr1,+,30000,30000,protein_coding\n"
+                    "ENSGT0002,G2,chr2,-,29000,29123,protein_coding\n"
+                    "ENSGT0003,G3,chr3,+,31000,31000,protein_coding\n")
+    tssf = workdir / "tss3.tsv"
+    tssf.write_text("idx\tens_id\tchrom\ttss\tstrand\tcount\tis_default\n")
+    common = [str(anno), str(tssf), "--no-liftover", "--genome", str(workdir / "hg19.fa"), "--synthetic-weights",
+              "0", "--gene-batch", "1"]
+    one = workdir / "tss_1rank"
+    tss.compute_main(common + ["-o", str(one)])
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    two = workdir / "tss_2rank"
+    env = dict(os.environ, EXPECTO_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "expecto_amd.tss",
+                        "compute"] + common + ["-o", str(two)],
+                       env=env, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    name = "Xreducedall.2002.representative_tss_top.npy"
+    a, b = np.load(one / name), np.load(two / name)
+    assert a.shape == (3, 20020)
+    np.testing.assert_array_equal(a, b)

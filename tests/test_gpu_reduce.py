@@ -1,6 +1,9 @@
 """GPU reductions (reduce.hip) against the oracle (oracle/reduce_np.py, which follows
-compute_expecto_features.py:88-124 and predict.py:87-124), and the 2-feature-per-thread
-kernels bitwise equal to the scalar ones (a misaligned ``out`` view forces the scalar kernel)."""
+compute_expecto_features.py:88-124 and predict.py:87-124) BIT FOR BIT: the kernels round every
+product before the sum (no FMA contraction) and sum the shifts sequentially in order, as
+numpy's reductions over a non-contiguous axis and predict.py's functools.reduce do.  The
+2-feature-per-thread kernels are bitwise equal to the scalar ones (a misaligned ``out`` view
+forces the scalar kernel)."""
 import numpy as np
 import pytest
 import torch
@@ -27,8 +30,7 @@ def test_tss_reduce_matches_oracle_and_scalar_kernel(nfeat):
     out_s = tss_reduce(fd, rd, w, out=_misaligned((G, 10 * nfeat))).cpu().numpy()
     np.testing.assert_array_equal(out, out_s)
     for g in range(G):
-        # per-output sums run in a different order than numpy's pairwise sum
-        np.testing.assert_allclose(out[g], tss_ref(f[g], r[g]), rtol=1e-12, atol=1e-12)
+        np.testing.assert_array_equal(out[g], tss_ref(f[g], r[g]))
 
 
 @pytest.mark.parametrize("nfeat", [2002, 37])
@@ -47,4 +49,40 @@ def test_variant_features_match_oracle_and_scalar_kernel(nfeat):
     out_s = variant_features(ed, dist, strand, shifts, out=_misaligned((n, 10 * nfeat))).cpu().numpy()
     np.testing.assert_array_equal(out, out_s)
     ref = variant_reduce(list(eff), variant_weights(dist, strand, shifts), nfeat)
-    np.testing.assert_allclose(out, ref, rtol=1e-12, atol=1e-12)
+    np.testing.assert_array_equal(out, ref)
+
+
+def test_variant_features_beyond_32_shifts():
+    """predict --maxshift above 3000 (33+ shifts): the weight table is sized per launch."""
+    from expecto_amd.features import variant_features
+    from expecto_amd.pipeline import shift_order
+    from oracle.reduce_np import variant_reduce, variant_weights
+    rng = np.random.default_rng(5)
+    shifts = shift_order(5000)                      # 51 shifts
+    n, nfeat = 40, 2002
+    eff = rng.standard_normal((len(shifts), n, nfeat)).astype(np.float32)
+    dist = rng.integers(-30000, 30000, n)
+    strand = rng.random(n) < 0.5
+    out = variant_features(torch.from_numpy(eff).cuda(), dist, strand, shifts).cpu().numpy()
+    np.testing.assert_array_equal(out, variant_reduce(list(eff), variant_weights(dist, strand, shifts), nfeat))
+
+
+def test_shift_reduce_matches_numpy_bitwise():
+    """geuvadis_sed_for_top_eqtls.py:83-121: float64 fwd/rc mean, then
+    np.sum(pos_weights[None,:,:,None] * preds[:,None], axis=2) with the legacy zero column."""
+    from expecto_amd import _lib
+    from expecto_amd.features import tss_pos_weights
+    rng = np.random.default_rng(6)
+    n, S, F = 3, 200, 2002
+    fwd = rng.random((n, S, F), dtype=np.float32)
+    rc = rng.random((n, S, F), dtype=np.float32)
+    w = tss_pos_weights()
+    out = torch.empty((n, 20030), dtype=torch.float64, device="cuda")
+    lib = _lib.load()
+    fd, rd, wd = torch.from_numpy(fwd).cuda(), torch.from_numpy(rc).cuda(), torch.from_numpy(w).cuda()
+    _lib.check(lib.expecto_shift_reduce(_lib.dptr(fd), _lib.dptr(rd), _lib.dptr(wd), n, S, F, 3, _lib.dptr(out),
+                                        _lib.stream_ptr()), "shift_reduce")
+    preds = (fwd.astype(np.float64) + rc.astype(np.float64)) / 2
+    want = np.sum(w[None, :, :, None] * preds[:, None, :, :], axis=2).reshape(-1, 10 * F)
+    want = np.concatenate([np.zeros((n, 10, 1)), want.reshape(n, 10, F)], axis=2).reshape(n, 20030)
+    np.testing.assert_array_equal(out.cpu().numpy(), want)
