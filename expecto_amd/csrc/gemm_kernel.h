@@ -534,44 +534,72 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
 // XOR swizzle on the SOURCE offset, undone on the read: position = chunk ^ (-(row >> 2) & 3).
 typedef float floatx4v __attribute__((ext_vector_type(4)));
 
+// (window, position) of row mw + off from the wave's (w0, t0) = divmod(mw, s_in): rows of a
+// tile span only a few windows, so stepping beats a 64-bit division per row.
+__device__ __forceinline__ void row_wt(long long w0, int t0, int off, int s_in, long long& w, int& t) {
+  t = t0 + off;
+  w = w0;
+  while (t >= s_in) {
+    t -= s_in;
+    ++w;
+  }
+}
+
 template <int EPI, int FMT, int NB = 10, int MB = 4>
 __device__ __forceinline__ void gemm_epilogue16(const GemmArgs& p, const floatx4v (&acc)[MB][NB], long long mw, int n0,
                                                 int ks, int lane) {
   const int fr = lane & 15, fq = lane >> 4;
+  const long long w0 = mw / p.s_in;
+  const int t0 = (int)(mw - w0 * p.s_in);
 #pragma unroll
-  for (int nb = 0; nb < NB; ++nb) {
-    const int n = n0 + nb * 16 + fr;
-    if (n >= p.n_store) continue;
-    const float bn = (EPI == EPI_PARTIAL) ? 0.f : p.bias[n];
-    // f16x3: acc * 2^-(s_in + s_w[n]) is exact (power of 2), so the value equals the unscaled sum
-    const float cs = (FMT == 2 && EPI != EPI_PARTIAL) ? p.col_scale[n] : 1.f;
+  for (int mb = 0; mb < MB; ++mb) {
+    const long long m4 = mw + mb * 16 + 4 * fq;   // first of this lane's 4 rows (multiple of 4)
+    if (EPI == EPI_PARTIAL) {
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) {
-      const long long m4 = mw + mb * 16 + 4 * fq;   // first of this lane's 4 rows (multiple of 4)
-      if (EPI == EPI_PARTIAL) {
+      for (int nb = 0; nb < NB; ++nb) {
+        const int n = n0 + nb * 16 + fr;
+        if (n >= p.n_store) continue;
         float* cp = p.C + (long long)ks * p.split_stride + n;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if (m4 + j < p.M) cp[(m4 + j) * p.ldc] = acc[mb][nb][j];
-      } else if (EPI == EPI_RELU_POOL4) {
-        if (m4 >= p.M) continue;
-        const long long w = m4 / p.s_in;
-        const int tp = (int)(m4 - w * p.s_in) >> 2;
-        if (tp >= p.t_valid) continue;
+      }
+    } else if (EPI == EPI_RELU_POOL4) {
+      if (m4 >= p.M) continue;
+      long long w;
+      int t;
+      row_wt(w0, t0, mb * 16 + 4 * fq, p.s_in, w, t);
+      const int tp = t >> 2;
+      if (tp >= p.t_valid) continue;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const int n = n0 + nb * 16 + fr;
+        if (n >= p.n_store) continue;
+        const float bn = p.bias[n];
+        // f16x3: acc * 2^-(s_in + s_w[n]) is exact (power of 2), so the value equals the unscaled sum
+        const float cs = FMT == 2 ? p.col_scale[n] : 1.f;
         float mx = fmaxf(fmaxf(acc[mb][nb][0], acc[mb][nb][1]), fmaxf(acc[mb][nb][2], acc[mb][nb][3]));
         if (FMT == 2) mx *= cs;
         store_act<FMT>(p.C, w * p.s_out + tp, p.ldc, n, fmaxf(mx + bn, 0.f), p.out_scale, p.ovf);
-      } else {
+      }
+    } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const long long m = m4 + j;
-          if (m >= p.M) continue;
-          const long long w = m / p.s_in;
-          const int tpos = (int)(m - w * p.s_in);
-          if (tpos >= p.t_valid) continue;
+      for (int j = 0; j < 4; ++j) {
+        const long long m = m4 + j;
+        if (m >= p.M) continue;
+        long long w;
+        int tpos;
+        row_wt(w0, t0, mb * 16 + 4 * fq + j, p.s_in, w, tpos);
+        if (tpos >= p.t_valid) continue;
+        const long long orow = p.c_rows ? p.c_rows[m] : (w * p.s_out + tpos);
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          const int n = n0 + nb * 16 + fr;
+          if (n >= p.n_store) continue;
+          const float bn = p.bias[n];
+          const float cs = FMT == 2 ? p.col_scale[n] : 1.f;
           const float a = FMT == 2 ? acc[mb][nb][j] * cs : acc[mb][nb][j];
           const float v = a + bn;
-          const long long orow = p.c_rows ? p.c_rows[m] : (w * p.s_out + tpos);
           if (EPI == EPI_SIGMOID)
             p.C[orow * p.ldc + n] = 1.0f / (1.0f + expf(-v));
           else
@@ -1222,6 +1250,8 @@ template <int MB = 4>
 __device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const floatx4v (&acc)[MB][10], long long mw,
                                                      int n0, int lane, char* lds) {
   const int fr = lane & 15, fq = lane >> 4;
+  const long long w0 = mw / p.s_in;
+  const int t0 = (int)(mw - w0 * p.s_in);
 #pragma unroll
   for (int half = 0; half < MB / 2; ++half) {
 #pragma unroll
@@ -1251,8 +1281,9 @@ __device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const fl
       const int k = i * 64 + lane, row = k / 40, ch = k - row * 40;
       const long long m = mw + half * 32 + row;
       if (m < p.M) {
-        const long long w = m / p.s_in;
-        const int tpos = (int)(m - w * p.s_in);
+        long long w;
+        int tpos;
+        row_wt(w0, t0, half * 32 + row, p.s_in, w, tpos);
         if (tpos < p.t_valid && n0 + (ch >> 3) * 32 < p.n_store) {
           const long long orow = w * p.s_out + tpos;
           char* g = (char*)p.C + (orow * ldb + (n0 >> 5)) * 128 + ch * 16;
@@ -1261,6 +1292,55 @@ __device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const fl
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
+// Pool epilogue of the f16x3 conv kernels through LDS.  A lane's 4 accumulator rows of a
+// 16-row block are one pool group (rows 4*fq..4*fq+3; m0 and s_in are multiples of 4), so the
+// pooled value needs no shuffle: maxpool(relu(x*cs + b)) = relu(max(x)*cs + b) (monotone maps).
+// The wave's 4*MB pooled rows x 160 columns are split into its private LDS area in the planes
+// layout, then stored as 16-B chunks (one contiguous 640-B run per pooled row) instead of two
+// 2-byte stores per value.  Same values as gemm_epilogue16<EPI_RELU_POOL4, 2>.
+template <int MB>
+__device__ __forceinline__ void epilogue_pool_h2_lds(const GemmArgs& p, const floatx4v (&acc)[MB][10], long long mw,
+                                                     int n0, int lane, char* lds) {
+  static_assert(4 * MB <= 32, "pooled rows per wave exceed the LDS area");
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int nb = 0; nb < 10; ++nb) {
+    const int n = n0 + nb * 16 + fr;
+    const float bn = n < p.n_store ? p.bias[n] : 0.f;
+    const float cs = n < p.n_store ? p.col_scale[n] : 0.f;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const float mx = fmaxf(fmaxf(acc[mb][nb][0], acc[mb][nb][1]), fmaxf(acc[mb][nb][2], acc[mb][nb][3]));
+      const float x = fmaxf(mx * cs + bn, 0.f) * p.out_scale;
+      if (!(fabsf(x) < 65504.f)) *p.ovf = 1;   // NaN/overflow: the call is recomputed
+      _Float16 hi, lo;
+      split_h2(x, hi, lo);
+      char* d = lds + (mb * 4 + fq) * H3E_ROW + (nb >> 1) * 128 + ((nb & 1) * 16 + fr) * 2;
+      *(_Float16*)d = hi;
+      *(_Float16*)(d + 64) = lo;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const long long ldb = p.ldc >> 5;
+  const long long w0 = mw / p.s_in;
+  const int t0 = (int)(mw - w0 * p.s_in);
+#pragma unroll 5
+  for (int i = 0; i < (4 * MB * 40) / 64; ++i) {
+    const int k = i * 64 + lane, row = k / 40, ch = k - row * 40;
+    const long long m4 = mw + 4 * row;                  // first conv row of pooled row `row`
+    if (m4 < p.M) {
+      long long w;
+      int t;
+      row_wt(w0, t0, 4 * row, p.s_in, w, t);
+      const int tp = t >> 2;
+      if (tp < p.t_valid && n0 + (ch >> 3) * 32 < p.n_store) {
+        char* g = (char*)p.C + ((w * p.s_out + tp) * ldb + (n0 >> 5)) * 128 + ch * 16;
+        *(floatx4v*)g = *(const floatx4v*)(lds + row * H3E_ROW + ch * 16);
+      }
+    }
   }
 }
 
@@ -1427,11 +1507,14 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
     }
     if (c + 1 < nchunk) read_a(aslab + ((c + 1) & 1) * G::ASLAB, 0, as);
   }
-  if constexpr (EPI == EPI_RELU) {
+  if constexpr (EPI == EPI_RELU || EPI == EPI_RELU_POOL4) {
     // the ring's last (duplicate) B pieces may still be landing: drain before reusing LDS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    epilogue_relu_h2_lds<MB>(p, acc, m0 + wave * 16 * MB, n0, lane, smem + wave * H3E_WAVE);
+    if constexpr (EPI == EPI_RELU)
+      epilogue_relu_h2_lds<MB>(p, acc, m0 + wave * 16 * MB, n0, lane, smem + wave * H3E_WAVE);
+    else
+      epilogue_pool_h2_lds<MB>(p, acc, m0 + wave * 16 * MB, n0, lane, smem + wave * H3E_WAVE);
   } else {
     gemm_epilogue16<EPI, 2, 10, MB>(p, acc, m0 + wave * 16 * MB, n0, 0, lane);
   }
@@ -1459,6 +1542,8 @@ __device__ __forceinline__ void epilogue_relu_h2_lds8m(const GemmArgs& p, const 
   constexpr int WR = 16 * MB;                          // rows per wave
   const int fr = lane & 15, fq = lane >> 4;
   const long long ldb = p.ldc >> 5;
+  const long long w0 = m0 / p.s_in;
+  const int t0 = (int)(m0 - w0 * p.s_in);
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
     if ((wm >> 1) == pass) {            // this pass stages rows 2*WR*pass .. +2*WR-1 (waves wm = 2*pass, 2*pass+1)
@@ -1488,8 +1573,9 @@ __device__ __forceinline__ void epilogue_relu_h2_lds8m(const GemmArgs& p, const 
       const int k = i * 512 + tid, row = k / 40, ch = k - row * 40;
       const long long m = m0 + pass * 2 * WR + row;
       if (m < p.M) {
-        const long long w = m / p.s_in;
-        const int tpos = (int)(m - w * p.s_in);
+        long long w;
+        int tpos;
+        row_wt(w0, t0, pass * 2 * WR + row, p.s_in, w, tpos);
         if (tpos < p.t_valid && n0 + (ch >> 3) * 32 < p.n_store) {
           char* g = (char*)p.C + ((w * p.s_out + tpos) * ldb + (n0 >> 5)) * 128 + ch * 16;
           *(floatx4v*)g = *(const floatx4v*)(lds + row * H3E_ROW + ch * 16);
@@ -1884,7 +1970,7 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (EPI == EPI_RELU) {
+    if constexpr (EPI == EPI_RELU || EPI == EPI_RELU_POOL4) {
       __builtin_amdgcn_s_barrier();                    // consumers' epilogue reuses the LDS
     }
     return;
@@ -1948,9 +2034,12 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
     }
     if (c + 1 < nchunk) read_a(aslab + ((c + 1) & 1) * G::ASLAB, 0, as);
   }
-  if constexpr (EPI == EPI_RELU) {
+  if constexpr (EPI == EPI_RELU || EPI == EPI_RELU_POOL4) {
     __builtin_amdgcn_s_barrier();                     // producers drained their tail pieces
-    epilogue_relu_h2_lds<4>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
+    if constexpr (EPI == EPI_RELU)
+      epilogue_relu_h2_lds<4>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
+    else
+      epilogue_pool_h2_lds<4>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
   } else {
     gemm_epilogue16<EPI, 2, 10, 4>(p, acc, m0 + wave * 64, n0, 0, lane);
   }
