@@ -649,7 +649,7 @@ constexpr ConvGeo kConv[5] = {
 // FC1 split-K: a fixed number of slabs per handle (default 20 of 3392; a divisor of
 // 67840/32 = 2120 K blocks), whatever the batch, so an FC1 output never depends on how many
 // windows shared the launch.
-constexpr int kFc2Splits = 7;          // FC2 K = 63 blocks of 32 -> 7 slabs of 9: a 2000-row FC2 fills
+constexpr int kFc2SplitsDefault = 7;   // FC2 K = 63 blocks of 32 -> 7 slabs of 9: a 2000-row FC2 fills
                                         // 728 workgroups instead of 104 (fixed: sums never depend on M)
 constexpr int kFcSplitsDefault = 20;   // 2080 workgroups for 2000 rows: 8.1 rounds of 256 CUs (10: 4.1)
 }  // namespace
@@ -692,7 +692,7 @@ struct expecto_beluga {
   float* P = nullptr;
   float* Q = nullptr;
   float* part = nullptr;
-  float* part2 = nullptr;        // FC2 split-K partials (kFc2Splits slabs; FC1's stay in `part`)
+  float* part2 = nullptr;        // FC2 split-K partials (fc2_splits slabs; FC1's stay in `part`)
   float* h1 = nullptr;
   long long* a_rows = nullptr;  // FC1 row table (segment path), max_batch entries
   long long* c_rows = nullptr;  // FC2 output-row table (segment path), max_batch entries
@@ -718,6 +718,7 @@ struct expecto_beluga {
   std::vector<void*> allocs;
   int precision = EXPECTO_PRECISION_BF16X6;
   int fc_splits = kFcSplitsDefault;   // FC1 split-K slabs: a divisor of 2120 K blocks, <= 32
+  int fc2_splits = kFc2SplitsDefault; // FC2 split-K slabs: a divisor of 63 K blocks
   int conv_tile = 0;                  // f16x3 conv M tile: 0 = auto (conv_tile_rows), 256 or 384
   int cus = 0;                        // compute units of the device (workgroups per round)
   bool profiling = false;
@@ -1029,7 +1030,7 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     a.Bp = g_precision == EXPECTO_PRECISION_F16X3 ? h->wh[6] : h->fc2p;
     a.col_scale = g_precision == EXPECTO_PRECISION_F16X3 ? h->cs[6] : nullptr;
     a.ldb = kHidLd;
-    a.kper = kHidLd / kFc2Splits;
+    a.kper = kHidLd / h->fc2_splits;
     a.taps = 1;
     a.n_tiles = npad_of(kNFeat) / GBN;
     a.m_tiles = m_tiles;
@@ -1040,10 +1041,10 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     a.split_stride = (long long)nb * kHidLd;
     LayerTimer lt(h, 8, st);
     if (h->profiling) h->macs[h->timer_base + 8] += (double)nb * kNFeat * kFc1Out;
-    if ((rc = launch_gemm<8, EPI_PARTIAL>(a, kFc2Splits, st))) return rc;
+    if ((rc = launch_gemm<8, EPI_PARTIAL>(a, h->fc2_splits, st))) return rc;
     const long long count = (long long)nb * kNFeat;
     fc2_reduce<<<dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st>>>(
-        h->part2, kFc2Splits, (long long)nb * kHidLd, nb, h->fc2b, a.col_scale, c_rows, y);
+        h->part2, h->fc2_splits, (long long)nb * kHidLd, nb, h->fc2b, a.col_scale, c_rows, y);
     if ((rc = check_launch("fc2_reduce"))) return rc;
   }
   return EXPECTO_OK;
@@ -1675,6 +1676,11 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
     EXPECTO_REQUIRE(v >= 1 && v <= 32 && (kFc1In / GBK) % v == 0, "EXPECTO_FC1_SPLITS must divide 2120 and be <= 32");
     h->fc_splits = v;
   }
+  if (const char* e = getenv("EXPECTO_FC2_SPLITS")) {   // tuning knob (fixed per handle, like FC1's)
+    const int v = atoi(e);
+    EXPECTO_REQUIRE(v >= 1 && 63 % v == 0, "EXPECTO_FC2_SPLITS must divide 63");
+    h->fc2_splits = v;
+  }
   if (const char* e = getenv("EXPECTO_OVERLAP")) h->overlap = atoi(e) != 0;   // same bits either way
   if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)
     const int v = atoi(e);
@@ -1684,7 +1690,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   const size_t partf = (size_t)h->fc_splits * max_batch * kHidLd;
   if ((rc = dalloc(h, &h->P, act_alloc(pf))) || (rc = dalloc(h, &h->Q, act_alloc(qf))) ||
       (rc = dalloc(h, &h->part, partf)) || (rc = dalloc(h, &h->h1, act_alloc((size_t)max_batch * kHidLd))) ||
-      (rc = dalloc(h, &h->part2, (size_t)kFc2Splits * max_batch * kHidLd)))
+      (rc = dalloc(h, &h->part2, (size_t)h->fc2_splits * max_batch * kHidLd)))
     return fail(rc);
   {
     float* rows = nullptr;
