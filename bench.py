@@ -88,9 +88,9 @@ def kernel_name(layer: str, precision: str, segments: bool = True) -> str:
     if precision == "f16x3":
         if l in (7, 8):
             return f"beluga_fc_h3p<{l}, {e}, 0, 3>"
-        if l == 2:   # conv2: 384-row tiles (the other conv layers: producer/consumer 256-row tiles)
+        if l in (2, 5):   # conv2, conv5: 384-row tiles (the others: producer/consumer 256-row tiles)
             return f"beluga_conv_h3r<{l}, {e}, 0>"
-        return f"beluga_conv_h3p<{l}, {e}, 0, 3>"
+        return f"beluga_conv_h3p<{l}, {e}, 256, 4>"
     return f"beluga_gemm<{l}, {e}, 4, 2, 32, 1>"
 
 

@@ -857,18 +857,20 @@ bool planes_gemm() { return g_precision != EXPECTO_PRECISION_FP32; }
 long long gemm_bm() { return planes_gemm() ? X6P_BM : GBM; }
 float exp2i(int e) { return std::ldexp(1.0f, e); }
 
-// M tile rows of an f16x3 conv launch.  The 384-row kernels (beluga_conv_h3r, beluga_conv_h3s<6>)
-// and the 256-row producer/consumer kernel (beluga_conv_h3p) give bitwise-equal results, so the
-// choice is free per launch (tests/test_gpu_forward.py::test_conv_tile_choice_is_bitwise).
-// tools/gemm_bench (2000 windows, fp32-equivalent TF/s): conv2 h3r 520 vs h3p 505-510; conv3
-// h3p 484 vs 468 (h3s<6>), conv4 522 vs 496 (h3r), conv5 491 vs 480, conv6 497 vs 467: 384-row
-// tiles only for conv2.  One workgroup fills a CU, so a launch is priced by its rounds of 256
+// M tile rows of an f16x3 conv launch.  The 384-row kernel (beluga_conv_h3r: 4 waves of 96 x 160,
+// each issuing its own LDS-DMA pieces one per MFMA unit) and the 256-row producer / consumer
+// kernel (beluga_conv_h3p<.., 256, 4>: 4-deep B ring, next-stage fragments read before the
+// barrier) give bitwise-equal results, so the choice is free per launch
+// (tests/test_gpu_forward.py::test_conv_tile_choice_is_bitwise).  tools/gemm_bench (1000 windows,
+// one box, fp32-equivalent TF/s, round 2): conv2 h3r 565 vs h3p 553, conv3 h3p 509 vs h3r 487,
+// conv5 h3r 504 vs h3p 482, conv6 h3p 524 vs h3r 498 (conv4, pooled: 537 vs 533): 384-row tiles
+// for conv2 and conv5.  One workgroup fills a CU, so a launch is priced by its rounds of 256
 // workgroups (the alt-delta runs of the pair path, 30-60 k rows, take whichever tile needs the
 // fewer row-rounds).  l: 0 = conv2 .. 4 = conv6.
 int conv_tile_rows(const expecto_beluga* h, int l, bool pool, long long M, int n_tiles) {
   if (g_precision != EXPECTO_PRECISION_F16X3) return (int)gemm_bm();
   if (h->conv_tile) return h->conv_tile;
-  if (!(pool && l == 0)) return 256;
+  if (!(l == 0 || l == 3)) return 256;   // 384-row tiles: conv2 (pool) and conv5
   const int cus = h->cus > 0 ? h->cus : 256;
   auto cost = [&](int bm, double per_row) {
     const long long blocks = (M + bm - 1) / bm * n_tiles;
@@ -900,14 +902,10 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
       // all bitwise equal (same products and k order per output); per-layer choice from
       // tools/gemm_bench: 256-row tiles on the producer/consumer kernel (MFMA waves never issue
       // LDS-DMA), 384-row tiles (conv2) on the 4-wave 96-row kernel
-      if (bm == 384) {
-        if constexpr (EPI == EPI_RELU)
-          beluga_conv_h3s<LAYER, EPI, 0, 6><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
-        else
-          beluga_conv_h3r<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
-      } else {
-        beluga_conv_h3p<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
-      }
+      if (bm == 384)
+        beluga_conv_h3r<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
+      else   // 4-deep B ring, next-stage fragments read before the stage barrier (TM 256)
+        beluga_conv_h3p<LAYER, EPI, 256, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
     } else {   // FC layers: producer / consumer waves, both operands through an LDS ring (same bits)
       beluga_fc_h3p<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
     }

@@ -1514,13 +1514,20 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
       }
       if (t < 7) read_a(slab, t + 1, as);     // same slab: already resident
       if constexpr (!(TM & 4)) {
-        // all but the B pieces of the last NSB-2 stages: B(s+1), and slab c+1 by its last tap
+        // all but the B pieces of the last NSB-2 stages: B(s+1), and slab c+1 by its last tap.
+        // The next tap's A fragment reads (from the slab, which no DMA touches before the
+        // chunk after next) stay in flight across the barrier: the MFMAs that use them wait.
+        // TM 128 (probe): round 1's lgkmcnt(0) here.
         if constexpr ((TM & 16) != 0)
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        else if constexpr (NSB == 4)
+        else if constexpr ((TM & 128) != 0 && NSB == 4)
           asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
-        else
+        else if constexpr ((TM & 128) != 0)
           asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+        else if constexpr (NSB == 4)
+          asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
         __builtin_amdgcn_s_barrier();
       }
       asm volatile("" ::: "memory");
@@ -1897,6 +1904,10 @@ __global__ __launch_bounds__(256, 1) void beluga_conv_h3r(GemmArgs p) {
 template <int LAYER, int EPI, int TM, int NSB>
 __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem) {
   static_assert(NSB == 3 || NSB == 4, "B ring depth");
+  // PF (NSB 4): producers keep one stage less in flight, so at the end of stage s the consumers
+  // can already read stage s+1's first B fragments (and, at a chunk's last tap, the next slab's
+  // A fragments) and start it right after the barrier without an LDS round trip.
+  constexpr bool PF = NSB == 4 && (TM & 256) != 0;
   using G = SlabGeo<4>;
   constexpr int ROW_KB = 128;
   constexpr int NAP = (G::PIECES + 3) / 4;            // slab pieces per producer wave and chunk (9)
@@ -1964,7 +1975,10 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
     issue_b(min(1, nk - 1), 1);
     if constexpr (NSB == 4) {
       issue_b(min(2, nk - 1), 2);
-      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      if constexpr (PF)
+        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");    // stages 0 and 1 landed
+      else
+        asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
     }
@@ -1982,7 +1996,9 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
         }
         if (!(TM & 2)) issue_b(min(s + NSB - 1, nk - 1), lslot);
         // everything but the B pieces of the last NSB-2 stages: B(s+1), and slab c+1 by tap 7
-        if constexpr (NSB == 4)
+        // (PF: all but this stage's pieces, so B(s+2) has landed at barrier s and the
+        // consumers read stage s+1's first fragments before that barrier)
+        if constexpr (NSB == 4 && !PF)
           asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
         else
           asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
@@ -2032,14 +2048,16 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
   __builtin_amdgcn_s_barrier();                       // slab 0 and B stage 0 landed
   asm volatile("" ::: "memory");
   bf16x8 as[4][3];
+  bf16x8 b0[3], b1[3];
   read_a(aslab, 0, as);
+  if constexpr (PF) read_b(bring, 0, b0);
   int slot = 0;
   for (int c = 0; c < nchunk; ++c) {
     const char* slab = aslab + (c & 1) * G::ASLAB;
     for (int t = 0; t < 8; ++t) {
       const char* base = bring + slot * H3C_BSTAGE;
-      bf16x8 b0[3], b1[3];
-      read_b(base, 0, b0);
+      const int nslot = slot + 1 == NSB ? 0 : slot + 1;
+      if constexpr (!PF) read_b(base, 0, b0);
 #pragma unroll
       for (int nb = 0; nb < 10; ++nb) {
         if (nb + 1 < 10) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
@@ -2047,13 +2065,19 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
         for (int mb = 0; mb < 4; ++mb) acc[mb][nb] = planes_mfma<2>(acc[mb][nb], as[mb], (nb & 1) ? b1 : b0);
         pin();
       }
-      if (t < 7) read_a(slab, t + 1, as);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (t < 7)
+        read_a(slab, t + 1, as);   // slab reads stay in flight across the barrier
+      else if (PF && c + 1 < nchunk)
+        read_a(aslab + ((c + 1) & 1) * G::ASLAB, 0, as);   // next slab landed by tap 6's barrier
+      if constexpr (PF) {
+        if (c * 8 + t + 1 < nk) read_b(bring + nslot * H3C_BSTAGE, 0, b0);   // stage s+1 landed at barrier s-1
+      }
+      if constexpr ((TM & 128) != 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // probe: round 1
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      slot = slot + 1 == NSB ? 0 : slot + 1;
+      slot = nslot;
     }
-    if (c + 1 < nchunk) read_a(aslab + ((c + 1) & 1) * G::ASLAB, 0, as);
+    if (!PF && c + 1 < nchunk) read_a(aslab + ((c + 1) & 1) * G::ASLAB, 0, as);
   }
   if constexpr (EPI == EPI_RELU || EPI == EPI_RELU_POOL4) {
     __builtin_amdgcn_s_barrier();                     // producers drained their tail pieces

@@ -238,9 +238,10 @@ int main(int argc, char** argv) {
     vs.push_back(mk6q<2, EPI_RELU_POOL4>("x6q"));
     vs.push_back(mkc3<2, EPI_RELU_POOL4>("h3c"));
     vs.push_back(mkr3<2, EPI_RELU_POOL4>("h3r"));
-    vs.push_back(mkr3<2, EPI_RELU_POOL4, 64>("h3r_burst"));
+    vs.push_back(mkr3<2, EPI_RELU_POOL4, 128>("h3r_lgkm0"));
     vs.push_back(mks3<2, EPI_RELU_POOL4, 4, 0>("h3s4"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4>("h3p"));
+    vs.push_back(mkp3<2, EPI_RELU_POOL4, 256, 4>("h3p4_pf"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 0, 4>("h3p4"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 2>("h3p_noglds"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 8>("h3p_hotAB"));
@@ -254,9 +255,10 @@ int main(int argc, char** argv) {
     vs.push_back(mk6q<3, EPI_RELU>("x6q"));
     vs.push_back(mkc3<3, EPI_RELU>("h3c"));
     vs.push_back(mkr3<3, EPI_RELU>("h3r"));
-    vs.push_back(mkr3<3, EPI_RELU, 64>("h3r_burst"));
+    vs.push_back(mkr3<3, EPI_RELU, 128>("h3r_lgkm0"));
     vs.push_back(mks3<3, EPI_RELU, 4, 0>("h3s4"));
     vs.push_back(mkp3<3, EPI_RELU>("h3p"));
+    vs.push_back(mkp3<3, EPI_RELU, 256, 4>("h3p4_pf"));
     vs.push_back(mkp3<3, EPI_RELU, 0, 4>("h3p4"));
     vs.push_back(mks3<3, EPI_RELU, 6, 0>("h3s6"));
   }
