@@ -719,6 +719,7 @@ struct expecto_beluga {
   int precision = EXPECTO_PRECISION_BF16X6;
   int fc_splits = kFcSplitsDefault;   // FC1 split-K slabs: a divisor of 2120 K blocks, <= 32
   int fc2_splits = kFc2SplitsDefault; // FC2 split-K slabs: a divisor of 63 K blocks
+  double fc1_m_order_mb = 128.0;      // FC1 dispatch: M tiles fastest while one split's A is <= this
   int conv_tile = 0;                  // f16x3 conv M tile: 0 = auto (conv_tile_rows), 256 or 384
   int cus = 0;                        // compute units of the device (workgroups per round)
   bool profiling = false;
@@ -995,12 +996,12 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     // Infinity Cache, so every XCD sweeps the same K slab (B slab read once); for larger M
     // (segment sweeps: 19,200 rows = 260 MB per slab) N tiles fastest, so the 13 N tiles of an
     // A tile run together (tools/gemm_bench fc1: +8 % at 4,000 rows, +5 % at 19,200 rows)
-    a.m_fastest = (double)m_tiles * gemm_bm() * (kFc1In / splits) * 4.0 <= 128.0 * (1 << 20) ? 1 : 0;
+    a.m_fastest = (double)m_tiles * gemm_bm() * (kFc1In / splits) * 4.0 <= h->fc1_m_order_mb * (1 << 20) ? 1 : 0;
+    a.linear_order = a.m_fastest;   // N tiles fastest: XCD-aware remap (consecutive tiles share an XCD)
     a.C = h->part;
     a.ldc = kHidLd;
     a.n_store = kHidLd;
     a.split_stride = part_rows * kHidLd;
-    a.linear_order = 1;
     a.ks_mask = ks_mask;
     EXPECTO_REQUIRE(!ks_mask || planes_gemm(), "slab mask needs the planes GEMM");
     LayerTimer lt(h, 6, st);
@@ -1679,6 +1680,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
     EXPECTO_REQUIRE(v >= 1 && 63 % v == 0, "EXPECTO_FC2_SPLITS must divide 63");
     h->fc2_splits = v;
   }
+  if (const char* e = getenv("EXPECTO_FC1_M_ORDER_MB")) h->fc1_m_order_mb = atof(e);   // same bits either way
   if (const char* e = getenv("EXPECTO_OVERLAP")) h->overlap = atoi(e) != 0;   // same bits either way
   if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)
     const int v = atoi(e);

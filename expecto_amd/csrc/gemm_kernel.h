@@ -1171,13 +1171,20 @@ __device__ __forceinline__ void gemm_fc_h3p_body(const GemmArgs& p, char* smem) 
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   bf16x8 as[4][3];
-  read_a(smem, as);
   int slot = 0;
   for (int s = 0; s < nk; ++s) {
     const char* base = smem + slot * FCP_STAGE;
     const int nslot = slot + 1 == NS ? 0 : slot + 1;
     bf16x8 b0[3], b1[3];
-    read_b(base, 0, b0);
+    // the stage's first B fragment, then its A fragments in MFMA order: the first MFMAs wait for
+    // 4 reads, not 10 (TM 128, probe: round 1's order, A first)
+    if constexpr ((TM & 128) != 0) {
+      read_a(base, as);
+      read_b(base, 0, b0);
+    } else {
+      read_b(base, 0, b0);
+      read_a(base, as);
+    }
 #pragma unroll
     for (int nb = 0; nb < 10; ++nb) {
       if (nb + 1 < 10) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
@@ -1185,10 +1192,8 @@ __device__ __forceinline__ void gemm_fc_h3p_body(const GemmArgs& p, char* smem) 
       for (int mb = 0; mb < 4; ++mb) acc[mb][nb] = planes_mfma<2>(acc[mb][nb], as[mb], (nb & 1) ? b1 : b0);
       pin();
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (s + 1 < nk) read_a(smem + nslot * FCP_STAGE, as);
     slot = nslot;
   }
   gemm_epilogue16<EPI, 2, 10, 4>(p, acc, m0 + wave * 64, n0, ks, lane);
@@ -1295,6 +1300,20 @@ __device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const fl
   }
 }
 
+// LDS swizzle of the conv kernels' A slab and B stages: the 16-B chunk c of row r sits at
+// position c ^ swz(r).  The 16x16x32 fragment reads of tap t read rows t..t+15 (A) and 0..15 (B);
+// a ds_read_b128 lane group then holds, per row residue mod 4 (= the bank quarter), four rows in
+// consecutive quads with chunk pattern (f, f^1, f^1, f) (the group's fq values).  swz(r) = 2 *
+// ((r >> 2) & 1) gives those four lanes distinct positions for EVERY t, i.e. conflict-free
+// reads at all 8 tap offsets; round 1's (-(r >> 2)) & 3 is conflict-free at t = 0 mod 4 only
+// (2-way conflicts otherwise: SQ_LDS_BANK_CONFLICT 25 % of SQ_LDS_IDX_ACTIVE on conv2).
+// TM 512 (probe): the old swizzle.  A permutation of LDS positions only: results unchanged.
+template <int TM>
+__device__ __forceinline__ int conv_swz(int r) {
+  if constexpr ((TM & 512) != 0) return (-(r >> 2)) & 3;
+  return ((r >> 2) & 1) << 1;
+}
+
 // Pool epilogue of the f16x3 conv kernels through LDS.  A lane's 4 accumulator rows of a
 // 16-row block are one pool group (rows 4*fq..4*fq+3; m0 and s_in are multiples of 4), so the
 // pooled value needs no shuffle: maxpool(relu(x*cs + b)) = relu(max(x)*cs + b) (monotone maps).
@@ -1364,7 +1383,7 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
   const long long lda_kb = p.lda / GBK;
   const int nchunk = (int)lda_kb;                     // Cin / 32
   const int nk = nchunk * 8;
-  auto swz = [](int r) { return (-(r >> 2)) & 3; };
+  auto swz = [](int r) { return conv_swz<TM>(r); };
   // A slab pieces: P = wave + 4*i (i < NA) of G::PIECES = row groups x 2 planes
   const char* Ab = (const char*)p.A + m0 * lda_kb * ROW_KB;
   const long long last_row = p.M - 1 + 7;             // Toeplitz rows read by the last output row
@@ -1635,7 +1654,7 @@ __device__ __forceinline__ void gemm_conv_h3s_body(const GemmArgs& p, char* smem
   const long long lda_kb = p.lda / GBK;
   const int nchunk = (int)lda_kb;
   const int nk = nchunk * 8;
-  auto swz = [](int r) { return (-(r >> 2)) & 3; };
+  auto swz = [](int r) { return conv_swz<TM>(r); };
   const char* Ab = (const char*)p.A + m0 * lda_kb * ROW_KB;
   const long long last_row = p.M - 1 + 7;
   const int na = (G::PIECES - wave + 7) / 8;          // A slab pieces P = wave + 8*i < PIECES
@@ -1924,7 +1943,7 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
   const long long lda_kb = p.lda / GBK;
   const int nchunk = (int)lda_kb;
   const int nk = nchunk * 8;
-  auto swz = [](int r) { return (-(r >> 2)) & 3; };
+  auto swz = [](int r) { return conv_swz<TM>(r); };
   char* const aslab = smem;
   char* const bring = smem + 2 * G::ASLAB;
 

@@ -132,7 +132,8 @@ int fc1_bench(int nb, int rounds, int splits) {
             {"fcr_m", fc1r_launch<0>}, {"fcr_n", fc1r_launch<0>}, {"fcr_x", fc1r_launch<0>},
             {"fcr_x_noload", fc1r_launch<2>}, {"fcr_x_hotAB", fc1r_launch<8>},
             {"fc4_m", fc1r_launch<0, 4>}, {"fc4_x", fc1r_launch<0, 4>},
-            {"fcp_m", fc1p_launch<0>}, {"fcp_x", fc1p_launch<0>}, {"fcp_x_noload", fc1p_launch<2>},
+            {"fcp_m", fc1p_launch<0>}, {"fcp_m_a1st", fc1p_launch<128>}, {"fcp_x", fc1p_launch<0>},
+            {"fcp_x_noload", fc1p_launch<2>},
             {"fcp_x_hotAB", fc1p_launch<8>}};
   constexpr int NV = sizeof(vs) / sizeof(vs[0]);
   const size_t csz = (size_t)splits * nb * ldc;
@@ -238,10 +239,11 @@ int main(int argc, char** argv) {
     vs.push_back(mk6q<2, EPI_RELU_POOL4>("x6q"));
     vs.push_back(mkc3<2, EPI_RELU_POOL4>("h3c"));
     vs.push_back(mkr3<2, EPI_RELU_POOL4>("h3r"));
-    vs.push_back(mkr3<2, EPI_RELU_POOL4, 128>("h3r_lgkm0"));
+    vs.push_back(mkr3<2, EPI_RELU_POOL4, 512>("h3r_oldswz"));
     vs.push_back(mks3<2, EPI_RELU_POOL4, 4, 0>("h3s4"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4>("h3p"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 256, 4>("h3p4_pf"));
+    vs.push_back(mkp3<2, EPI_RELU_POOL4, 256 | 512, 4>("h3p4_pf_oldswz"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 0, 4>("h3p4"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 2>("h3p_noglds"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 8>("h3p_hotAB"));
@@ -255,10 +257,11 @@ int main(int argc, char** argv) {
     vs.push_back(mk6q<3, EPI_RELU>("x6q"));
     vs.push_back(mkc3<3, EPI_RELU>("h3c"));
     vs.push_back(mkr3<3, EPI_RELU>("h3r"));
-    vs.push_back(mkr3<3, EPI_RELU, 128>("h3r_lgkm0"));
+    vs.push_back(mkr3<3, EPI_RELU, 512>("h3r_oldswz"));
     vs.push_back(mks3<3, EPI_RELU, 4, 0>("h3s4"));
     vs.push_back(mkp3<3, EPI_RELU>("h3p"));
     vs.push_back(mkp3<3, EPI_RELU, 256, 4>("h3p4_pf"));
+    vs.push_back(mkp3<3, EPI_RELU, 256 | 512, 4>("h3p4_pf_oldswz"));
     vs.push_back(mkp3<3, EPI_RELU, 0, 4>("h3p4"));
     vs.push_back(mks3<3, EPI_RELU, 6, 0>("h3s6"));
   }
