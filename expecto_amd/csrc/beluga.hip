@@ -646,12 +646,14 @@ constexpr ConvGeo kConv[5] = {
     {480, 640, 120, 113, 113, 0},  // conv5
     {640, 640, 113, 106, 106, 0},  // conv6 -> FC1 reads 106*640 = 67840 contiguous floats
 };
-// FC1 split-K: a fixed number of slabs per handle (default 20 of 3392; a divisor of
+// FC1 split-K: a fixed number of slabs per handle (default 8 of 8480; a divisor of
 // 67840/32 = 2120 K blocks), whatever the batch, so an FC1 output never depends on how many
 // windows shared the launch.
 constexpr int kFc2SplitsDefault = 7;   // FC2 K = 63 blocks of 32 -> 7 slabs of 9: a 2000-row FC2 fills
                                         // 728 workgroups instead of 104 (fixed: sums never depend on M)
-constexpr int kFcSplitsDefault = 20;   // 2080 workgroups for 2000 rows: 8.1 rounds of 256 CUs (10: 4.1)
+constexpr int kFcSplitsDefault = 8;    // round 2 sweep (tools/knob_sweep.py, interleaved): 8 vs 20 slabs
+                                       // +0.6-0.9 % on the 200-window workload, +0.3-1.2 % on configs[1]
+                                       // (4: -0.6 / -3.7 %), with 2.5x less split-K partial traffic
 }  // namespace
 
 struct expecto_beluga {

@@ -1049,6 +1049,10 @@ constexpr int FCP_STAGE = 2 * FCP_APLANE + 2 * X6P_B_PLANE;   // 52 KB
 template <int LAYER, int EPI, int TM, int NS>
 __device__ __forceinline__ void gemm_fc_h3p_body(const GemmArgs& p, char* smem) {
   static_assert(NS == 3 || NS == 4, "ring depth");
+  // PF: producers wait for ALL their pieces at each stage end (stage s+NS-1 landed at barrier s),
+  // so the consumers read stage s+1's first fragments before barrier s and start it without an
+  // LDS round trip; the loads get one stage less to land.
+  constexpr bool PF = (TM & 256) != 0;
   constexpr int ROW_KB = 128;
   const unsigned nblk = gridDim.x, bid = blockIdx.x;
   const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
@@ -1116,7 +1120,9 @@ __device__ __forceinline__ void gemm_fc_h3p_body(const GemmArgs& p, char* smem) 
                                                  boff[j], (unsigned)(s * ROW_KB), 0, 0);
     };
     for (int s = 0; s < NS - 1; ++s) issue(min(s, nk - 1), s);
-    if constexpr (NS == 3)
+    if constexpr (PF)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (NS == 3)
       asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
     else
       asm volatile("s_waitcnt vmcnt(26)" ::: "memory");
@@ -1125,8 +1131,10 @@ __device__ __forceinline__ void gemm_fc_h3p_body(const GemmArgs& p, char* smem) 
     for (int s = 0; s < nk; ++s) {
       const int lslot = slot == 0 ? NS - 1 : slot - 1;   // stage s+NS-1 goes where s-1 was
       if (!(TM & 2)) issue(min(s + NS - 1, nk - 1), lslot);
-      // all but the pieces of the last NS-2 stages: stage s+1 landed
-      if constexpr (NS == 3)
+      // all but the pieces of the last NS-2 stages: stage s+1 landed (PF: all of them)
+      if constexpr (PF)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if constexpr (NS == 3)
         asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
       else
         asm volatile("s_waitcnt vmcnt(26)" ::: "memory");
@@ -1171,14 +1179,19 @@ __device__ __forceinline__ void gemm_fc_h3p_body(const GemmArgs& p, char* smem) 
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   bf16x8 as[4][3];
+  bf16x8 b0[3], b1[3];
+  if constexpr (PF) {
+    read_b(smem, 0, b0);
+    read_a(smem, as);
+  }
   int slot = 0;
   for (int s = 0; s < nk; ++s) {
     const char* base = smem + slot * FCP_STAGE;
     const int nslot = slot + 1 == NS ? 0 : slot + 1;
-    bf16x8 b0[3], b1[3];
     // the stage's first B fragment, then its A fragments in MFMA order: the first MFMAs wait for
     // 4 reads, not 10 (TM 128, probe: round 1's order, A first)
-    if constexpr ((TM & 128) != 0) {
+    if constexpr (PF) {
+    } else if constexpr ((TM & 128) != 0) {
       read_a(base, as);
       read_b(base, 0, b0);
     } else {
@@ -1191,6 +1204,12 @@ __device__ __forceinline__ void gemm_fc_h3p_body(const GemmArgs& p, char* smem) 
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb) acc[mb][nb] = planes_mfma<2>(acc[mb][nb], as[mb], (nb & 1) ? b1 : b0);
       pin();
+    }
+    if constexpr (PF) {
+      if (s + 1 < nk) {   // stage s+1 landed at barrier s-1
+        read_b(smem + nslot * FCP_STAGE, 0, b0);
+        read_a(smem + nslot * FCP_STAGE, as);
+      }
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");

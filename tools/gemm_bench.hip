@@ -132,7 +132,8 @@ int fc1_bench(int nb, int rounds, int splits) {
             {"fcr_m", fc1r_launch<0>}, {"fcr_n", fc1r_launch<0>}, {"fcr_x", fc1r_launch<0>},
             {"fcr_x_noload", fc1r_launch<2>}, {"fcr_x_hotAB", fc1r_launch<8>},
             {"fc4_m", fc1r_launch<0, 4>}, {"fc4_x", fc1r_launch<0, 4>},
-            {"fcp_m", fc1p_launch<0>}, {"fcp_m_a1st", fc1p_launch<128>}, {"fcp_x", fc1p_launch<0>},
+            {"fcp_m", fc1p_launch<0>}, {"fcp_m_pf", fc1p_launch<256>}, {"fcp_x", fc1p_launch<0>},
+            {"fcp_x_pf", fc1p_launch<256>},
             {"fcp_x_noload", fc1p_launch<2>},
             {"fcp_x_hotAB", fc1p_launch<8>}};
   constexpr int NV = sizeof(vs) / sizeof(vs[0]);
