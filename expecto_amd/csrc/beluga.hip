@@ -485,10 +485,18 @@ __global__ void seg_delta_pool(const float* __restrict__ conv4, int t4, const fl
   store_act_rt(fmt, out, (long long)m * kDW[4] + gi, 480, c, mx);
 }
 
-// alt conv6 phase blocks: the ref block (t6 rows) with rows [r6, r6+20) from the alt run
+// alt conv6 phase blocks: the ref block (t6 rows) with rows [r6, r6+20) from the alt run.  Only
+// the rows some alt window reads are written: a window at offset o (strand orientation) holds the
+// SNV at q iff o <= q < o + 2000, and reads rows [o/16, o/16 + 106) of its phase block, so every
+// alt window lies in [(q-1999)/16, q/16 + 106) -- at most kAltRows6 rows (was: the whole block,
+// 2 x 425 MB per chunk of the 200-window workload).
+constexpr int kAltRows6 = 232;   // ceil(1999/16) + 106 + 1
 __global__ void seg_alt_blocks(const float* __restrict__ ref6, const float* __restrict__ d6, int n_ph, int t6,
                                const int* __restrict__ tab, int row16, float* __restrict__ out) {
-  const int t = blockIdx.x, m = blockIdx.y;
+  const int m = blockIdx.y;
+  const int q = tab[(m / n_ph) * kSegTab];
+  const int t = (q >= 1999 ? (q - 1999) >> 4 : 0) + blockIdx.x;
+  if (t >= t6 || t >= (q >> 4) + 106) return;
   const int r6 = tab[(m / n_ph) * kSegTab + 13 + m % n_ph];
   const floatx4* src = (t >= r6 && t < r6 + kDW[6])
                            ? reinterpret_cast<const floatx4*>(d6) + ((long long)m * kDW[6] + t - r6) * row16
@@ -723,6 +731,7 @@ struct expecto_beluga {
   int fc2_splits = kFc2SplitsDefault; // FC2 split-K slabs: a divisor of 63 K blocks
   double fc1_m_order_mb = 128.0;      // FC1 dispatch: M tiles fastest while one split's A is <= this
   int conv_tile = 0;                  // f16x3 conv M tile: 0 = auto (conv_tile_rows), 256 or 384
+  int seg_chunk_windows = 0;          // segment path: windows per chunk cap (0 = none; tuning knob)
   int cus = 0;                        // compute units of the device (workgroups per round)
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;
@@ -1219,13 +1228,16 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
   const int strands = mode == EXPECTO_STRAND_BOTH ? 2 : 1;
   // alt runs: one block per segment (conv1..4) or per (segment, phase) (pool2, conv5, conv6)
   const int blk_per_seg = pr ? std::max(n_ph, 1) : 0;
-  // chunks of whole segments: grow while the segment buffers, the FC workspace (<= max_batch
-  // windows) and the alt-run buffers (<= max_batch blocks) fit
+  // chunks of whole segments: grow while the segment buffers and the alt-run buffers (<= max_batch
+  // blocks) fit.  The FC stage of a chunk runs in slices of <= max_batch windows (its workspace),
+  // so a chunk is not bounded by its window count: one large chunk instead of several keeps every
+  // conv launch's last partial round of 256 workgroups to one per chunk (the 200-window workload:
+  // 96 segments per strand in one chunk instead of 40 + 40 + 16)
   std::vector<std::pair<int, int>> chunks;
   for (int s0 = 0; s0 < n_seg;) {
     int s1 = s0 + 1;
-    while (s1 < n_seg && s1 - s0 < seg_cap && first[s1 + 1] - first[s0] <= h->max_batch &&
-           (long long)(s1 + 1 - s0) * blk_per_seg <= h->max_batch)
+    while (s1 < n_seg && s1 - s0 < seg_cap && (long long)(s1 + 1 - s0) * blk_per_seg <= h->max_batch &&
+           (h->seg_chunk_windows <= 0 || first[s1 + 1] - first[s0] <= h->seg_chunk_windows))
       ++s1;
     chunks.push_back({s0, s1});
     s0 = s1;
@@ -1271,7 +1283,6 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
     for (const auto& chunk : chunks) {
       const int s0 = chunk.first, s1 = chunk.second;
       const int w0 = first[s0], nw = first[s1] - first[s0];
-      EXPECTO_REQUIRE(nw <= h->max_batch, "more windows in one segment than max_batch");
       const int ns = s1 - s0;
       const long long nb = (long long)ns * n_ph;
       // Alt runs (segment pairs) on the handle's second stream `sa`: the alt input patch of
@@ -1367,47 +1378,57 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
         const int4 phi = make_int4(ph_idx[0], ph_idx[1], ph_idx[2], ph_idx[3]);
         const long long row_base = (long long)sd * strand_rows;
         const int* widx = pr ? h->fc_perm_d + (size_t)sd * n_win + w0 : nullptr;   // FC row order
-        seg_a_rows<<<dim3((nw + 255) / 256), dim3(256), 0, st>>>(h->win_seg_d, h->win_off_d,
-                                                                 win_row ? h->win_row_d : nullptr, widx, w0, nw, s0,
-                                                                 is_rc ? 1 : 0, L, n_ph, phi, g.T6, row_base,
-                                                                 h->a_rows, h->c_rows);
-        if ((rc = check_launch("seg_a_rows"))) return rc;
-        if ((rc = run_fc(h, h->P, h->a_rows, nw, y, st, h->c_rows))) return rc;
+        // windows of this chunk holding the SNV (alt FC: the first n_alt FC rows, widx order) and
+        // the others (copies of the ref rows)
+        int n_alt = 0, ic0 = 0, ic1 = 0;
         if (pr) {
-          // windows of this chunk holding the SNV (alt FC) and the others (copies of the ref rows)
-          const int ia0 = (int)(std::lower_bound(alt_w.begin(), alt_w.end(), w0) - alt_w.begin());
-          const int ia1 = (int)(std::lower_bound(alt_w.begin(), alt_w.end(), w0 + nw) - alt_w.begin());
-          const int ic0 = (int)(std::lower_bound(copy_w.begin(), copy_w.end(), w0) - copy_w.begin());
-          const int ic1 = (int)(std::lower_bound(copy_w.begin(), copy_w.end(), w0 + nw) - copy_w.begin());
-          if ((rc = st_wait(h->pev[13]))) return rc;   // alt conv6 runs (and the Q reads of their patches)
-          if (ia1 > ia0) {  // alt conv6 blocks into Q (conv5 rows are dead), then their FC
-            seg_alt_blocks<<<dim3(g.T6, (unsigned)nb), dim3(64), 0, st>>>(h->P, h->D0, n_ph, g.T6, h->seg_tab,
-                                                                         640 * eb / 16, h->Q);
+          n_alt = (int)(std::lower_bound(alt_w.begin(), alt_w.end(), w0 + nw) -
+                        std::lower_bound(alt_w.begin(), alt_w.end(), w0));
+          ic0 = (int)(std::lower_bound(copy_w.begin(), copy_w.end(), w0) - copy_w.begin());
+          ic1 = (int)(std::lower_bound(copy_w.begin(), copy_w.end(), w0 + nw) - copy_w.begin());
+        }
+        // FC slices of <= max_batch rows (the FC workspace); the alt FC of a slice's alt rows
+        // reuses that slice's ref partials, so it runs right after the slice's ref FC
+        for (int f0 = 0; f0 < nw; f0 += h->max_batch) {
+          const int fn = std::min(h->max_batch, nw - f0);
+          seg_a_rows<<<dim3((fn + 255) / 256), dim3(256), 0, st>>>(
+              h->win_seg_d, h->win_off_d, win_row ? h->win_row_d : nullptr, widx ? widx + f0 : nullptr, w0 + f0,
+              fn, s0, is_rc ? 1 : 0, L, n_ph, phi, g.T6, row_base, h->a_rows, h->c_rows);
+          if ((rc = check_launch("seg_a_rows"))) return rc;
+          if ((rc = run_fc(h, h->P, h->a_rows, fn, y, st, h->c_rows))) return rc;
+          const int na = std::min(n_alt - f0, fn);   // alt rows of this slice: [f0, f0 + na)
+          if (na <= 0) continue;
+          if (f0 == 0) {
+            if ((rc = st_wait(h->pev[13]))) return rc;   // alt conv6 runs (and the Q reads of their patches)
+            // alt conv6 blocks into Q (conv5 rows are dead): only the rows the alt windows read
+            seg_alt_blocks<<<dim3(kAltRows6, (unsigned)nb), dim3(64), 0, st>>>(h->P, h->D0, n_ph, g.T6, h->seg_tab,
+                                                                              640 * eb / 16, h->Q);
             if ((rc = check_launch("seg_alt_blocks"))) return rc;
-            const int n_alt = ia1 - ia0;   // the first n_alt FC rows of the chunk (widx)
-            seg_a_rows<<<dim3((n_alt + 255) / 256), dim3(256), 0, st>>>(
-                h->win_seg_d, h->win_off_d, win_row ? h->win_row_d : nullptr, widx, 0, n_alt, s0,
-                is_rc ? 1 : 0, L, n_ph, phi, g.T6, row_base, h->a_rows, h->c_rows);
-            if ((rc = check_launch("seg_a_rows"))) return rc;
-            const unsigned* mask = nullptr;
-            double frac = 1.0;
-            if (planes_gemm()) {
-              const int tiles = (int)((n_alt + gemm_bm() - 1) / gemm_bm());
-              unsigned* md = reinterpret_cast<unsigned*>(h->slab_mask);
-              EXPECTO_HIP_CHECK(hipMemsetAsync(md, 0, tiles * sizeof(unsigned), st));
-              fc1_slab_mask_seg<<<dim3((n_alt + 255) / 256), dim3(256), 0, st>>>(
-                  widx, n_alt, h->win_seg_d, h->win_off_d, s0, is_rc ? 1 : 0, L, phi, h->seg_tab, (int)gemm_bm(),
-                  kFc1In / h->fc_splits, md);
-              if ((rc = check_launch("fc1_slab_mask_seg"))) return rc;
-              mask = md;
-              if (h->profiling) {   // executed share of the slabs, counted on the device (no sync)
-                if ((rc = count_slab_macs(h, md, tiles, n_alt, st))) return rc;
-                frac = 0.0;
-              }
-            }
-            DeltaScope ds(h);
-            if ((rc = run_fc(h, h->Q, h->a_rows, n_alt, pr->y_alt, st, h->c_rows, mask, frac, nw))) return rc;
           }
+          seg_a_rows<<<dim3((na + 255) / 256), dim3(256), 0, st>>>(
+              h->win_seg_d, h->win_off_d, win_row ? h->win_row_d : nullptr, widx + f0, 0, na, s0, is_rc ? 1 : 0,
+              L, n_ph, phi, g.T6, row_base, h->a_rows, h->c_rows);
+          if ((rc = check_launch("seg_a_rows"))) return rc;
+          const unsigned* mask = nullptr;
+          double frac = 1.0;
+          if (planes_gemm()) {
+            const int tiles = (int)((na + gemm_bm() - 1) / gemm_bm());
+            unsigned* md = reinterpret_cast<unsigned*>(h->slab_mask);
+            EXPECTO_HIP_CHECK(hipMemsetAsync(md, 0, tiles * sizeof(unsigned), st));
+            fc1_slab_mask_seg<<<dim3((na + 255) / 256), dim3(256), 0, st>>>(
+                widx + f0, na, h->win_seg_d, h->win_off_d, s0, is_rc ? 1 : 0, L, phi, h->seg_tab, (int)gemm_bm(),
+                kFc1In / h->fc_splits, md);
+            if ((rc = check_launch("fc1_slab_mask_seg"))) return rc;
+            mask = md;
+            if (h->profiling) {   // executed share of the slabs, counted on the device (no sync)
+              if ((rc = count_slab_macs(h, md, tiles, na, st))) return rc;
+              frac = 0.0;
+            }
+          }
+          DeltaScope ds(h);
+          if ((rc = run_fc(h, h->Q, h->a_rows, na, pr->y_alt, st, h->c_rows, mask, frac, fn))) return rc;
+        }
+        if (pr) {
           if (ic1 > ic0) {
             copy_rows<<<dim3(ic1 - ic0), dim3(256), 0, st>>>(y, pr->y_alt, h->copy_w_d + ic0,
                                                              win_row ? h->win_row_d : nullptr, row_base);
@@ -1684,6 +1705,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   }
   if (const char* e = getenv("EXPECTO_FC1_M_ORDER_MB")) h->fc1_m_order_mb = atof(e);   // same bits either way
   if (const char* e = getenv("EXPECTO_OVERLAP")) h->overlap = atoi(e) != 0;   // same bits either way
+  if (const char* e = getenv("EXPECTO_SEG_CHUNK_WINDOWS")) h->seg_chunk_windows = atoi(e);   // same bits either way
   if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)
     const int v = atoi(e);
     EXPECTO_REQUIRE(v == 0 || v == 256 || v == 384, "EXPECTO_CONV_TILE must be 0 (auto), 256 or 384");

@@ -94,10 +94,10 @@ def test_variant_feature_reduction_matches_predict_py():
         assert_close(out[name], feats[name], rtol=1e-9, atol=1e-12, what=f"variant features {name}")
 
 
-def _engine(precision="bf16x6"):
+def _engine(precision="bf16x6", max_batch=300):
     import math
     from expecto_amd import beluga
-    eng = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=300).cuda().engine()
+    eng = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=max_batch).cuda().engine()
     eng.set_precision(precision)
     return eng
 
@@ -202,12 +202,14 @@ def test_variant_pipeline_pairs_equal_per_window():
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("precision", ["bf16x6", "f16x3", "fp32"])
-def test_segment_pairs_alt_runs_are_bitwise_equal(precision):
+@pytest.mark.parametrize("precision,max_batch", [("bf16x6", 300), ("f16x3", 300), ("fp32", 300), ("f16x3", 40)])
+def test_segment_pairs_alt_runs_are_bitwise_equal(precision, max_batch):
     """forward_segment_pairs == full forwards of every ref and alt window, for SNVs at the
-    segment edges and in the middle, windows at the first/last offsets, both strands."""
+    segment edges and in the middle, windows at the first/last offsets, both strands.
+    max_batch 40: 10-segment chunks of 80 windows, each chunk's FC in two slices of 40 rows with
+    alt windows in both (the alt FC of a slice reuses that slice's ref partials)."""
     import torch
-    eng = _engine(precision)
+    eng = _engine(precision, max_batch)
     rng = np.random.default_rng(11)
     L = 2000 + 1600
     q = np.array([0, 3, 7, 500, 1234, 1799, 1800, 2001, 3000, L - 9, L - 2, L - 1], np.int32)
