@@ -52,6 +52,8 @@ SIGNATURES = {
     "expecto_beluga_layer_times": (ctypes.c_int, [c_vp, c_f64p, c_i64p, c_f64p, ctypes.c_int]),
     "expecto_variant_windows": (ctypes.c_int, [c_vp, ctypes.c_longlong, c_vp, c_vp, c_vp, ctypes.c_int, c_vp,
                                                ctypes.c_int, c_vp, c_vp]),
+    "expecto_indel_windows": (ctypes.c_int, [c_vp, ctypes.c_longlong, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                             ctypes.c_int, c_vp, c_vp]),
     "expecto_tss_windows": (ctypes.c_int, [c_vp, ctypes.c_longlong, c_vp, c_vp, ctypes.c_int, c_vp, ctypes.c_int,
                                            c_vp, c_vp]),
     "expecto_diff": (ctypes.c_int, [c_vp, c_vp, ctypes.c_longlong, c_vp, c_vp]),

@@ -1051,6 +1051,16 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     a.split_stride = (long long)nb * kHidLd;
     LayerTimer lt(h, 8, st);
     if (h->profiling) h->macs[h->timer_base + 8] += (double)nb * kNFeat * kFc1Out;
+    if (h->fc2_splits == 1) {
+      // no split: bias + sigmoid in the GEMM epilogue, rows scattered through c_rows (the
+      // same per-element unscale, bias and expf as fc2_reduce over one slab: same bits)
+      a.C = y;
+      a.ldc = kNFeat;
+      a.c_rows = c_rows;
+      a.bias = h->fc2b;
+      a.s_in = a.t_valid = a.s_out = 1;
+      return launch_gemm<8, EPI_SIGMOID>(a, 1, st);
+    }
     if ((rc = launch_gemm<8, EPI_PARTIAL>(a, h->fc2_splits, st))) return rc;
     const long long count = (long long)nb * kNFeat;
     fc2_reduce<<<dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st>>>(

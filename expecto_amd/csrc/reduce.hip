@@ -44,6 +44,38 @@ __global__ void variant_windows_kernel(const uint8_t* __restrict__ genome, long 
   *reinterpret_cast<unsigned*>(codes + ((long long)(allele * n_shift + j) * n + v) * kLen + i4) = packed;
 }
 
+// Indel / MNP windows (chromatin.py:202-209 then the centre crop of :164) for items whose
+// 2100-base fetch window lies inside its contig, with 0 <= mutpos, mutpos + lref <= 2100 and a
+// spliced length >= 2000 (the host keeps the rest, chromatin.py's Python-slicing corner cases).
+// Spliced sequence S = G[s0, s0+mutpos) + allele + G[s0+mutpos+lref, s0+2100); output code i =
+// S[crop + i], crop = floor((len(S) - 2000) / 2).  Item t: start0[t] = s0, the allele's codes at
+// allele_codes[allele_off[t] .. + lalt[t]).  4 codes per thread (uint32 stores).
+__global__ void indel_windows_kernel(const uint8_t* __restrict__ genome, long long genome_len,
+                                     const long long* __restrict__ start0, const int* __restrict__ mutpos,
+                                     const int* __restrict__ lref, const int* __restrict__ lalt,
+                                     const int* __restrict__ crop, const int* __restrict__ allele_off,
+                                     const uint8_t* __restrict__ allele_codes, uint8_t* __restrict__ codes) {
+  const long long t = blockIdx.y;
+  const int i4 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i4 >= kLen) return;
+  const long long s0 = start0[t];
+  const int mp = mutpos[t], lr = lref[t], la = lalt[t], c0 = crop[t], ao = allele_off[t];
+  unsigned packed = 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int k = c0 + i4 + e;
+    unsigned c;
+    if (k >= mp && k < mp + la) {
+      c = allele_codes[ao + k - mp];
+    } else {
+      const long long g = s0 + (k < mp ? k : k - la + lr);
+      c = (g >= 0 && g < genome_len) ? genome[g] : 4u;
+    }
+    packed |= c << (8 * e);
+  }
+  *reinterpret_cast<unsigned*>(codes + t * kLen + i4) = packed;
+}
+
 // TSS tiling (compute_expecto_features.py:107-111): window of gene g at shift s covers the
 // 1-based positions tss + s*strand - 999 .. tss + s*strand + 1000 -> 0-based offset
 // tss_off[g] + s*strand - 999 + i.  Output codes[(g*n_shift + j)*2000 + i].
@@ -342,6 +374,19 @@ int expecto_variant_windows(const uint8_t* genome, long long genome_len, const l
   variant_windows_kernel<<<grid, dim3(256), 0, as_stream(stream)>>>(genome, genome_len, var_off, ref_code, alt_code, n,
                                                                     shifts, n_shift, codes);
   return check_launch("variant_windows");
+}
+
+int expecto_indel_windows(const uint8_t* genome, long long genome_len, const long long* start0, const int* mutpos,
+                          const int* lref, const int* lalt, const int* crop, const int* allele_off,
+                          const uint8_t* allele_codes, int n, uint8_t* codes, void* stream) {
+  EXPECTO_REQUIRE(n >= 0 && n <= 65535, "0..65535 indel windows per call");
+  if (n == 0) return EXPECTO_OK;
+  EXPECTO_REQUIRE(genome && start0 && mutpos && lref && lalt && crop && allele_off && allele_codes && codes,
+                  "null argument");
+  dim3 grid((kLen / 4 + 255) / 256, n);
+  indel_windows_kernel<<<grid, dim3(256), 0, as_stream(stream)>>>(genome, genome_len, start0, mutpos, lref, lalt, crop,
+                                                                  allele_off, allele_codes, codes);
+  return check_launch("indel_windows");
 }
 
 int expecto_tss_windows(const uint8_t* genome, long long genome_len, const long long* tss_off, const int8_t* strand,

@@ -32,6 +32,14 @@ def init(backend: str | None = None):
     return rank, world, local
 
 
+def _single(world: int) -> bool:
+    """True when there is nothing to exchange: one rank and no process group.  A process group of
+    one rank (the RCCL smoke test on a one-GPU box) still runs the collectives."""
+    import torch.distributed as dist
+
+    return world == 1 and not (dist.is_available() and dist.is_initialized())
+
+
 def shard_range(n: int, rank: int, world: int):
     """Contiguous [lo, hi) range of n items for `rank` (first n % world ranks get one more)."""
     q, r = divmod(n, world)
@@ -64,7 +72,7 @@ def gather_rows(t: torch.Tensor, dim: int, n_total: int, world: int):
     shards (RCCL ring over xGMI on the GPU)."""
     import torch.distributed as dist
 
-    if world == 1:
+    if _single(world):
         return t
     pad = _padded(t, dim, n_total, world)
     parts = [torch.empty_like(pad) for _ in range(world)]
@@ -79,7 +87,7 @@ def gather_rows_to(t: torch.Tensor, dim: int, n_total: int, world: int, rank: in
     each shard once over xGMI into `dst`, and no other rank allocates the full size."""
     import torch.distributed as dist
 
-    if world == 1:
+    if _single(world):
         return t
     pad = _padded(t, dim, n_total, world)
     if pad.is_cuda and dist.get_backend() == "gloo":
@@ -96,7 +104,7 @@ def gather_blocks_to(t: torch.Tensor, dim: int, counts, world: int, rank: int, d
     None elsewhere."""
     import torch.distributed as dist
 
-    if world == 1:
+    if _single(world):
         return [t]
     m = max(counts)
     x = t.movedim(dim, 0)

@@ -170,17 +170,77 @@ class VariantPipeline:
         if rows == "variant" and (prep["seg"] is None or ind_idx.size):
             raise ValueError('rows="variant" needs SNVs on 4-aligned shifts (the segment path)')
         if ind_idx.size:
-            # indels / MNPs: length-changing splice + floor crop on the host (chromatin.py:164,209)
-            host = np.empty((2, S, ind_idx.size, 2000), np.uint8)
-            for k, v in enumerate(ind_idx):
-                for j, sh in enumerate(shifts):
-                    for a, allele in enumerate((vs.ref[v], vs.alt[v])):
-                        w = fetch_window(self.fasta, vs.chrom[v], int(vs.pos[v]), vs.ref[v], allele, sh)
-                        c = seq_codes(w)
-                        host[a, j, k, :] = 4
-                        host[a, j, k, :c.size] = c
-            prep["ind_codes"] = torch.from_numpy(host).to(dev)
+            prep["ind_codes"] = self._indel_window_codes(vs, ind_idx, shifts)
         return prep
+
+    def _indel_window_codes(self, vs: VariantSet, ind_idx: np.ndarray, shifts) -> torch.Tensor:
+        """uint8 [2 alleles, S, n_ind, 2000] windows of indels / MNPs: the length-changing splice
+        of fetchSeqs and the floor centre crop of encodeSeqs (chromatin.py:164,202-209).  Items
+        whose 2100-base fetch window lies inside the contig with the splice inside it and a
+        spliced length >= 2000 are built on the device (expecto_indel_windows, one kernel for the
+        batch); the rest -- the reference's Python-slicing corner cases (negative slice starts,
+        windows cut by the contig end) -- through the host twin fetch_window + seq_codes."""
+        S, ni = len(shifts), ind_idx.size
+        A, J, K = (x.ravel() for x in np.meshgrid(np.arange(2), np.arange(S), np.arange(ni), indexing="ij"))
+        v = ind_idx[K]
+        sh = np.asarray(shifts, np.int64)[J]
+        pos = np.asarray(vs.pos, np.int64).reshape(-1)[v]
+        chroms = [vs.chrom[x] for x in v]
+        lens = np.array([[len(vs.ref[x]), len(vs.alt[x])] for x in ind_idx], np.int64).reshape(ni, 2)
+        lref, lalt = lens[K, 0], lens[K, A]
+        mut = 1049 - sh                                  # mutpos of fetchSeqs (windowsize 2100)
+        ls = 2100 - lref + lalt                          # spliced length
+        crop = (ls - 2000) // 2                          # floor((len - 2000) / 2), chromatin.py:164
+        cs = pos + sh - 1050                             # window start inside the contig (0-based)
+        clen = np.array([self.dg.lengths[c] for c in chroms], np.int64)
+        acodes = [[_LUT[np.frombuffer(vs.ref[x].encode("latin-1"), np.uint8)],
+                   _LUT[np.frombuffer(vs.alt[x].encode("latin-1"), np.uint8)]] for x in ind_idx]
+        valid = np.array([[(c != 255).all() for c in pair] for pair in acodes], bool).reshape(ni, 2)
+        dev_ok = (cs >= 0) & (cs + 2100 <= clen) & (mut >= 0) & (mut + lref <= 2100) & (ls >= 2000) & valid[K, A]
+        s0 = np.array([self.dg.offsets[c] for c in chroms], np.int64) + cs
+        # encodeSeqs' KeyError on characters outside A/C/G/T/N/H/- in the visible genome bases
+        bad = self.dg.host.invalid_offsets
+        if bad.size and dev_ok.any():
+            d = np.nonzero(dev_ok)[0]
+            lo1, hi1 = s0[d] + crop[d], s0[d] + np.minimum(mut[d], crop[d] + 2000)
+            lo2 = s0[d] + np.maximum(mut[d] + lalt[d], crop[d]) - lalt[d] + lref[d]
+            hi2 = s0[d] + crop[d] + 2000 - lalt[d] + lref[d]
+            for lo, hi in ((lo1, hi1), (lo2, hi2)):
+                i = np.searchsorted(bad, lo)
+                hit = (i < bad.size) & (bad[np.minimum(i, bad.size - 1)] < hi) & (lo < hi)
+                if hit.any():
+                    b = bad[i[np.nonzero(hit)[0][0]]]
+                    raise KeyError(chr(self.dg.host.invalid_chars[np.searchsorted(bad, b)]))
+        flat = [c for pair in acodes for c in pair]      # allele (k, a) -> flat index 2k + a
+        aoff = np.concatenate([[0], np.cumsum([c.size for c in flat])]).astype(np.int64)
+        table = np.concatenate(flat + [np.zeros(1, np.uint8)]).astype(np.uint8)
+        n_items = 2 * S * ni
+        out = torch.empty((n_items, 2000), dtype=torch.uint8, device=self.device)
+        d = np.nonzero(dev_ok)[0]
+        if d.size:
+            dev = self.device
+            tab = torch.from_numpy(table).to(dev)
+            cols = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in
+                    (s0[d], mut[d].astype(np.int32), lref[d].astype(np.int32), lalt[d].astype(np.int32),
+                     crop[d].astype(np.int32), aoff[2 * K[d] + A[d]].astype(np.int32))]
+            blk = torch.empty((d.size, 2000), dtype=torch.uint8, device=dev)
+            st = _lib.stream_ptr()
+            for i0 in range(0, d.size, 65535):
+                i1 = min(d.size, i0 + 65535)
+                _lib.check(self.lib.expecto_indel_windows(
+                    _lib.dptr(self.dg.codes), self.dg.codes.numel(), *(_lib.dptr(c[i0:i1]) for c in cols),
+                    _lib.dptr(tab), i1 - i0, _lib.dptr(blk[i0:i1]), st), "indel_windows")
+            out[torch.from_numpy(d).to(dev)] = blk
+        h = np.nonzero(~dev_ok)[0]
+        if h.size:
+            host = np.full((h.size, 2000), 4, np.uint8)
+            for r, t in enumerate(h):
+                x = int(v[t])
+                allele = vs.alt[x] if A[t] else vs.ref[x]
+                c = seq_codes(fetch_window(self.fasta, vs.chrom[x], int(vs.pos[x]), vs.ref[x], allele, int(sh[t])))
+                host[r, :c.size] = c
+            out[torch.from_numpy(h).to(self.device)] = torch.from_numpy(host).to(self.device)
+        return out.view(2, S, ni, 2000)
 
     def _snv_window_codes(self, prep: dict) -> torch.Tensor:
         """uint8 [2 alleles, S, n_snv, 2000] per-window codes on the device."""

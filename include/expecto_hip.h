@@ -18,6 +18,8 @@
  *                                  is generated inside the conv1 kernel from base codes
  *   expecto_variant_windows        fetchSeqs window splice for SNVs (chromatin.py:175-209)
  *                                  from a device-resident genome
+ *   expecto_indel_windows          fetchSeqs splice + centre crop for indels / MNPs
+ *                                  (chromatin.py:164,202-209) from a device-resident genome
  *   expecto_tss_windows            TSS tiling genome.sequence(...) + encodeSeqs
  *                                  (compute_expecto_features.py:107-113)
  *   expecto_diff                   diff = alt - ref (chromatin.py:281)
@@ -199,6 +201,17 @@ int expecto_beluga_layer_times(expecto_beluga_t h, double* ms, long long* calls,
 int expecto_variant_windows(const uint8_t* genome, long long genome_len, const long long* var_off,
                             const uint8_t* ref_code, const uint8_t* alt_code, int n,
                             const int* shifts, int n_shift, uint8_t* codes, void* stream);
+
+/* Indel / MNP windows (chromatin.py:202-209, centre crop :164).  Item t's 2100-base fetch
+ * window starts at 0-based genome offset start0[t]; the allele (lalt[t] codes at
+ * allele_codes[allele_off[t]..]) replaces lref[t] bases at mutpos[t]; output
+ * codes[t*2000 + i] = S[crop[t] + i] of the spliced sequence S (crop = floor((len(S)-2000)/2)).
+ * Callers keep items with a window past the contig, mutpos < 0, mutpos + lref > 2100 or
+ * len(S) < 2000 on the host (the reference's Python-slicing corner cases). */
+int expecto_indel_windows(const uint8_t* genome, long long genome_len, const long long* start0,
+                          const int* mutpos, const int* lref, const int* lalt, const int* crop,
+                          const int* allele_off, const uint8_t* allele_codes, int n, uint8_t* codes,
+                          void* stream);
 
 /* TSS tiling windows (compute_expecto_features.py:107-111): gene g, shift j covers the
  * 0-based genome offsets tss_off[g] + shifts[j]*strand[g] - 999 + i, i = 0..1999

@@ -349,3 +349,42 @@ def test_tss_compute_two_ranks_equals_one(workdir):
     a, b = np.load(one / name), np.load(two / name)
     assert a.shape == (3, 20020)
     np.testing.assert_array_equal(a, b)
+
+
+def test_indel_windows_device_equal_host_splice():
+    """Indel / MNP windows built by expecto_indel_windows equal the host fetch_window +
+    seq_codes (chromatin.py:164,202-209) for insertions, deletions, MNPs, an N in the allele,
+    deletions longer than 100 bp (spliced length < 2000: the host's Python-slicing path) and a
+    window cut by the contig end (host path)."""
+    from expecto_amd import synthetic
+    from expecto_amd.encode import seq_codes
+    from expecto_amd.genome import DeviceGenome, Fasta
+    from expecto_amd.pipeline import VariantPipeline, VariantSet, fetch_window, shift_order
+    g = synthetic.genome_bytes(**GENOME_ARGS)
+    fa = Fasta.from_dict(g)
+    pipe = VariantPipeline(_engine(), fa, DeviceGenome(fa))
+    rng = np.random.default_rng(31)
+    rows = []
+    names = sorted(g)
+    for lr, la in [(1, 2), (1, 7), (1, 60), (2, 1), (9, 1), (40, 1), (3, 3), (5, 2), (2, 5), (150, 1), (120, 4),
+                   (1, 1200)]:
+        c = names[int(rng.integers(0, len(names)))]
+        p = int(rng.integers(3000, len(g[c]) - 3000))
+        ref = g[c][p - 1:p - 1 + lr].decode().upper()
+        alt = "".join("ACGT"[int(x)] for x in rng.integers(0, 4, la))
+        rows.append((c, p, ref, alt))
+    rows.append((names[0], 5000, g[names[0]][4999:5001].decode().upper(), "ANT"))
+    c = names[1]
+    p = len(g[c]) - 900                                   # the +800 windows run past the contig end
+    rows.append((c, p, g[c][p - 1:p + 1].decode().upper(), "G"))
+    vs = VariantSet([r[0] for r in rows], np.array([r[1] for r in rows]), [r[2] for r in rows], [r[3] for r in rows])
+    shifts = shift_order(800)
+    got = pipe._indel_window_codes(vs, np.arange(len(rows)), shifts).cpu().numpy()
+    want = np.full(got.shape, 4, np.uint8)
+    for k, (c, p, r, a) in enumerate(rows):
+        for j, sh in enumerate(shifts):
+            for ai, allele in enumerate((r, a)):
+                cc = seq_codes(fetch_window(fa, c, p, r, allele, sh))
+                want[ai, j, k, :cc.size] = cc
+    bad = np.argwhere((got != want).any(-1))
+    assert bad.size == 0, f"(allele, shift, item) rows differ: {bad[:8].tolist()}"
