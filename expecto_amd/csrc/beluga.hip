@@ -108,6 +108,132 @@ __global__ __launch_bounds__(320) void beluga_conv1(const float* __restrict__ x,
   }
 }
 
+// conv1 on MFMA (f16x3 path).  One-hot inputs are exact in fp16, so conv1 is a K = 32 GEMM
+// (k = tap*4 + channel) whose A row t is the 32 halves of positions t..t+7: per 16-row block a
+// lane builds its A fragment (positions t + 2fq and t + 2fq + 1, 4 channels each) from two base
+// codes in registers -- no im2col, no LDS read for A.  B = the conv1 weights as per-row scaled
+// fp16 planes (hi, lo), held in registers: wave w owns output channels 64w..64w+63 (two 32-channel
+// plane groups, 4 MFMA column blocks).  Products x_lo*w_hi (float inputs only: the 22-bit split
+// of a one-hot value has x_lo = 0), x*w_lo, x*w_hi accumulate in fp32 -- the same arithmetic
+// class as every other f16x3 layer, so codes and one-hot floats give the same bits.  Epilogue:
+// unscale, bias, ReLU and the conv2-input scale in one FMA + max (the scales are powers of 2),
+// canonical split, staged per wave through LDS so each row's two 128-B plane groups leave as
+// 16-B stores (the VALU kernel's 2-byte stores and 32 FMAs per output were its limit).
+// 5 waves; 256 output rows per workgroup in 32-row steps.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int C1H_ROWS = 256, C1H_STEP = 32;
+constexpr int C1H_WROW = 2 * 128 + 16;   // staged bytes per row and wave (2 plane groups + pad)
+
+__device__ __forceinline__ unsigned onehot_h2(unsigned c, unsigned hi_pair) {
+  // fp16 1.0 (0x3C00) in the half of channel c within the channel pair (0,1) or (2,3)
+  return (c >> 1) == hi_pair ? (0x3C00u << ((c & 1u) * 16u)) : 0u;
+}
+
+__global__ __launch_bounds__(320) void beluga_conv1_h3(const float* __restrict__ x, const uint8_t* __restrict__ codes,
+                                                       long long code_stride, int n_src, int mode, long long row0,
+                                                       const _Float16* __restrict__ wpl, const float* __restrict__ cs1,
+                                                       const float* __restrict__ b1, float* __restrict__ out,
+                                                       int out_rows, int len, float osc, int* __restrict__ ovf) {
+  __shared__ unsigned char cl[C1H_ROWS + 8];
+  __shared__ __attribute__((aligned(16))) char stg[5][C1H_STEP * C1H_WROW];
+  const int t0 = blockIdx.x * C1H_ROWS;
+  const long long win = blockIdx.y;
+  const long long r = row0 + win;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int T = len - 7;
+  long long src = r;
+  bool rc = (mode == EXPECTO_STRAND_RC);
+  if (mode == EXPECTO_STRAND_BOTH && r >= n_src) {
+    src = r - n_src;
+    rc = true;
+  }
+  if (!x) {
+    for (int j = tid; j < C1H_ROWS + 7; j += 320) {
+      const int pos = t0 + j;
+      unsigned c = 4;
+      if (pos < len) {
+        c = codes[src * code_stride + (rc ? len - 1 - pos : pos)];
+        if (rc && c < 4) c = 3 - c;
+      }
+      cl[j] = (unsigned char)c;
+    }
+  }
+  const int fr = lane & 15, fq = lane >> 4;
+  halfx8 bh[4], bl[4];
+  float sc[4], bb[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    const int n = 64 * wave + 16 * cb + fr;
+    bh[cb] = *reinterpret_cast<const halfx8*>(wpl + n * 64 + 8 * fq);
+    bl[cb] = *reinterpret_cast<const halfx8*>(wpl + n * 64 + 32 + 8 * fq);
+    sc[cb] = cs1[n] * osc;
+    bb[cb] = b1[n] * osc;
+  }
+  __syncthreads();
+  char* const sw = stg[wave];
+  float vmax = 0.f;
+  bool bad = false;
+  const int tend = min(C1H_ROWS, T - t0);
+  for (int s = 0; s < tend; s += C1H_STEP) {
+    floatx4v acc[2][4];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int tr = s + 16 * rb + fr + 2 * fq;     // first of the lane's two positions (tile-relative)
+      halfx8 ah, al;
+      if (!x) {
+        const unsigned c0 = cl[tr], c1 = cl[tr + 1];
+        const u32x4 u = {onehot_h2(c0, 0), onehot_h2(c0, 1), onehot_h2(c1, 0), onehot_h2(c1, 1)};
+        ah = __builtin_bit_cast(halfx8, u);
+        al = halfx8{};
+      } else {
+        const float* xr = x + r * (4LL * len);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int pos = t0 + tr + (e >> 2);
+          const float v = pos < len ? xr[(e & 3) * (long long)len + pos] : 0.f;
+          bad |= !(fabsf(v) < 65504.f);   // out of fp16 range (or NaN): recomputed in bf16x6
+          _Float16 h, l;
+          split_h2(v, h, l);
+          ah[e] = h;
+          al[e] = l;
+        }
+      }
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        floatx4v c = {0.f, 0.f, 0.f, 0.f};
+        if (x) c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[cb], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[cb], c, 0, 0, 0);
+        acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[cb], c, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float v = fmaxf(fmaf(acc[rb][cb][j], sc[cb], bb[cb]), 0.f);
+          vmax = fmaxf(vmax, v);
+          _Float16 h, l;
+          split_h2(v, h, l);
+          char* d = sw + (16 * rb + 4 * fq + j) * C1H_WROW + (cb >> 1) * 128 + ((cb & 1) * 16 + fr) * 2;
+          *reinterpret_cast<_Float16*>(d) = h;
+          *reinterpret_cast<_Float16*>(d + 64) = l;
+        }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < (C1H_STEP * 16) / 64; ++i) {   // 32 rows x 16 chunks of 16 B
+      const int k = i * 64 + lane, row = k >> 4, ch = k & 15;
+      if (s + row < tend) {
+        char* g = reinterpret_cast<char*>(out) + ((win * out_rows + t0 + s + row) * 10 + 2 * wave) * 128 + ch * 16;
+        *reinterpret_cast<floatx4*>(g) = *reinterpret_cast<const floatx4*>(sw + row * C1H_WROW + ch * 16);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  if ((bad || !(vmax < 65504.f)) && ovf) *ovf = 1;
+}
+
 __global__ void fc1_reduce(const float* __restrict__ part, int splits, long long split_stride, long long count,
                            const float* __restrict__ bias, float* __restrict__ h1, int fmt,
                            const float* __restrict__ col_scale, float osc, int* __restrict__ ovf) {
@@ -550,6 +676,13 @@ __global__ void repack_conv(const float* __restrict__ W, int cout, int cin, int 
   Wt[i] = n < cout ? W[((long long)n * cin + ci) * 8 + tap] : 0.f;
 }
 
+__global__ void repack_conv1(const float* __restrict__ w1, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // out index n*32 + tap*4 + ci
+  if (i >= 320 * 32) return;
+  const int n = i >> 5, k = i & 31, tap = k >> 2, ci = k & 3;
+  out[i] = w1[n * 32 + ci * 8 + tap];
+}
+
 __global__ void repack_fc1(const float* __restrict__ W, int npad, float* __restrict__ Wp) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long long)npad * kFc1In) return;
@@ -684,6 +817,8 @@ struct expecto_beluga {
   // device overflow flag.
   float* wh[7] = {};
   int* swd[7] = {};
+  float* w1h = nullptr;          // conv1 on MFMA: fp16 planes [320][hi 32 | lo 32] (k = tap*4 + ci),
+  float* cs1 = nullptr;          //   per-row unscale 2^-s_w[n] (one-hot input: no input scale)
   float* cs[7] = {};
   int sx[7] = {};
   int f16_target = 10;
@@ -930,6 +1065,13 @@ int run_conv1(expecto_beluga* h, const float* x, const uint8_t* codes, long long
               long long row0, int nb, int len, int out_rows, hipStream_t st, float* dst = nullptr) {
   LayerTimer lt(h, 0, st);
   if (h->profiling) h->macs[h->timer_base + 0] += (double)nb * (len - 7) * 320 * 32;
+  if (g_precision == EXPECTO_PRECISION_F16X3 && h->w1h) {
+    dim3 grid((len - 7 + C1H_ROWS - 1) / C1H_ROWS, nb);
+    beluga_conv1_h3<<<grid, dim3(320), 0, st>>>(x, codes, code_stride, n_src, mode, row0,
+                                                reinterpret_cast<const _Float16*>(h->w1h), h->cs1, h->b1,
+                                                dst ? dst : h->P, out_rows, len, exp2i(h->sx[0]), h->ovf);
+    return check_launch("beluga_conv1_h3");
+  }
   dim3 grid((len - 7 + C1_T - 1) / C1_T, nb);
   beluga_conv1<<<grid, dim3(320), 0, st>>>(x, codes, code_stride, n_src, mode, row0, h->w1, h->b1,
                                            dst ? dst : h->P, out_rows, len, act_fmt(), exp2i(h->sx[0]), h->ovf);
@@ -1627,6 +1769,18 @@ int f16_prepare(expecto_beluga* h, hipStream_t st) {
     split_planes_h2<<<dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st>>>(
         y.w, y.rows, (int)y.K, h->swd[g], reinterpret_cast<_Float16*>(h->wh[g]));
     if ((rc = check_launch("split_planes_h2"))) return rc;
+  }
+  {  // conv1 (beluga_conv1_h3): weights repacked to k = tap*4 + ci, per-row scaled planes
+    float *w1r = nullptr, *sw1 = nullptr;
+    if ((rc = dalloc(h, &w1r, 320 * 32)) || (rc = dalloc(h, &sw1, 320)) || (rc = dalloc(h, &h->cs1, 320)) ||
+        (rc = dalloc(h, &h->w1h, 320 * 32)))
+      return rc;
+    repack_conv1<<<dim3(40), dim3(256), 0, st>>>(h->w1, w1r);
+    row_scale_exp<<<dim3(320), dim3(256), 0, st>>>(w1r, 32, reinterpret_cast<int*>(sw1));
+    split_planes_h2<<<dim3(10), dim3(256), 0, st>>>(w1r, 320, 32, reinterpret_cast<int*>(sw1),
+                                                    reinterpret_cast<_Float16*>(h->w1h));
+    col_scales<<<dim3(2), dim3(256), 0, st>>>(reinterpret_cast<int*>(sw1), 320, 0, h->cs1);
+    if ((rc = check_launch("conv1 planes"))) return rc;
   }
   if ((rc = f16_calibrate(h, st))) return rc;
   h->f16_ready = true;
