@@ -1043,6 +1043,39 @@ __global__ __launch_bounds__(64 * NW, 1) void beluga_fc_h3(GemmArgs p) {
 // planes (32 pieces, per-lane 64-bit sources: a_rows gathers windows from anywhere in the
 // activation buffer) + B 160 columns x 2 planes (20 pieces); 3 stages = 156 KB.  Same operands,
 // products and k order per output as beluga_fc_h3: bitwise equal.
+constexpr int H3E_ROW = 656;
+constexpr int H3E_WAVE = 32 * H3E_ROW;                 // 20,992 B per wave
+
+// Split-K partial epilogue through LDS: a wave's 64 x 160 fp32 tile is, per row, one contiguous
+// 640-B run of the partial slab (row stride ldc).  The accumulator layout scatters it over 4-B
+// pieces (16 lanes = 64 B per store); staged per 32-row half in the wave's LDS area (row stride
+// H3E_ROW = 656 B: the 4 row groups of a ds_write_b32 land on distinct banks), it leaves as
+// 16-B stores, 40 per row.  Same values and addresses as gemm_epilogue16<EPI_PARTIAL>.
+__device__ __forceinline__ void epilogue_partial_lds(const GemmArgs& p, const floatx4v (&acc)[4][10], long long mw,
+                                                     int n0, int ks, int lane, char* lds) {
+  const int fr = lane & 15, fq = lane >> 4;
+  float* const cbase = p.C + (long long)ks * p.split_stride;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+#pragma unroll
+    for (int nb = 0; nb < 10; ++nb)
+#pragma unroll
+      for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *(float*)(lds + (mh * 16 + 4 * fq + j) * H3E_ROW + (nb * 16 + fr) * 4) = acc[2 * half + mh][nb][j];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll 4
+    for (int i = 0; i < 20; ++i) {
+      const int k = i * 64 + lane, row = k / 40, ch = k - row * 40;
+      const long long m = mw + half * 32 + row;
+      if (m < p.M && n0 + 4 * ch < p.n_store)
+        *(floatx4v*)(cbase + m * p.ldc + n0 + 4 * ch) = *(const floatx4v*)(lds + row * H3E_ROW + ch * 16);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
 constexpr int FCP_APLANE = 256 * 64;                   // 16 KB
 constexpr int FCP_STAGE = 2 * FCP_APLANE + 2 * X6P_B_PLANE;   // 52 KB
 
@@ -1142,6 +1175,8 @@ __device__ __forceinline__ void gemm_fc_h3p_body(const GemmArgs& p, char* smem) 
       slot = slot + 1 == NS ? 0 : slot + 1;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (EPI == EPI_PARTIAL && (TM & 4096) == 0)
+      __builtin_amdgcn_s_barrier();   // tail pieces landed: the consumers' epilogue reuses the LDS
     return;
   }
 
@@ -1215,7 +1250,12 @@ __device__ __forceinline__ void gemm_fc_h3p_body(const GemmArgs& p, char* smem) 
     asm volatile("" ::: "memory");
     slot = nslot;
   }
-  gemm_epilogue16<EPI, 2, 10, 4>(p, acc, m0 + wave * 64, n0, ks, lane);
+  if constexpr (EPI == EPI_PARTIAL && (TM & 4096) == 0) {
+    __builtin_amdgcn_s_barrier();   // producers drained their tail pieces
+    epilogue_partial_lds(p, acc, m0 + wave * 64, n0, ks, lane, smem + wave * H3E_WAVE);
+  } else {   // TM 4096 (probe): round 1's scattered 4-byte partial stores
+    gemm_epilogue16<EPI, 2, 10, 4>(p, acc, m0 + wave * 64, n0, ks, lane);
+  }
 }
 
 template <int LAYER, int EPI, int TM = 0, int NS = 3>
@@ -1267,29 +1307,35 @@ constexpr int h3c_lds_mb() { return 2 * SlabGeo<MB>::ASLAB + NSB * H3C_BSTAGE; }
 // accumulator layout scatters it over 2-byte pieces.  Each half of the tile (32 rows) is split
 // into the wave's private LDS area (row stride 656 B: the 4 row groups of a ds_write_b16 land
 // on distinct banks), then written out as 16-B chunks (20 per lane), each row fully coalesced.
-constexpr int H3E_ROW = 656;
-constexpr int H3E_WAVE = 32 * H3E_ROW;                 // 20,992 B per wave
 
-template <int MB = 4>
+template <int MB = 4, bool OLDOVF = false>
 __device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const floatx4v (&acc)[MB][10], long long mw,
                                                      int n0, int lane, char* lds) {
   const int fr = lane & 15, fq = lane >> 4;
   const long long w0 = mw / p.s_in;
   const int t0 = (int)(mw - w0 * p.s_in);
+  // overflow: a running max per lane and ONE flag store at the end (a per-value conditional
+  // store compiled to a branch and exec-mask juggling around every value: ~4 instructions each)
+  float vmax = 0.f;
 #pragma unroll
   for (int half = 0; half < MB / 2; ++half) {
 #pragma unroll
     for (int nb = 0; nb < 10; ++nb) {
       const int n = n0 + nb * 16 + fr;
-      const float bn = n < p.n_store ? p.bias[n] : 0.f;
-      const float cs = n < p.n_store ? p.col_scale[n] : 0.f;
+      // fmaxf(acc*cs + b, 0) * osc with the power-of-2 scales folded: the same value
+      const float cso = n < p.n_store ? p.col_scale[n] * p.out_scale : 0.f;
+      const float bo = n < p.n_store ? p.bias[n] * p.out_scale : 0.f;
 #pragma unroll
       for (int mh = 0; mh < 2; ++mh) {
         const int mb = 2 * half + mh;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float x = fmaxf(acc[mb][nb][j] * cs + bn, 0.f) * p.out_scale;
-          if (!(fabsf(x) < 65504.f)) *p.ovf = 1;   // NaN/overflow: the call is recomputed
+          const float x = fmaxf(fmaf(acc[mb][nb][j], cso, bo), 0.f);
+          if constexpr (OLDOVF) {   // probe: round 1's per-value flag store
+            if (!(fabsf(x) < 65504.f)) *p.ovf = 1;
+          } else {
+            vmax = fmaxf(vmax, x);
+          }
           _Float16 hi, lo;
           split_h2(x, hi, lo);
           char* d = lds + (mh * 16 + 4 * fq + j) * H3E_ROW + (nb >> 1) * 128 + ((nb & 1) * 16 + fr) * 2;
@@ -1317,6 +1363,7 @@ __device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const fl
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
+  if (!(vmax < 65504.f)) *p.ovf = 1;   // overflow: the call is recomputed (bf16x6)
 }
 
 // LDS swizzle of the conv kernels' A slab and B stages: the 16-B chunk c of row r sits at
@@ -1339,21 +1386,26 @@ __device__ __forceinline__ int conv_swz(int r) {
 // The wave's 4*MB pooled rows x 160 columns are split into its private LDS area in the planes
 // layout, then stored as 16-B chunks (one contiguous 640-B run per pooled row) instead of two
 // 2-byte stores per value.  Same values as gemm_epilogue16<EPI_RELU_POOL4, 2>.
-template <int MB>
+template <int MB, bool OLDOVF = false>
 __device__ __forceinline__ void epilogue_pool_h2_lds(const GemmArgs& p, const floatx4v (&acc)[MB][10], long long mw,
                                                      int n0, int lane, char* lds) {
   static_assert(4 * MB <= 32, "pooled rows per wave exceed the LDS area");
   const int fr = lane & 15, fq = lane >> 4;
+  float vmax = 0.f;   // overflow: running max, one flag store at the end
 #pragma unroll
   for (int nb = 0; nb < 10; ++nb) {
     const int n = n0 + nb * 16 + fr;
-    const float bn = n < p.n_store ? p.bias[n] : 0.f;
-    const float cs = n < p.n_store ? p.col_scale[n] : 0.f;
+    const float cso = n < p.n_store ? p.col_scale[n] * p.out_scale : 0.f;
+    const float bo = n < p.n_store ? p.bias[n] * p.out_scale : 0.f;
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
       const float mx = fmaxf(fmaxf(acc[mb][nb][0], acc[mb][nb][1]), fmaxf(acc[mb][nb][2], acc[mb][nb][3]));
-      const float x = fmaxf(mx * cs + bn, 0.f) * p.out_scale;
-      if (!(fabsf(x) < 65504.f)) *p.ovf = 1;   // NaN/overflow: the call is recomputed
+      const float x = fmaxf(fmaf(mx, cso, bo), 0.f);
+      if constexpr (OLDOVF) {   // probe: round 1's per-value flag store
+        if (!(fabsf(x) < 65504.f)) *p.ovf = 1;
+      } else {
+        vmax = fmaxf(vmax, x);
+      }
       _Float16 hi, lo;
       split_h2(x, hi, lo);
       char* d = lds + (mb * 4 + fq) * H3E_ROW + (nb >> 1) * 128 + ((nb & 1) * 16 + fr) * 2;
@@ -1380,6 +1432,7 @@ __device__ __forceinline__ void epilogue_pool_h2_lds(const GemmArgs& p, const fl
       }
     }
   }
+  if (!(vmax < 65504.f)) *p.ovf = 1;   // overflow: the call is recomputed (bf16x6)
 }
 
 // NSB: depth of the B ring (3: loads of stage s+2 in flight during stage s; 4: s+3).
@@ -2117,12 +2170,22 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
     }
     if (!PF && c + 1 < nchunk) read_a(aslab + ((c + 1) & 1) * G::ASLAB, 0, as);
   }
+  if constexpr ((TM & 2048) != 0) {   // timing probe (wrong results): no epilogue, one store per lane
+    __builtin_amdgcn_s_barrier();
+    float t = 0.f;
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 10; ++nb) t += acc[mb][nb][0] + acc[mb][nb][1] + acc[mb][nb][2] + acc[mb][nb][3];
+    p.C[(m0 + wave * 64 + lane) % p.M] = t;
+    return;
+  }
   if constexpr (EPI == EPI_RELU || EPI == EPI_RELU_POOL4) {
     __builtin_amdgcn_s_barrier();                     // producers drained their tail pieces
     if constexpr (EPI == EPI_RELU)
-      epilogue_relu_h2_lds<4>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
+      epilogue_relu_h2_lds<4, (TM & 4096) != 0>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
     else
-      epilogue_pool_h2_lds<4>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
+      epilogue_pool_h2_lds<4, (TM & 4096) != 0>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
   } else {
     gemm_epilogue16<EPI, 2, 10, 4>(p, acc, m0 + wave * 64, n0, 0, lane);
   }

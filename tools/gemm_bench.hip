@@ -135,7 +135,8 @@ int fc1_bench(int nb, int rounds, int splits) {
             {"fcp_m", fc1p_launch<0>}, {"fcp_m_pf", fc1p_launch<256>}, {"fcp_x", fc1p_launch<0>},
             {"fcp_x_pf", fc1p_launch<256>},
             {"fcp_x_noload", fc1p_launch<2>},
-            {"fcp_x_hotAB", fc1p_launch<8>}};
+            {"fcp_x_hotAB", fc1p_launch<8>},
+            {"fcp_m_old", fc1p_launch<4096>}, {"fcp_x_old", fc1p_launch<4096>}};
   constexpr int NV = sizeof(vs) / sizeof(vs[0]);
   const size_t csz = (size_t)splits * nb * ldc;
   std::vector<float> ref(csz), out(csz);
@@ -246,6 +247,8 @@ int main(int argc, char** argv) {
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 256, 4>("h3p4_pf"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 256 | 512, 4>("h3p4_pf_oldswz"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 0, 4>("h3p4"));
+    vs.push_back(mkp3<2, EPI_RELU_POOL4, 256 | 2048, 4>("h3p4_pf_noepi"));
+    vs.push_back(mkp3<2, EPI_RELU_POOL4, 256 | 4096, 4>("h3p4_pf_oldovf"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 2>("h3p_noglds"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 8>("h3p_hotAB"));
     vs.push_back(mks3<2, EPI_RELU_POOL4, 6, 0>("h3s6"));
@@ -264,6 +267,8 @@ int main(int argc, char** argv) {
     vs.push_back(mkp3<3, EPI_RELU, 256, 4>("h3p4_pf"));
     vs.push_back(mkp3<3, EPI_RELU, 256 | 512, 4>("h3p4_pf_oldswz"));
     vs.push_back(mkp3<3, EPI_RELU, 0, 4>("h3p4"));
+    vs.push_back(mkp3<3, EPI_RELU, 256 | 2048, 4>("h3p4_pf_noepi"));
+    vs.push_back(mkp3<3, EPI_RELU, 256 | 4096, 4>("h3p4_pf_oldovf"));
     vs.push_back(mks3<3, EPI_RELU, 6, 0>("h3s6"));
   }
   auto args_for = [&](int bm, float* C) {
@@ -283,7 +288,8 @@ int main(int argc, char** argv) {
   if (only) {
     std::vector<Variant> keep;
     for (auto& v : vs)
-      if (v.name == only || v.name == vs[0].name) keep.push_back(v);
+      if ((std::string(",") + only + ",").find("," + v.name + ",") != std::string::npos || v.name == vs[0].name)
+        keep.push_back(v);   // VARIANT: comma-separated names
     vs = keep;
     times.assign(vs.size(), {});
   }
@@ -332,7 +338,7 @@ int main(int argc, char** argv) {
         }
         if (vs[v].name == "h3c") ref_h3 = out;
         if (vs[v].name.rfind("h3", 0) == 0 && vs[v].name != "h3c" && !ref_h3.empty() &&
-            vs[v].name.find("noglds") == std::string::npos) {
+            vs[v].name.find("noglds") == std::string::npos && vs[v].name.find("noepi") == std::string::npos) {
           size_t bad = 0;
           for (size_t i = 0; i < csz; ++i) bad += memcmp(&ref_h3[i], &out[i], 4) != 0;
           printf("variant %s vs h3c: %zu elements differ bitwise\n", vs[v].name.c_str(), bad);
