@@ -215,7 +215,7 @@ __global__ __launch_bounds__(320) void beluga_conv1_h3(const float* __restrict__
           const float v = fmaxf(fmaf(acc[rb][cb][j], sc[cb], bb[cb]), 0.f);
           vmax = fmaxf(vmax, v);
           _Float16 h, l;
-          split_h2(v, h, l);
+          split_h2p(v, h, l);
           char* d = sw + (16 * rb + 4 * fq + j) * C1H_WROW + (cb >> 1) * 128 + ((cb & 1) * 16 + fr) * 2;
           *reinterpret_cast<_Float16*>(d) = h;
           *reinterpret_cast<_Float16*>(d + 64) = l;
@@ -276,7 +276,7 @@ __global__ void fc1_reduce_h2(const float* __restrict__ part, int splits, long l
     const float x = v * osc;
     bad |= !(fabsf(x) < 65504.f);
     _Float16 hh, ll;
-    split_h2(x, hh, ll);
+    split_h2p(x, hh, ll);   // FC2 reads the planes as stored (no re-split): the plain split
     hv[e] = hh;
     lv[e] = ll;
   }

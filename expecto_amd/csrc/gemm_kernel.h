@@ -108,6 +108,17 @@ __device__ __forceinline__ void split_h2(const float x, _Float16& hi, _Float16& 
   lo = (_Float16)(r - (float)hi);
 }
 
+// Plain 2-way split, hi = RNE16(x), lo = RNE16(x - hi): the same recovered value hi + lo as
+// split_h2 (x rounded to >= 22 bits) at 2 conversions fewer.  Used wherever the planes are
+// consumed as stored; values that are recovered and re-split (the unpooled conv4 rows of the
+// segment path, pooled by pool4_phases / seg_delta_pool) must meet the values the other paths
+// store as the CANONICAL pair of that recovered value: conv4's pooled epilogue and the pool
+// kernels keep split_h2 (tools/gemm_bench: conv3 / conv5 / conv6 +3-4 % from the plain split).
+__device__ __forceinline__ void split_h2p(const float x, _Float16& hi, _Float16& lo) {
+  hi = (_Float16)x;
+  lo = (_Float16)(x - (float)hi);
+}
+
 template <int FMT>
 __device__ __forceinline__ void store_act(float* C, long long row, long long ld, int n, float v, float osc = 1.f,
                                           int* ovf = nullptr) {
@@ -1308,7 +1319,13 @@ constexpr int h3c_lds_mb() { return 2 * SlabGeo<MB>::ASLAB + NSB * H3C_BSTAGE; }
 // into the wave's private LDS area (row stride 656 B: the 4 row groups of a ds_write_b16 land
 // on distinct banks), then written out as 16-B chunks (20 per lane), each row fully coalesced.
 
-template <int MB = 4, bool OLDOVF = false>
+// PROBE (timing probes, gemm_bench only): 1 = round 1's per-value overflow store, 2 = no global
+// stores, 4 = no split (hi = the fp16 rounding, lo = 0: wrong results), 8 = streamed
+// (nontemporal) stores, 16 = canonical split.  tools/gemm_bench 2000 windows: streamed stores
+// +1.6-3.4 %, plain split +2.8-4.1 % on conv3 / conv5 / conv6 -- but neither moved the layer times
+// of the 200-window pipeline in a same-box A/B (tools/ab_bench.sh); the streamed stores cost conv1
+// 6 %, so stores stay cached.
+template <int MB = 4, int PROBE = 0>
 __device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const floatx4v (&acc)[MB][10], long long mw,
                                                      int n0, int lane, char* lds) {
   const int fr = lane & 15, fq = lane >> 4;
@@ -1331,13 +1348,20 @@ __device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const fl
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float x = fmaxf(fmaf(acc[mb][nb][j], cso, bo), 0.f);
-          if constexpr (OLDOVF) {   // probe: round 1's per-value flag store
+          if constexpr ((PROBE & 1) != 0) {   // probe: round 1's per-value flag store
             if (!(fabsf(x) < 65504.f)) *p.ovf = 1;
           } else {
             vmax = fmaxf(vmax, x);
           }
           _Float16 hi, lo;
-          split_h2(x, hi, lo);
+          if constexpr ((PROBE & 4) != 0) {
+            hi = (_Float16)x;
+            lo = (_Float16)0.f;
+          } else if constexpr ((PROBE & 16) != 0) {
+            split_h2(x, hi, lo);                   // probe: round 1's canonical split
+          } else {
+            split_h2p(x, hi, lo);
+          }
           char* d = lds + (mh * 16 + 4 * fq + j) * H3E_ROW + (nb >> 1) * 128 + ((nb & 1) * 16 + fr) * 2;
           *(_Float16*)d = hi;
           *(_Float16*)(d + 64) = lo;
@@ -1354,10 +1378,14 @@ __device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const fl
         long long w;
         int tpos;
         row_wt(w0, t0, half * 32 + row, p.s_in, w, tpos);
-        if (tpos < p.t_valid && n0 + (ch >> 3) * 32 < p.n_store) {
+        if (tpos < p.t_valid && n0 + (ch >> 3) * 32 < p.n_store && (PROBE & 2) == 0) {
           const long long orow = w * p.s_out + tpos;
           char* g = (char*)p.C + (orow * ldb + (n0 >> 5)) * 128 + ch * 16;
-          *(floatx4v*)g = *(const floatx4v*)(lds + row * H3E_ROW + ch * 16);
+          const floatx4v v = *(const floatx4v*)(lds + row * H3E_ROW + ch * 16);
+          if constexpr ((PROBE & 8) != 0)
+            __builtin_nontemporal_store(v, (floatx4v*)g);   // probe: streamed store
+          else
+            *(floatx4v*)g = v;
         }
       }
     }
@@ -1386,7 +1414,7 @@ __device__ __forceinline__ int conv_swz(int r) {
 // The wave's 4*MB pooled rows x 160 columns are split into its private LDS area in the planes
 // layout, then stored as 16-B chunks (one contiguous 640-B run per pooled row) instead of two
 // 2-byte stores per value.  Same values as gemm_epilogue16<EPI_RELU_POOL4, 2>.
-template <int MB, bool OLDOVF = false>
+template <int MB, bool OLDOVF = false, bool CANON = false>
 __device__ __forceinline__ void epilogue_pool_h2_lds(const GemmArgs& p, const floatx4v (&acc)[MB][10], long long mw,
                                                      int n0, int lane, char* lds) {
   static_assert(4 * MB <= 32, "pooled rows per wave exceed the LDS area");
@@ -1407,7 +1435,10 @@ __device__ __forceinline__ void epilogue_pool_h2_lds(const GemmArgs& p, const fl
         vmax = fmaxf(vmax, x);
       }
       _Float16 hi, lo;
-      split_h2(x, hi, lo);
+      if constexpr (CANON)
+        split_h2(x, hi, lo);
+      else
+        split_h2p(x, hi, lo);
       char* d = lds + (mb * 4 + fq) * H3E_ROW + (nb >> 1) * 128 + ((nb & 1) * 16 + fr) * 2;
       *(_Float16*)d = hi;
       *(_Float16*)(d + 64) = lo;
@@ -1633,7 +1664,7 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
     if constexpr (EPI == EPI_RELU)
       epilogue_relu_h2_lds<MB>(p, acc, m0 + wave * 16 * MB, n0, lane, smem + wave * H3E_WAVE);
     else
-      epilogue_pool_h2_lds<MB>(p, acc, m0 + wave * 16 * MB, n0, lane, smem + wave * H3E_WAVE);
+      epilogue_pool_h2_lds<MB, false, LAYER == 4>(p, acc, m0 + wave * 16 * MB, n0, lane, smem + wave * H3E_WAVE);
   } else {
     gemm_epilogue16<EPI, 2, 10, MB>(p, acc, m0 + wave * 16 * MB, n0, 0, lane);
   }
@@ -2183,9 +2214,11 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
   if constexpr (EPI == EPI_RELU || EPI == EPI_RELU_POOL4) {
     __builtin_amdgcn_s_barrier();                     // producers drained their tail pieces
     if constexpr (EPI == EPI_RELU)
-      epilogue_relu_h2_lds<4, (TM & 4096) != 0>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
+      epilogue_relu_h2_lds<4, ((TM & 4096) ? 1 : 0) | ((TM & 8192) ? 2 : 0) | ((TM & 16384) ? 4 : 0) |
+                                  ((TM & 32768) ? 8 : 0) | ((TM & 65536) ? 16 : 0)>(
+          p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
     else
-      epilogue_pool_h2_lds<4, (TM & 4096) != 0>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
+      epilogue_pool_h2_lds<4, (TM & 4096) != 0, LAYER == 4>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
   } else {
     gemm_epilogue16<EPI, 2, 10, 4>(p, acc, m0 + wave * 64, n0, 0, lane);
   }

@@ -269,6 +269,11 @@ int main(int argc, char** argv) {
     vs.push_back(mkp3<3, EPI_RELU, 0, 4>("h3p4"));
     vs.push_back(mkp3<3, EPI_RELU, 256 | 2048, 4>("h3p4_pf_noepi"));
     vs.push_back(mkp3<3, EPI_RELU, 256 | 4096, 4>("h3p4_pf_oldovf"));
+    vs.push_back(mkp3<3, EPI_RELU, 256 | 8192, 4>("h3p4_pf_nostore"));
+    vs.push_back(mkp3<3, EPI_RELU, 256 | 16384, 4>("h3p4_pf_nosplit"));
+    vs.push_back(mkp3<3, EPI_RELU, 256 | 8192 | 16384, 4>("h3p4_pf_nostore_nosplit"));
+    vs.push_back(mkp3<3, EPI_RELU, 256 | 32768, 4>("h3p4_pf_ntstore"));
+    vs.push_back(mkp3<3, EPI_RELU, 256 | 65536, 4>("h3p4_pf_canon"));
     vs.push_back(mks3<3, EPI_RELU, 6, 0>("h3s6"));
   }
   auto args_for = [&](int bm, float* C) {
@@ -338,7 +343,8 @@ int main(int argc, char** argv) {
         }
         if (vs[v].name == "h3c") ref_h3 = out;
         if (vs[v].name.rfind("h3", 0) == 0 && vs[v].name != "h3c" && !ref_h3.empty() &&
-            vs[v].name.find("noglds") == std::string::npos && vs[v].name.find("noepi") == std::string::npos) {
+            vs[v].name.find("noglds") == std::string::npos && vs[v].name.find("noepi") == std::string::npos &&
+            vs[v].name.find("nosplit") == std::string::npos && vs[v].name.find("nostore") == std::string::npos) {
           size_t bad = 0;
           for (size_t i = 0; i < csz; ++i) bad += memcmp(&ref_h3[i], &out[i], 4) != 0;
           printf("variant %s vs h3c: %zu elements differ bitwise\n", vs[v].name.c_str(), bad);
