@@ -495,9 +495,9 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-# Handle workspace (windows per launch chunk): 8192 lets the segment path put ~40 variants'
-# 200-window segments in one chunk (tools/seg200_sweep.py: 4000 -> 8192 windows and 24 -> 96
-# variants per step take the 200-window workload from 799 to 881 variants/s).
+# Handle workspace (windows per per-window chunk and per FC slice of the segment path; round 1:
+# 4000 -> 8192 windows and 24 -> 96 variants per step took the 200-window workload from 799 to
+# 881 variants/s).  Round 2: the 96 variants' segments of a strand run as one chunk.
 MAX_BATCH = 8192
 
 if __name__ == "__main__":
