@@ -306,6 +306,34 @@ def pmc_traffic(key, kernel):
     return None, None
 
 
+def pmc_held_clock(key, kernel):
+    """MFMA-busy fraction and held clock of ``kernel`` from the same committed profile as
+    pmc_traffic (profiles/<tag>/pmc_sq.csv + kernel_stats.csv of this bench command):
+    busy = SQ_VALU_MFMA_BUSY_CYCLES / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8 XCDs), clock =
+    GRBM_GUI_ACTIVE / 8 / average duration.  The nominal peak assumes 2.4 GHz; under this load
+    the chip holds a lower clock (MI355X_MICROARCH.md "DVFS give-back"), so frac's ceiling is
+    clock / 2.4 GHz."""
+    import csv
+    import glob
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "traffic.json")), reverse=True):
+        d = os.path.dirname(path)
+        try:
+            if json.load(open(path)).get("profile_key") != key:
+                continue
+            sq = [r for r in csv.DictReader(open(os.path.join(d, "pmc_sq.csv"))) if kernel in r["kernel"]]
+            st = [r for r in csv.DictReader(open(os.path.join(d, "kernel_stats.csv"))) if kernel in r["Name"]]
+        except (OSError, ValueError, KeyError):
+            continue
+        if not sq or not st:
+            continue
+        g = float(sq[0]["GRBM_GUI_ACTIVE"]) / 8
+        busy = float(sq[0]["SQ_VALU_MFMA_BUSY_CYCLES"]) / 1024 / g
+        clock = g / (float(st[0]["AverageNs"]) * 1e-9) / 1e9
+        return {"mfma_busy": busy, "held_clock_ghz": clock, "frac_ceiling_at_held_clock": clock / 2.4,
+                "source": os.path.relpath(os.path.join(d, "pmc_sq.csv"), REPO)}
+    return None
+
+
 def layer_summary(layers, el_steps):
     return ({k: ms / el_steps for k, (ms, c, m) in layers.items()},
             {k: 2.0 * m / (ms * 1e-3) / 1e12 for k, (ms, c, m) in layers.items() if ms > 0})
@@ -428,6 +456,9 @@ def main():
     if roof["traffic"] is not None:
         roof["traffic_unit"] = "bytes/launch (HBM read+write)"
         roof["traffic_source"] = src
+    held = pmc_held_clock(key, roof["kernel"])
+    if held is not None:
+        roof["pmc"] = held
     rec = {
         "metric": METRIC, "value": m["units_per_s"], "unit": "variants/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": m["ms_per_step"], "higher_is_better": True, "scaling": "weak",
