@@ -85,6 +85,14 @@ def gather_segments(lib, dg, start: torch.Tensor, seg_len: int, splice_pos=None,
     return codes
 
 
+def to_device(a, device) -> torch.Tensor:
+    """Host array -> device tensor without a host sync: staged through pinned memory (torch's
+    caching host allocator keeps it alive until the copy ran), so preparing batch k+1 does not
+    wait for batch k's kernels (a pageable .to(device) synchronises the stream)."""
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 class VariantPipeline:
     """Holds the device genome + model engine; computes shift sweeps for variant batches.
 
@@ -129,8 +137,8 @@ class VariantPipeline:
         ac = np.array([_allele_code(vs.alt[v]) for v in snv_idx], np.uint8).reshape(-1)
         ns = snv_idx.size
         dev = self.device
-        prep = {"n": n, "S": S, "shifts": shifts, "rows": rows, "snv_idx": torch.from_numpy(snv_idx).to(dev),
-                "ind_idx": torch.from_numpy(ind_idx).to(dev), "n_snv": ns, "n_ind": ind_idx.size,
+        prep = {"n": n, "S": S, "shifts": shifts, "rows": rows, "snv_idx": to_device(snv_idx, dev),
+                "ind_idx": to_device(ind_idx, dev), "n_snv": ns, "n_ind": ind_idx.size,
                 "seg": None, "win": None, "ind_codes": None}
         lo_s, hi_s = min(shifts), max(shifts)
         if ns and S > 1 and self.use_segments and all((x - lo_s) % 4 == 0 for x in shifts):
@@ -141,10 +149,10 @@ class VariantPipeline:
                 v_i, j_i = np.meshgrid(np.arange(ns), np.arange(S), indexing="ij")
                 prep["seg"] = {
                     "L": L, "pairs": True,
-                    "start": torch.from_numpy(off[snv_idx] + lo_s - 999).to(dev),
+                    "start": to_device(off[snv_idx] + lo_s - 999, dev),
                     "splice_pos": torch.full((ns,), 999 - lo_s, dtype=torch.int32, device=dev),
-                    "splice_code": torch.from_numpy(rc).to(dev),
-                    "alt_code": torch.from_numpy(ac).to(dev),
+                    "splice_code": to_device(rc, dev),
+                    "alt_code": to_device(ac, dev),
                     "var_pos": np.full(ns, 999 - lo_s, np.int32),
                     "win_seg": v_i.ravel().astype(np.int32),
                     "win_off": (np.asarray(shifts)[j_i.ravel()] - lo_s).astype(np.int32),
@@ -155,18 +163,18 @@ class VariantPipeline:
                 a_i, v_i, j_i = np.meshgrid(np.arange(2), np.arange(ns), np.arange(S), indexing="ij")
                 prep["seg"] = {
                     "L": L, "pairs": False,
-                    "start": torch.from_numpy(np.concatenate([off[snv_idx], off[snv_idx]]) + lo_s - 999).to(dev),
+                    "start": to_device(np.concatenate([off[snv_idx], off[snv_idx]]) + lo_s - 999, dev),
                     "splice_pos": torch.full((2 * ns,), 999 - lo_s, dtype=torch.int32, device=dev),
-                    "splice_code": torch.from_numpy(np.concatenate([rc, ac])).to(dev),
+                    "splice_code": to_device(np.concatenate([rc, ac]), dev),
                     "win_seg": (a_i * ns + v_i).ravel().astype(np.int32),
                     "win_off": (np.asarray(shifts)[j_i.ravel()] - lo_s).astype(np.int32),
                     "win_row": (((a_i * S + j_i) * ns + v_i) if rows == "shift" else
                                 ((a_i * ns + v_i) * S + j_i)).ravel().astype(np.int32),
                 }
         elif ns:
-            prep["win"] = {"off": torch.from_numpy(off[snv_idx]).to(dev), "rc": torch.from_numpy(rc).to(dev),
-                           "ac": torch.from_numpy(ac).to(dev),
-                           "sh": torch.tensor(shifts, dtype=torch.int32, device=dev)}
+            prep["win"] = {"off": to_device(off[snv_idx], dev), "rc": to_device(rc, dev),
+                           "ac": to_device(ac, dev),
+                           "sh": to_device(np.asarray(shifts, np.int32), dev)}
         if rows == "variant" and (prep["seg"] is None or ind_idx.size):
             raise ValueError('rows="variant" needs SNVs on 4-aligned shifts (the segment path)')
         if ind_idx.size:
@@ -219,8 +227,8 @@ class VariantPipeline:
         d = np.nonzero(dev_ok)[0]
         if d.size:
             dev = self.device
-            tab = torch.from_numpy(table).to(dev)
-            cols = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in
+            tab = to_device(table, dev)
+            cols = [to_device(np.ascontiguousarray(x), dev) for x in
                     (s0[d], mut[d].astype(np.int32), lref[d].astype(np.int32), lalt[d].astype(np.int32),
                      crop[d].astype(np.int32), aoff[2 * K[d] + A[d]].astype(np.int32))]
             blk = torch.empty((d.size, 2000), dtype=torch.uint8, device=dev)
@@ -230,7 +238,7 @@ class VariantPipeline:
                 _lib.check(self.lib.expecto_indel_windows(
                     _lib.dptr(self.dg.codes), self.dg.codes.numel(), *(_lib.dptr(c[i0:i1]) for c in cols),
                     _lib.dptr(tab), i1 - i0, _lib.dptr(blk[i0:i1]), st), "indel_windows")
-            out[torch.from_numpy(d).to(dev)] = blk
+            out[to_device(d, dev)] = blk
         h = np.nonzero(~dev_ok)[0]
         if h.size:
             host = np.full((h.size, 2000), 4, np.uint8)
@@ -239,7 +247,7 @@ class VariantPipeline:
                 allele = vs.alt[x] if A[t] else vs.ref[x]
                 c = seq_codes(fetch_window(self.fasta, vs.chrom[x], int(vs.pos[x]), vs.ref[x], allele, int(sh[t])))
                 host[r, :c.size] = c
-            out[torch.from_numpy(h).to(self.device)] = torch.from_numpy(host).to(self.device)
+            out[to_device(h, self.device)] = to_device(host, self.device)
         return out.view(2, S, ni, 2000)
 
     def _snv_window_codes(self, prep: dict) -> torch.Tensor:
