@@ -5,6 +5,8 @@
   run on the same inputs (tests/golden/make_golden_example.py).
 * configs[1]: the bench workload itself (1k SNVs, shift 0: device window generation + the
   pair path + diff) with 32 sampled windows recomputed by the torch-CPU oracle.
+* configs[3]: one rank's shard (12,500 SNVs x 9 shifts): sampled windows vs the oracle, exact
+  diff, and the two halves of a 2-rank split equal to the whole bit for bit.
 * configs[4]: one rank's shard of the TSS tiling (2,560 genes x 200 windows x fwd/rc through
   the segment path + the exp-decay reduction) with sampled genes against the oracle forward
   and reduction (compute_expecto_features.py:88-128).
@@ -113,3 +115,40 @@ def test_configs4_tss_shard_sampled_against_oracle():
         # predictions it is within the parity bar carried through the weights
         np.testing.assert_array_equal(f_got, tss_reduce(y[0], y[1], w))
         assert_close(f_got, tss_reduce(want[:200], want[200:], w), what=f"gene {g} features")
+
+
+def test_configs3_rank_shard_12500_snvs_9_shifts():
+    """configs[3]'s per-rank shape (100k SNVs over 8 GPUs = 12,500 SNVs x 9 shifts, +-800):
+    sampled windows of every shift against the torch-CPU oracle, diff == alt - ref exactly, and
+    the shard computed as the two halves a 2-rank split would hold (dist.shard_range) equals the
+    whole bit for bit -- rank boundaries never change a row."""
+    from expecto_amd import beluga, dist as edist, synthetic
+    from expecto_amd.encode import seq_codes
+    from expecto_amd.genome import DeviceGenome, Fasta
+    from expecto_amd.pipeline import VariantPipeline, VariantSet, fetch_window, shift_order
+    genome = synthetic.genome_bytes(n_contigs=8, contig_len=2_000_000, seed=33)
+    fa = Fasta.from_dict(genome)
+    n = 12_500
+    snv = synthetic.snvs(genome, n, seed=3)
+    vs = VariantSet([s[0] for s in snv], np.array([s[1] for s in snv]), [s[2] for s in snv], [s[3] for s in snv])
+    shifts = shift_order(800)
+    m = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=8192)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    eng = m.cuda().engine()
+    pipe = VariantPipeline(eng, fa, DeviceGenome(fa))
+    y = pipe.predict(vs, shifts)                           # [2 strands, 2 alleles, 9, n, 2002]
+    assert y.shape == (2, 2, 9, n, 2002) and bool(torch.isfinite(y).all())
+    d = pipe.diff(y)
+    assert torch.equal(d, y[:, 1] - y[:, 0])
+    for r in range(2):
+        lo, hi = edist.shard_range(n, r, 2)
+        part = VariantSet(vs.chrom[lo:hi], vs.pos[lo:hi], vs.ref[lo:hi], vs.alt[lo:hi])
+        assert torch.equal(pipe.predict(part, shifts), y[:, :, :, lo:hi]), f"rank {r} half differs"
+    rng = np.random.default_rng(5)
+    pick = [(int(v), int(j)) for v, j in zip(rng.choice(n, 16, replace=False), rng.integers(0, 9, 16))]
+    codes = np.stack([seq_codes(fetch_window(fa, vs.chrom[v], int(vs.pos[v]), vs.ref[v], al, shifts[j]))
+                      for v, j in pick for al in (vs.ref[v], vs.alt[v])])         # 32 windows
+    want = _oracle_forward(sd, codes)
+    yc = y.cpu().numpy()
+    got = np.stack([yc[st, a, j, v] for st in (0, 1) for v, j in pick for a in (0, 1)])
+    assert_close(got, want, what="configs[3] rank shard sampled windows vs oracle")
