@@ -145,6 +145,9 @@ def compute_main(argv=None):
     p.add_argument('-o', dest="out_dir", type=str, default='temp_compute_expecto_features')
     p.add_argument('--no-liftover', action='store_true', dest='no_liftover',
                    help='treat every hg38 TSS as unmapped (the reference needs the liftover package)')
+    p.add_argument('--chain-file', default=None, dest='chain_file',
+                   help='UCSC hg38ToHg19 chain file for the TSS liftover (default: $EXPECTO_CHAIN_FILE, '
+                        'else the liftover package)')
     _common_args(p)
     args = p.parse_args(argv)
     if args.windowsize != 2000:
@@ -159,12 +162,11 @@ def compute_main(argv=None):
     if args.no_liftover:
         converter = None
     else:
+        from .liftover import get_lifter
         try:
-            from liftover import get_lifter
-        except ImportError as e:
-            raise RuntimeError("the hg38->hg19 TSS override needs the `liftover` package; "
-                               "pass --no-liftover to keep the annotated TSSs") from e
-        converter = get_lifter('hg38', 'hg19')
+            converter = get_lifter('hg38', 'hg19', args.chain_file)
+        except RuntimeError as e:
+            raise RuntimeError(f"{e}; or pass --no-liftover to keep the annotated TSSs") from e
     genes = []
     found = no_map = 0
     for i, line in enumerate(open(args.annoFile)):
