@@ -381,7 +381,7 @@ def tss_workload(eng, genome, dg, dev, genes=96, steps=2):
             "projected_20k_genes_s_1gpu": 20000 / gps, "projected_20k_genes_s_8gpu_weak": 20000 / gps / 8}
 
 
-def cli_streamed(genome, n=4096):
+def cli_streamed(genome, n=8192):
     """The chromatin CLI end to end (chromatin.py:243-286) on configs[2]'s +-800 sweep of n
     seeded SNVs: device forward + diff + D2H into pinned buffers + the .diff.h5 row writes of
     every shift, streamed in batches of n/4 (batch k+1 computes while batch k is written, the
@@ -412,7 +412,8 @@ def cli_streamed(genome, n=4096):
                 runs.append(dict(chromatin.LAST_RUN))
             st = min(runs, key=lambda r: r["loop_s"])
             out[name] = {"loop_s": st["loop_s"], "variants_per_s": st["variants"] / st["loop_s"],
-                         "batches": st["batches"]}
+                         "batches": st["batches"], "host_launch_s": st["launch_s"], "host_wait_s": st["wait_s"],
+                         "host_write_s": st["write_s"]}
         nv = chromatin.LAST_RUN["variants"]
         out["variants"] = nv
         out["h5_bytes_written"] = 9 * 3 * 2 * nv * 2002 * 4
