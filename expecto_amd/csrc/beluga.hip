@@ -865,6 +865,7 @@ struct expecto_beluga {
   int fc_splits = kFcSplitsDefault;   // FC1 split-K slabs: a divisor of 2120 K blocks, <= 32
   int fc2_splits = kFc2SplitsDefault; // FC2 split-K slabs: a divisor of 63 K blocks
   double fc1_m_order_mb = 128.0;      // FC1 dispatch: M tiles fastest while one split's A is <= this
+  int fc1_order = 0;                  // 2: slab-outermost, XCD-owned M tiles for large M (EXPECTO_FC1_ORDER)
   int conv_tile = 0;                  // f16x3 conv M tile: 0 = auto (conv_tile_rows), 256 or 384
   int seg_chunk_windows = 0;          // segment path: windows per chunk cap (0 = none; tuning knob)
   int cus = 0;                        // compute units of the device (workgroups per round)
@@ -1151,6 +1152,8 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     // A tile run together (tools/gemm_bench fc1: +8 % at 4,000 rows, +5 % at 19,200 rows)
     a.m_fastest = (double)m_tiles * gemm_bm() * (kFc1In / splits) * 4.0 <= h->fc1_m_order_mb * (1 << 20) ? 1 : 0;
     a.linear_order = a.m_fastest;   // N tiles fastest: XCD-aware remap (consecutive tiles share an XCD)
+    if (h->fc1_order == 2 && !a.m_fastest && m_tiles % 8 == 0 && planes_gemm() && g_precision == EXPECTO_PRECISION_F16X3)
+      a.m_fastest = 2;              // slab-outermost, XCD-owned M tiles (gemm_fc_h3p_body)
     a.C = h->part;
     a.ldc = kHidLd;
     a.n_store = kHidLd;
@@ -1868,6 +1871,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
     h->fc2_splits = v;
   }
   if (const char* e = getenv("EXPECTO_FC1_M_ORDER_MB")) h->fc1_m_order_mb = atof(e);   // same bits either way
+  if (const char* e = getenv("EXPECTO_FC1_ORDER")) h->fc1_order = atoi(e);              // same bits either way
   if (const char* e = getenv("EXPECTO_OVERLAP")) h->overlap = atoi(e) != 0;   // same bits either way
   if (const char* e = getenv("EXPECTO_SEG_CHUNK_WINDOWS")) h->seg_chunk_windows = atoi(e);   // same bits either way
   if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)

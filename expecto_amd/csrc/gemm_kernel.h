@@ -1104,7 +1104,17 @@ __device__ __forceinline__ void gemm_fc_h3p_body(const GemmArgs& p, char* smem) 
       p.linear_order ? bid : (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
   long long mt;
   int nt, ks;
-  if (p.m_fastest) {
+  if (p.m_fastest == 2) {
+    // split-K slab outermost over the whole chip (all XCDs sweep one weight slab together, so it
+    // is read from HBM once and shared through the Infinity Cache), and within a slab XCD x owns
+    // the M tiles mt = x mod 8, running each one's N tiles back to back (its A rows stay in the
+    // XCD's L2).  Needs m_tiles % 8 == 0 (the host checks).
+    const long long per_ks = p.m_tiles * p.n_tiles;
+    ks = (int)(bid / per_ks);
+    const unsigned j = (unsigned)((bid - ks * per_ks) >> 3);
+    mt = (long long)(j / (unsigned)p.n_tiles) * 8 + (bid & 7u);
+    nt = (int)(j % (unsigned)p.n_tiles);
+  } else if (p.m_fastest) {
     mt = lin % p.m_tiles;
     const long long rest = lin / p.m_tiles;
     nt = (int)(rest % p.n_tiles);
