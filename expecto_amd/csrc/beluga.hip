@@ -864,7 +864,7 @@ struct expecto_beluga {
   int precision = EXPECTO_PRECISION_BF16X6;
   int fc_splits = kFcSplitsDefault;   // FC1 split-K slabs: a divisor of 2120 K blocks, <= 32
   int fc2_splits = kFc2SplitsDefault; // FC2 split-K slabs: a divisor of 63 K blocks
-  double fc1_m_order_mb = 128.0;      // FC1 dispatch: M tiles fastest while one split's A is <= this
+  double fc1_m_order_mb = 80.0;       // FC1 dispatch: M tiles fastest while one split's A is <= this
   int fc1_order = 0;                  // 2: slab-outermost, XCD-owned M tiles for large M (EXPECTO_FC1_ORDER)
   int conv_tile = 0;                  // f16x3 conv M tile: 0 = auto (conv_tile_rows), 256 or 384
   int seg_chunk_windows = 0;          // segment path: windows per chunk cap (0 = none; tuning knob)
@@ -1146,10 +1146,12 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     a.taps = 1;
     a.n_tiles = n_tiles1;
     a.m_tiles = m_tiles;
-    // dispatch order: M tiles fastest while one split-K slab of A (all rows) stays within the
-    // Infinity Cache, so every XCD sweeps the same K slab (B slab read once); for larger M
-    // (segment sweeps: 19,200 rows = 260 MB per slab) N tiles fastest, so the 13 N tiles of an
-    // A tile run together (tools/gemm_bench fc1: +8 % at 4,000 rows, +5 % at 19,200 rows)
+    // dispatch order: M tiles fastest while one split-K slab of A (all rows) is small (<= 80 MB:
+    // 2,000-row configs[1] calls, 69 MB), so every XCD sweeps the same K slab (B slab read once);
+    // for larger M N tiles fastest, so the 13 N tiles of an A tile run together (tools/gemm_bench
+    // fc1: +8 % at 4,000 rows, +5 % at 19,200 rows; round 2: the 2,816-row last FC slice of the
+    // 200-window workload, 95 MB per slab, read 6.6 TB/s of L2 misses in M order, and 80 instead
+    // of 128 MB gained 0.6-0.7 % on that workload in two interleaved sweeps)
     a.m_fastest = (double)m_tiles * gemm_bm() * (kFc1In / splits) * 4.0 <= h->fc1_m_order_mb * (1 << 20) ? 1 : 0;
     a.linear_order = a.m_fastest;   // N tiles fastest: XCD-aware remap (consecutive tiles share an XCD)
     if (h->fc1_order == 2 && !a.m_fastest && m_tiles % 8 == 0 && planes_gemm() && g_precision == EXPECTO_PRECISION_F16X3)
