@@ -997,11 +997,6 @@ thread_local int g_precision = EXPECTO_PRECISION_BF16X6;
 
 // activation storage format (gemm_kernel.h): 1 bf16 planes (bf16x6), 2 scaled fp16 planes
 // (f16x3), 0 fp32 rows; bytes per element 6 / 4 / 4
-// FC last N tile launched apart without its 4 padding column blocks (EXPECTO_FC_NARROW=1; same
-// bits): off by default -- the second, one-round launch costs more than the 3 % of FC1's MFMAs
-// it saves (200-window workload 984 vs 993, configs[1] 30.4 k vs 30.9 k, interleaved sweep)
-bool g_fc_narrow = false;
-
 int act_fmt() {
   return g_precision == EXPECTO_PRECISION_BF16X6 ? 1 : g_precision == EXPECTO_PRECISION_F16X3 ? 2 : 0;
 }
@@ -1059,22 +1054,6 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
         beluga_conv_h3r<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
       else   // 4-deep B ring, next-stage fragments read before the stage barrier (TM 256)
         beluga_conv_h3p<LAYER, EPI, 256, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
-    } else if (g_fc_narrow && a.n_tiles * GBN > a.n_store && a.n_store - (a.n_tiles - 1) * GBN <= 96 &&
-               (EPI == EPI_PARTIAL || EPI == EPI_SIGMOID)) {
-      // FC layers, last N tile apart: its stored columns fit 6 of the 10 column blocks
-      // (2016 / 2002 = 12 x 160 + 96 / + 82), so it runs without the MFMAs of the 4 padding
-      // blocks (FC1: 3 % of its MFMAs).  Same products per stored column: same bits.
-      const long long nt = a.n_tiles - 1, n0 = nt * GBN;
-      GemmArgs main = a, last = a;
-      main.n_tiles = nt;
-      last.n_tiles = 1;
-      last.Bp = static_cast<const char*>(a.Bp) + n0 * a.ldb * 4;   // planes [n][K/32][2][32]: 4 B per (n, k)
-      last.C = a.C + n0;
-      last.n_store = (int)(a.n_store - n0);
-      if (a.bias) last.bias = a.bias + n0;
-      if (a.col_scale) last.col_scale = a.col_scale + n0;
-      beluga_fc_h3p<LAYER, EPI><<<dim3((unsigned)(main.m_tiles * nt * splits)), dim3(512), 0, st>>>(main);
-      beluga_fc_h3p<LAYER, EPI, 0, 3, 6><<<dim3((unsigned)(last.m_tiles * splits)), dim3(512), 0, st>>>(last);
     } else {   // FC layers: producer / consumer waves, both operands through an LDS ring (same bits)
       beluga_fc_h3p<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
     }
@@ -1895,7 +1874,6 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   }
   if (const char* e = getenv("EXPECTO_FC1_M_ORDER_MB")) h->fc1_m_order_mb = atof(e);   // same bits either way
   if (const char* e = getenv("EXPECTO_FC1_ORDER")) h->fc1_order = atoi(e);              // same bits either way
-  if (const char* e = getenv("EXPECTO_FC_NARROW")) g_fc_narrow = atoi(e) != 0;         // same bits either way
   if (const char* e = getenv("EXPECTO_OVERLAP")) h->overlap = atoi(e) != 0;   // same bits either way
   if (const char* e = getenv("EXPECTO_SEG_CHUNK_WINDOWS")) h->seg_chunk_windows = atoi(e);   // same bits either way
   if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)

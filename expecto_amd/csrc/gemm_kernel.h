@@ -1090,10 +1090,7 @@ __device__ __forceinline__ void epilogue_partial_lds(const GemmArgs& p, const fl
 constexpr int FCP_APLANE = 256 * 64;                   // 16 KB
 constexpr int FCP_STAGE = 2 * FCP_APLANE + 2 * X6P_B_PLANE;   // 52 KB
 
-// NBV: column blocks of 16 the MFMA waves compute (10 = the full 160-column tile; 6 = the last N
-// tile of FC1 / FC2, whose 96 stored columns (2016, 2002) are launched apart: its 4 padding
-// blocks cost 3 % of FC1's MFMAs otherwise).  The producers stage the full B tile either way.
-template <int LAYER, int EPI, int TM, int NS, int NBV = 10>
+template <int LAYER, int EPI, int TM, int NS>
 __device__ __forceinline__ void gemm_fc_h3p_body(const GemmArgs& p, char* smem) {
   static_assert(NS == 3 || NS == 4, "ring depth");
   // PF: producers wait for ALL their pieces at each stage end (stage s+NS-1 landed at barrier s),
@@ -1258,8 +1255,8 @@ __device__ __forceinline__ void gemm_fc_h3p_body(const GemmArgs& p, char* smem) 
       read_a(base, as);
     }
 #pragma unroll
-    for (int nb = 0; nb < NBV; ++nb) {
-      if (nb + 1 < NBV) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
+    for (int nb = 0; nb < 10; ++nb) {
+      if (nb + 1 < 10) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb) acc[mb][nb] = planes_mfma<2>(acc[mb][nb], as[mb], (nb & 1) ? b1 : b0);
       pin();
@@ -1282,10 +1279,10 @@ __device__ __forceinline__ void gemm_fc_h3p_body(const GemmArgs& p, char* smem) 
   }
 }
 
-template <int LAYER, int EPI, int TM = 0, int NS = 3, int NBV = 10>
+template <int LAYER, int EPI, int TM = 0, int NS = 3>
 __global__ __launch_bounds__(512, 1) void beluga_fc_h3p(GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[NS * FCP_STAGE];
-  gemm_fc_h3p_body<LAYER, EPI, TM, NS, NBV>(p, smem);
+  gemm_fc_h3p_body<LAYER, EPI, TM, NS>(p, smem);
 }
 
 // ---- f16x3 conv GEMM with the Toeplitz A tile staged once per channel chunk -------------
