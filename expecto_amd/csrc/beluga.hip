@@ -838,9 +838,10 @@ struct expecto_beluga {
   float* Q = nullptr;
   float* part = nullptr;
   float* part2 = nullptr;        // FC2 split-K partials (fc2_splits slabs; FC1's stay in `part`)
-  float* h1 = nullptr;
+  float* h1 = nullptr;          // FC1 output rows: fc2_rows (+ max_batch alt rows) of the segment path
   long long* a_rows = nullptr;  // FC1 row table (segment path), max_batch entries
-  long long* c_rows = nullptr;  // FC2 output-row table (segment path), max_batch entries
+  long long* c_rows = nullptr;  // FC2 output-row table (segment path), fc2_rows + max_batch entries
+  int fc2_rows = 0;             // segment path, FC2 unsplit: h1 rows gathered per FC2 launch
   int* win_seg_d = nullptr;     // window tables of the current segment call
   int* alt_w_d = nullptr;       //   segment pairs: windows holding the SNV / the others
   int* copy_w_d = nullptr;
@@ -1125,9 +1126,12 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
 // part_rows: row count of the split-K partial slabs (default nb): an alt FC1 that recomputes
 // only some slabs of the first nb rows of an earlier ref FC1 over part_rows rows reuses its
 // partials for the others.
-int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb, float* y, hipStream_t st,
-           const long long* c_rows = nullptr, const unsigned* ks_mask = nullptr, double slab_frac = 1.0,
-           long long part_rows = 0) {
+// h1 rows (FC1 output, FC2 input) start `rows` rows into the h1 buffer
+float* h1_rows(expecto_beluga* h, long long rows) { return h->h1 + rows * kHidLd * act_bytes() / 4; }
+
+// FC1 (split-K slabs into `part`) + fc1_reduce (bias, ReLU, activation planes) into h1.
+int run_fc1(expecto_beluga* h, const float* act, const long long* a_rows, int nb, float* h1, hipStream_t st,
+            const unsigned* ks_mask = nullptr, double slab_frac = 1.0, long long part_rows = 0) {
   if (part_rows <= 0) part_rows = nb;
   int rc;
   const long long m_tiles = (nb + gemm_bm() - 1) / gemm_bm();
@@ -1172,15 +1176,22 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     const bool f16 = g_precision == EXPECTO_PRECISION_F16X3;
     if (act_fmt() == 2)
       fc1_reduce_h2<<<dim3((unsigned)((count / 4 + 255) / 256)), dim3(256), 0, st>>>(
-          h->part, splits, part_rows * kHidLd, count / 4, h->fc1b, h->h1, h->cs[5], exp2i(h->sx[6]), h->ovf);
+          h->part, splits, part_rows * kHidLd, count / 4, h->fc1b, h1, h->cs[5], exp2i(h->sx[6]), h->ovf);
     else
       fc1_reduce<<<dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st>>>(
-          h->part, splits, part_rows * kHidLd, count, h->fc1b, h->h1, act_fmt(), f16 ? h->cs[5] : nullptr, exp2i(h->sx[6]), h->ovf);
+          h->part, splits, part_rows * kHidLd, count, h->fc1b, h1, act_fmt(), f16 ? h->cs[5] : nullptr, exp2i(h->sx[6]), h->ovf);
     if ((rc = check_launch("fc1_reduce"))) return rc;
   }
+  return EXPECTO_OK;
+}
+
+// FC2 + sigmoid over nb h1 rows; output row m goes to y row c_rows[m] (or m).
+int run_fc2(expecto_beluga* h, const float* h1, int nb, float* y, hipStream_t st, const long long* c_rows) {
+  int rc;
+  const long long m_tiles = (nb + gemm_bm() - 1) / gemm_bm();
   {
     GemmArgs a{};
-    a.A = h->h1;
+    a.A = h1;
     a.lda = kHidLd;
     a.M = nb;
     a.B = h->fc2w;
@@ -1191,7 +1202,10 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     a.taps = 1;
     a.n_tiles = npad_of(kNFeat) / GBN;
     a.m_tiles = m_tiles;
-    a.m_fastest = 1;
+    // M tiles fastest while the A slab is small; N tiles fastest (XCD-aware remap: an XCD runs
+    // the 13 N tiles of its A tiles back to back) for the large unsplit launches of the segment
+    // path, whose h1 rows (up to fc2_rows x 8 KB) would otherwise be streamed once per N tile
+    a.m_fastest = (double)m_tiles * gemm_bm() * (kHidLd / h->fc2_splits) * 4.0 <= h->fc1_m_order_mb * (1 << 20) ? 1 : 0;
     a.C = h->part2;
     a.ldc = kHidLd;
     a.n_store = kNFeat;
@@ -1215,6 +1229,14 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
     if ((rc = check_launch("fc2_reduce"))) return rc;
   }
   return EXPECTO_OK;
+}
+
+int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb, float* y, hipStream_t st,
+           const long long* c_rows = nullptr, const unsigned* ks_mask = nullptr, double slab_frac = 1.0,
+           long long part_rows = 0) {
+  int rc;
+  if ((rc = run_fc1(h, act, a_rows, nb, h->h1, st, ks_mask, slab_frac, part_rows))) return rc;
+  return run_fc2(h, h->h1, nb, y, st, c_rows);
 }
 
 // Profiling: the executed MACs of an alt FC1 that runs only the masked split-K slabs of its
@@ -1544,15 +1566,31 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
           ic0 = (int)(std::lower_bound(copy_w.begin(), copy_w.end(), w0) - copy_w.begin());
           ic1 = (int)(std::lower_bound(copy_w.begin(), copy_w.end(), w0 + nw) - copy_w.begin());
         }
-        // FC slices of <= max_batch rows (the FC workspace); the alt FC of a slice's alt rows
-        // reuses that slice's ref partials, so it runs right after the slice's ref FC
+        // FC1 slices of <= max_batch rows (the FC1 workspace); the alt FC of a slice's alt rows
+        // reuses that slice's ref partials, so it runs right after the slice's ref FC1.  FC2
+        // unsplit: the slices' h1 rows (and FC2 output rows) gather into one FC2 launch of up to
+        // fc2_rows rows (split FC2: per slice)
+        const bool gather2 = h->fc2_splits == 1;
+        int pend = 0;   // gathered h1 rows awaiting FC2
+        auto flush2 = [&]() -> int {
+          const int n2 = pend;
+          pend = 0;
+          return n2 ? run_fc2(h, h->h1, n2, y, st, h->c_rows) : EXPECTO_OK;
+        };
         for (int f0 = 0; f0 < nw; f0 += h->max_batch) {
           const int fn = std::min(h->max_batch, nw - f0);
+          if (gather2 && pend + fn > h->fc2_rows && (rc = flush2())) return rc;
+          long long* crow = h->c_rows + (gather2 ? pend : 0);
           seg_a_rows<<<dim3((fn + 255) / 256), dim3(256), 0, st>>>(
               h->win_seg_d, h->win_off_d, win_row ? h->win_row_d : nullptr, widx ? widx + f0 : nullptr, w0 + f0,
-              fn, s0, is_rc ? 1 : 0, L, n_ph, phi, g.T6, row_base, h->a_rows, h->c_rows);
+              fn, s0, is_rc ? 1 : 0, L, n_ph, phi, g.T6, row_base, h->a_rows, crow);
           if ((rc = check_launch("seg_a_rows"))) return rc;
-          if ((rc = run_fc(h, h->P, h->a_rows, fn, y, st, h->c_rows))) return rc;
+          if (gather2) {
+            if ((rc = run_fc1(h, h->P, h->a_rows, fn, h1_rows(h, pend), st))) return rc;
+            pend += fn;
+          } else if ((rc = run_fc(h, h->P, h->a_rows, fn, y, st, h->c_rows))) {
+            return rc;
+          }
           const int na = std::min(n_alt - f0, fn);   // alt rows of this slice: [f0, f0 + na)
           if (na <= 0) continue;
           if (f0 == 0) {
@@ -1562,9 +1600,10 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
                                                                               640 * eb / 16, h->Q);
             if ((rc = check_launch("seg_alt_blocks"))) return rc;
           }
+          long long* acrow = gather2 ? h->c_rows + h->fc2_rows : h->c_rows;   // alt rows apart
           seg_a_rows<<<dim3((na + 255) / 256), dim3(256), 0, st>>>(
               h->win_seg_d, h->win_off_d, win_row ? h->win_row_d : nullptr, widx + f0, 0, na, s0, is_rc ? 1 : 0,
-              L, n_ph, phi, g.T6, row_base, h->a_rows, h->c_rows);
+              L, n_ph, phi, g.T6, row_base, h->a_rows, acrow);
           if ((rc = check_launch("seg_a_rows"))) return rc;
           const unsigned* mask = nullptr;
           double frac = 1.0;
@@ -1583,8 +1622,16 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
             }
           }
           DeltaScope ds(h);
-          if ((rc = run_fc(h, h->Q, h->a_rows, na, pr->y_alt, st, h->c_rows, mask, frac, fn))) return rc;
+          if (gather2) {
+            float* h1a = h1_rows(h, h->fc2_rows);
+            if ((rc = run_fc1(h, h->Q, h->a_rows, na, h1a, st, mask, frac, fn)) ||
+                (rc = run_fc2(h, h1a, na, pr->y_alt, st, acrow)))
+              return rc;
+          } else if ((rc = run_fc(h, h->Q, h->a_rows, na, pr->y_alt, st, h->c_rows, mask, frac, fn))) {
+            return rc;
+          }
         }
+        if ((rc = flush2())) return rc;   // the ref rows are read by copy_rows below
         if (pr) {
           if (ic1 > ic0) {
             copy_rows<<<dim3(ic1 - ic0), dim3(256), 0, st>>>(y, pr->y_alt, h->copy_w_d + ic0,
@@ -1881,14 +1928,21 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
     EXPECTO_REQUIRE(v == 0 || v == 256 || v == 384, "EXPECTO_CONV_TILE must be 0 (auto), 256 or 384");
     h->conv_tile = v;
   }
+  // segment path with FC2 unsplit: the FC1 slices' h1 rows of a chunk are gathered into one FC2
+  // launch of up to fc2_rows rows (a 2,016-deep GEMM fills whole rounds of the chip only at
+  // ~20 k rows; EXPECTO_FC2_ROWS, same bits for any value)
+  h->fc2_rows = h->fc2_splits == 1 ? 4 * max_batch : max_batch;
+  if (const char* e = getenv("EXPECTO_FC2_ROWS"))
+    if (h->fc2_splits == 1) h->fc2_rows = std::max(max_batch, atoi(e));
   const size_t partf = (size_t)h->fc_splits * max_batch * kHidLd;
+  const size_t h1_rows = (size_t)h->fc2_rows + (h->fc2_splits == 1 ? max_batch : 0);
   if ((rc = dalloc(h, &h->P, act_alloc(pf))) || (rc = dalloc(h, &h->Q, act_alloc(qf))) ||
-      (rc = dalloc(h, &h->part, partf)) || (rc = dalloc(h, &h->h1, act_alloc((size_t)max_batch * kHidLd))) ||
+      (rc = dalloc(h, &h->part, partf)) || (rc = dalloc(h, &h->h1, act_alloc(h1_rows * kHidLd))) ||
       (rc = dalloc(h, &h->part2, (size_t)h->fc2_splits * max_batch * kHidLd)))
     return fail(rc);
   {
     float* rows = nullptr;
-    if ((rc = dalloc(h, &rows, (size_t)max_batch * 4))) return fail(rc);
+    if ((rc = dalloc(h, &rows, (size_t)(max_batch + h1_rows) * 2))) return fail(rc);
     h->a_rows = reinterpret_cast<long long*>(rows);
     h->c_rows = h->a_rows + max_batch;
   }
