@@ -484,7 +484,8 @@ def cfg3_rank_shard(pipe, eng, genome, rank, world, dev):
     return {"snvs_per_rank": n, "shifts": sh9, "compute_s": el, "variants_per_s": world * n / el,
             "f16_fallback_steps": fb,
             "gather": {"ms": gms, "bytes_into_rank0": nbytes, "GB_per_s": nbytes / (gms * 1e-3) / 1e9,
-                       "what": "every rank's y + diff to rank 0, one shift at a time (RCCL gather)"}}
+                       "what": f"every rank's y + diff to rank 0, one shift at a time "
+                               f"({'RCCL' if torch.distributed.get_backend() == 'nccl' else 'gloo'} gather)"}}
 
 
 def main():
