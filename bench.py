@@ -140,7 +140,9 @@ def hbm_reductions(dev):
         [1000, 20020] fp64 (3.2 MB read + 160 KB written per gene);
       variant (predict.py:87-136): 20000 variants x 9 shifts x 2002 fp32 -> [20000, 20020] fp64
         (write-dominated: "fp64_fill_ceiling" times torch's zero_ of the same output, the
-        practical write rate on this box)."""
+        practical write rate on this box);
+      sed (geuvadis_sed_for_top_eqtls.py:83-121): the headline step's per-allele reduction, 96
+        variants x 200 shifts x fwd/rc -> [96, 20030] fp64 (a small grid: 3 waves per SIMD)."""
     from expecto_amd import features
     g = torch.Generator(device=dev).manual_seed(3)
     res = {}
@@ -156,11 +158,21 @@ def hbm_reductions(dev):
     plus = rng.integers(0, 2, n_var).astype(bool)
     sh = shift_order(800)
     vout = torch.empty((n_var, 10 * F), dtype=torch.float64, device=dev)
+    # the headline step's own reduction (geuvadis_sed_for_top_eqtls.py:83-121): one allele of
+    # the 96-variant step, float64 fwd/rc mean, legacy 20030 layout
+    from expecto_amd import _lib
+    lib, NS = _lib.load(), 96
+    sfwd, src = fwd[:NS], rc[:NS]
+    sout = torch.empty((NS, 10 * (F + 1)), dtype=torch.float64, device=dev)
+    def sed_reduce():
+        _lib.check(lib.expecto_shift_reduce(_lib.dptr(sfwd), _lib.dptr(src), _lib.dptr(w), NS, S, F, 3,
+                                            _lib.dptr(sout), _lib.stream_ptr()), "shift_reduce")
     for name, fn, nbytes in (
             ("fp64_fill_ceiling", lambda: vout.zero_(), n_var * 10 * F * 8),   # write-only reference
             ("tss_reduce", lambda: features.tss_reduce(fwd, rc, w, out), 2 * G * S * F * 4 + G * 10 * F * 8),
             ("variant_reduce", lambda: features.variant_features(eff, dist, plus, sh, vout),
-             S9 * n_var * F * 4 + n_var * 10 * F * 8)):
+             S9 * n_var * F * 4 + n_var * 10 * F * 8),
+            ("sed_shift_reduce_96", sed_reduce, 2 * NS * S * F * 4 + NS * 10 * (F + 1) * 8)):
         fn()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -173,7 +185,7 @@ def hbm_reductions(dev):
         gbs = nbytes / (ms * 1e-3) / 1e9
         res[name] = {"ms": ms, "bytes": nbytes, "GB_per_s": gbs, "peak_GB_per_s": HBM_PEAK_GBS,
                      "frac": gbs / HBM_PEAK_GBS}
-    del fwd, rc, eff, out, vout
+    del fwd, rc, eff, out, vout, sfwd, src, sout
     torch.cuda.empty_cache()
     return res
 

@@ -287,18 +287,56 @@ __global__ void fc1_reduce_h2(const float* __restrict__ part, int splits, long l
 }
 
 // FC2 output: y[c_rows[m] or m][n] = sigmoid(sum_k part[k][m][n] * col_scale[n] + bias[n]) (Beluga.py:46-48)
-__global__ void fc2_reduce(const float* __restrict__ part, int splits, long long split_stride, int M,
-                           const float* __restrict__ bias, const float* __restrict__ col_scale,
-                           const long long* __restrict__ c_rows, float* __restrict__ y) {
+// HBM-bound (splits x 8 KB read per 8 KB row written).  Grid (kNFeat/512, row blocks): a
+// thread takes 2 adjacent features (8-B loads and store, no 64-bit division for m / n) and
+// issues a chunk's split loads before summing them; per value the same k-order sum, unscale,
+// bias and sigmoid as the one-value-per-thread kernel it replaces.
+constexpr int kFc2Chunk = 8;
+__device__ __forceinline__ float fc2_value(float s, const float* __restrict__ col_scale, const float* __restrict__ bias,
+                                           int n) {
+  if (col_scale) s *= col_scale[n];   // f16x3: exact power-of-2 unscaling of the split-K sum
+  const float v = s + bias[n];
+  return 1.0f / (1.0f + expf(-v));
+}
+__global__ __launch_bounds__(256) void fc2_reduce(const float* __restrict__ part, int splits, long long split_stride,
+                                                  int M, const float* __restrict__ bias,
+                                                  const float* __restrict__ col_scale,
+                                                  const long long* __restrict__ c_rows, float* __restrict__ y) {
+  static_assert(kNFeat % 2 == 0 && kHidLd % 2 == 0, "2 features per thread");
+  const int n = 2 * (blockIdx.x * blockDim.x + threadIdx.x);
+  if (n >= kNFeat) return;
+  for (long long m = blockIdx.y; m < M; m += gridDim.y) {
+    const float* src = part + m * kHidLd + n;
+    float s0 = 0.f, s1 = 0.f;
+    for (int k0 = 0; k0 < splits; k0 += kFc2Chunk) {
+      float2 v[kFc2Chunk];
+#pragma unroll
+      for (int u = 0; u < kFc2Chunk; ++u)
+        v[u] = *reinterpret_cast<const float2*>(src + (long long)min(k0 + u, splits - 1) * split_stride);
+#pragma unroll
+      for (int u = 0; u < kFc2Chunk; ++u)
+        if (k0 + u < splits) {
+          s0 += v[u].x;
+          s1 += v[u].y;
+        }
+    }
+    float2 o;
+    o.x = fc2_value(s0, col_scale, bias, n);
+    o.y = fc2_value(s1, col_scale, bias, n + 1);
+    *reinterpret_cast<float2*>(y + (c_rows ? c_rows[m] : m) * kNFeat + n) = o;
+  }
+}
+// One value per thread, for an output pointer that is not 8-byte aligned (same values).
+__global__ void fc2_reduce1(const float* __restrict__ part, int splits, long long split_stride, int M,
+                            const float* __restrict__ bias, const float* __restrict__ col_scale,
+                            const long long* __restrict__ c_rows, float* __restrict__ y) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long long)M * kNFeat) return;
   const int m = (int)(i / kNFeat), n = (int)(i - (long long)m * kNFeat);
   const long long src = (long long)m * kHidLd + n;
   float s = 0.f;
   for (int k = 0; k < splits; ++k) s += part[k * split_stride + src];
-  if (col_scale) s *= col_scale[n];   // f16x3: exact power-of-2 unscaling of the split-K sum
-  const float v = s + bias[n];
-  y[(c_rows ? c_rows[m] : m) * kNFeat + n] = 1.0f / (1.0f + expf(-v));
+  y[(c_rows ? c_rows[m] : m) * kNFeat + n] = fc2_value(s, col_scale, bias, n);
 }
 
 // MaxPool(1,4) floor mode at pool phases p (segment path, SURVEY.md 5 "trunk sharing"):
@@ -1223,9 +1261,12 @@ int run_fc2(expecto_beluga* h, const float* h1, int nb, float* y, hipStream_t st
       return launch_gemm<8, EPI_SIGMOID>(a, 1, st);
     }
     if ((rc = launch_gemm<8, EPI_PARTIAL>(a, h->fc2_splits, st))) return rc;
-    const long long count = (long long)nb * kNFeat;
-    fc2_reduce<<<dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st>>>(
-        h->part2, h->fc2_splits, (long long)nb * kHidLd, nb, h->fc2b, a.col_scale, c_rows, y);
+    if ((reinterpret_cast<uintptr_t>(y) & 7) == 0)
+      fc2_reduce<<<dim3((unsigned)((kNFeat / 2 + 255) / 256), (unsigned)std::max<long long>(1, std::min<long long>(nb, 65535))), dim3(256), 0,
+                   st>>>(h->part2, h->fc2_splits, (long long)nb * kHidLd, nb, h->fc2b, a.col_scale, c_rows, y);
+    else
+      fc2_reduce1<<<dim3((unsigned)(((long long)nb * kNFeat + 255) / 256)), dim3(256), 0, st>>>(
+          h->part2, h->fc2_splits, (long long)nb * kHidLd, nb, h->fc2b, a.col_scale, c_rows, y);
     if ((rc = check_launch("fc2_reduce"))) return rc;
   }
   return EXPECTO_OK;

@@ -145,6 +145,11 @@ __global__ void fwd_rc_avg_kernel(const float* __restrict__ x, int rows, int col
 // ((double)a + (double)b) / 2 like numpy on float64 prediction arrays; LEGACY writes the
 // "backwards compatibility" layout 10 x [0, f_0 .. f_{nfeat-1}] (a zero column ahead of each
 // decay block: 10 * (nfeat + 1) = 20030 features).  Shifts are summed sequentially in order.
+// Shifts whose input loads a reduction thread issues together before it runs their products
+// (all four shift/spatial reductions below): the sums still go shift by shift in order, so the
+// results are bitwise those of the one-load-then-products loop.
+constexpr int kRedChunk = 8;
+
 template <bool F64AVG, bool LEGACY>
 __global__ void shift_reduce_kernel(const float* __restrict__ fwd, const float* __restrict__ rc,
                                     const double* __restrict__ weights, int n_shift, int nfeat,
@@ -164,11 +169,24 @@ __global__ void shift_reduce_kernel(const float* __restrict__ fwd, const float* 
   for (int k = 0; k < 10; ++k) acc[k] = 0.0;
   const float* pf = fwd + g * n_shift * nfeat + f;
   const float* pr = rc + g * n_shift * nfeat + f;
-  for (int s = 0; s < n_shift; ++s) {
-    const float a = pf[(long long)s * nfeat], b = pr[(long long)s * nfeat];
-    const double pd = F64AVG ? ((double)a + (double)b) / 2.0 : (double)(0.5f * (a + b));
+  // the grid is only n_seq x nfeat threads (~3 waves per SIMD on the 96-variant step), so a
+  // loop waiting on every load was latency-bound: a chunk's 2 x kRedChunk loads go out first
+  for (int s0 = 0; s0 < n_shift; s0 += kRedChunk) {
+    float a[kRedChunk], b[kRedChunk];
 #pragma unroll
-    for (int k = 0; k < 10; ++k) acc[k] += wsx[k * n_shift + s] * pd;
+    for (int u = 0; u < kRedChunk; ++u) {
+      const int s = min(s0 + u, n_shift - 1);
+      a[u] = pf[(long long)s * nfeat];
+      b[u] = pr[(long long)s * nfeat];
+    }
+#pragma unroll
+    for (int u = 0; u < kRedChunk; ++u) {
+      if (s0 + u < n_shift) {
+        const double pd = F64AVG ? ((double)a[u] + (double)b[u]) / 2.0 : (double)(0.5f * (a[u] + b[u]));
+#pragma unroll
+        for (int k = 0; k < 10; ++k) acc[k] += wsx[k * n_shift + s0 + u] * pd;
+      }
+    }
   }
 #pragma unroll
   for (int k = 0; k < 10; ++k) o[(long long)k * (nfeat + kStride) + kStride + f] = acc[k];
@@ -228,15 +246,25 @@ __global__ void tss_reduce2_kernel(const float* __restrict__ fwd, const float* _
   const long long h2 = nfeat / 2;
   const float2* pf = reinterpret_cast<const float2*>(fwd + g * n_shift * nfeat + f);
   const float2* pr = reinterpret_cast<const float2*>(rc + g * n_shift * nfeat + f);
-#pragma unroll 4
-  for (int s = 0; s < n_shift; ++s) {
-    const float2 x = pf[s * h2], y = pr[s * h2];
-    const double p0 = (double)(0.5f * (x.x + y.x)), p1 = (double)(0.5f * (x.y + y.y));  // f32 like numpy
+  for (int s0 = 0; s0 < n_shift; s0 += kRedChunk) {   // a chunk's loads first, sums in shift order
+    float2 x[kRedChunk], y[kRedChunk];
 #pragma unroll
-    for (int k = 0; k < 10; ++k) {
-      const double w = wsh[k * n_shift + s];
-      a0[k] += w * p0;
-      a1[k] += w * p1;
+    for (int u = 0; u < kRedChunk; ++u) {
+      const int s = min(s0 + u, n_shift - 1);
+      x[u] = pf[s * h2];
+      y[u] = pr[s * h2];
+    }
+#pragma unroll
+    for (int u = 0; u < kRedChunk; ++u) {
+      if (s0 + u < n_shift) {
+        const double p0 = (double)(0.5f * (x[u].x + y[u].x)), p1 = (double)(0.5f * (x[u].y + y[u].y));  // f32 like numpy
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+          const double w = wsh[k * n_shift + s0 + u];
+          a0[k] += w * p0;
+          a1[k] += w * p1;
+        }
+      }
     }
   }
   double* o = out + g * 10LL * nfeat + f;
@@ -290,6 +318,7 @@ __global__ void variant_reduce2_kernel(const float* __restrict__ eff, const long
 #pragma clang fp contract(off)   // products rounded before the sum, as numpy
   extern __shared__ double wsh[];   // [n_shift][10]
   const long long v = blockIdx.y;
+  const int f = 2 * (blockIdx.x * blockDim.x + threadIdx.x);
   const double decay[5] = {0.01, 0.02, 0.05, 0.1, 0.2};
   for (int j = threadIdx.x; j < n_shift; j += blockDim.x) {
     const long long sgn = strand_plus[v] ? 1 : -1;
@@ -303,19 +332,33 @@ __global__ void variant_reduce2_kernel(const float* __restrict__ eff, const long
       wsh[j * 10 + 5 + k] = d >= 0 ? e : 0.0;
     }
   }
-  __syncthreads();
-  const int f = 2 * (blockIdx.x * blockDim.x + threadIdx.x);
-  if (f >= nfeat) return;
   double a0[10], a1[10];
 #pragma unroll
   for (int k = 0; k < 10; ++k) a0[k] = a1[k] = 0.0;
-  for (int j = 0; j < n_shift; ++j) {
-    const float2 e2 = *reinterpret_cast<const float2*>(eff + ((long long)j * n + v) * nfeat + f);
-    const double e0 = (double)e2.x, e1 = (double)e2.y;
+  // a chunk's loads go out before its products; the first chunk's before the weight barrier,
+  // so they overlap the exp-table prologue (sums still in shift order)
+  for (int j0 = 0; j0 < n_shift; j0 += kRedChunk) {
+    float2 e2[kRedChunk];
 #pragma unroll
-    for (int k = 0; k < 10; ++k) {
-      a0[k] += e0 * wsh[j * 10 + k];
-      a1[k] += e1 * wsh[j * 10 + k];
+    for (int u = 0; u < kRedChunk; ++u) {
+      const int j = min(j0 + u, n_shift - 1);
+      e2[u] = f < nfeat ? *reinterpret_cast<const float2*>(eff + ((long long)j * n + v) * nfeat + f) : float2{0.f, 0.f};
+    }
+    if (j0 == 0) {
+      __syncthreads();
+      if (f >= nfeat) return;
+    }
+#pragma unroll
+    for (int u = 0; u < kRedChunk; ++u) {
+      if (j0 + u < n_shift) {
+        const int j = j0 + u;
+        const double e0 = (double)e2[u].x, e1 = (double)e2[u].y;
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+          a0[k] += e0 * wsh[j * 10 + k];
+          a1[k] += e1 * wsh[j * 10 + k];
+        }
+      }
     }
   }
   double* o = out + v * 10LL * nfeat + f;

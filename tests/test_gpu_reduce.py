@@ -16,21 +16,23 @@ def _misaligned(shape):
     return buf[1:].view(*shape)          # 8-byte but not 16-byte aligned
 
 
-@pytest.mark.parametrize("nfeat", [2002, 37])
-def test_tss_reduce_matches_oracle_and_scalar_kernel(nfeat):
+@pytest.mark.parametrize("nfeat,S", [(2002, 200), (37, 200), (2002, 13)])
+def test_tss_reduce_matches_oracle_and_scalar_kernel(nfeat, S):
+    """S = 13: a shift count that is not a multiple of the kernels' 8-shift load chunk."""
     from expecto_amd.features import tss_pos_weights, tss_reduce
     from oracle.reduce_np import tss_reduce as tss_ref
     rng = np.random.default_rng(3)
-    G, S = 5, 200
+    G = 5
     f = rng.random((G, S, nfeat), dtype=np.float32)
     r = rng.random((G, S, nfeat), dtype=np.float32)
-    w = torch.from_numpy(tss_pos_weights()).cuda()
+    wn = np.ascontiguousarray(tss_pos_weights()[:, :S])
+    w = torch.from_numpy(wn).cuda()
     fd, rd = torch.from_numpy(f).cuda(), torch.from_numpy(r).cuda()
     out = tss_reduce(fd, rd, w).cpu().numpy()
     out_s = tss_reduce(fd, rd, w, out=_misaligned((G, 10 * nfeat))).cpu().numpy()
     np.testing.assert_array_equal(out, out_s)
     for g in range(G):
-        np.testing.assert_array_equal(out[g], tss_ref(f[g], r[g]))
+        np.testing.assert_array_equal(out[g], tss_ref(f[g], r[g], wn))
 
 
 @pytest.mark.parametrize("nfeat", [2002, 37])
@@ -67,16 +69,18 @@ def test_variant_features_beyond_32_shifts():
     np.testing.assert_array_equal(out, variant_reduce(list(eff), variant_weights(dist, strand, shifts), nfeat))
 
 
-def test_shift_reduce_matches_numpy_bitwise():
+@pytest.mark.parametrize("S", [200, 13])
+def test_shift_reduce_matches_numpy_bitwise(S):
     """geuvadis_sed_for_top_eqtls.py:83-121: float64 fwd/rc mean, then
-    np.sum(pos_weights[None,:,:,None] * preds[:,None], axis=2) with the legacy zero column."""
+    np.sum(pos_weights[None,:,:,None] * preds[:,None], axis=2) with the legacy zero column
+    (S = 13: the first 13 shifts' weights, a ragged last load chunk)."""
     from expecto_amd import _lib
     from expecto_amd.features import tss_pos_weights
     rng = np.random.default_rng(6)
-    n, S, F = 3, 200, 2002
+    n, F = 3, 2002
     fwd = rng.random((n, S, F), dtype=np.float32)
     rc = rng.random((n, S, F), dtype=np.float32)
-    w = tss_pos_weights()
+    w = np.ascontiguousarray(tss_pos_weights()[:, :S])
     out = torch.empty((n, 20030), dtype=torch.float64, device="cuda")
     lib = _lib.load()
     fd, rd, wd = torch.from_numpy(fwd).cuda(), torch.from_numpy(rc).cuda(), torch.from_numpy(w).cuda()
