@@ -175,9 +175,10 @@ __global__ void shift_reduce_kernel(const float* __restrict__ fwd, const float* 
     float a[kRedChunk], b[kRedChunk];
 #pragma unroll
     for (int u = 0; u < kRedChunk; ++u) {
-      const int s = min(s0 + u, n_shift - 1);
-      a[u] = pf[(long long)s * nfeat];
-      b[u] = pr[(long long)s * nfeat];
+      if (s0 + u < n_shift) {
+        a[u] = pf[(long long)(s0 + u) * nfeat];
+        b[u] = pr[(long long)(s0 + u) * nfeat];
+      }
     }
 #pragma unroll
     for (int u = 0; u < kRedChunk; ++u) {
@@ -250,9 +251,10 @@ __global__ void tss_reduce2_kernel(const float* __restrict__ fwd, const float* _
     float2 x[kRedChunk], y[kRedChunk];
 #pragma unroll
     for (int u = 0; u < kRedChunk; ++u) {
-      const int s = min(s0 + u, n_shift - 1);
-      x[u] = pf[s * h2];
-      y[u] = pr[s * h2];
+      if (s0 + u < n_shift) {
+        x[u] = pf[(s0 + u) * h2];
+        y[u] = pr[(s0 + u) * h2];
+      }
     }
 #pragma unroll
     for (int u = 0; u < kRedChunk; ++u) {
@@ -311,14 +313,11 @@ __global__ void variant_reduce_kernel(const float* __restrict__ eff, const long 
 
 // 2 features per thread (as tss_reduce2_kernel): 4 instead of 8 workgroups per variant compute
 // the 9 x 10 weights, float2 loads and double2 stores; bitwise equal to variant_reduce_kernel.
-__global__ void variant_reduce2_kernel(const float* __restrict__ eff, const long long* __restrict__ dist,
-                                       const uint8_t* __restrict__ strand_plus, const int* __restrict__ shifts,
-                                       int n_shift, int n, int nfeat, const double* __restrict__ lut,
-                                       int lut_len, double* __restrict__ out) {
-#pragma clang fp contract(off)   // products rounded before the sum, as numpy
-  extern __shared__ double wsh[];   // [n_shift][10]
-  const long long v = blockIdx.y;
-  const int f = 2 * (blockIdx.x * blockDim.x + threadIdx.x);
+// The weight prologue of one variant (shared by all its features).
+__device__ __forceinline__ void variant_weights_lds(const long long* __restrict__ dist,
+                                                    const uint8_t* __restrict__ strand_plus,
+                                                    const int* __restrict__ shifts, int n_shift, long long v,
+                                                    const double* __restrict__ lut, int lut_len, double* wsh) {
   const double decay[5] = {0.01, 0.02, 0.05, 0.1, 0.2};
   for (int j = threadIdx.x; j < n_shift; j += blockDim.x) {
     const long long sgn = strand_plus[v] ? 1 : -1;
@@ -332,33 +331,29 @@ __global__ void variant_reduce2_kernel(const float* __restrict__ eff, const long
       wsh[j * 10 + 5 + k] = d >= 0 ? e : 0.0;
     }
   }
+}
+
+__global__ void variant_reduce2_kernel(const float* __restrict__ eff, const long long* __restrict__ dist,
+                                       const uint8_t* __restrict__ strand_plus, const int* __restrict__ shifts,
+                                       int n_shift, int n, int nfeat, const double* __restrict__ lut,
+                                       int lut_len, double* __restrict__ out) {
+#pragma clang fp contract(off)   // products rounded before the sum, as numpy
+  extern __shared__ double wsh[];   // [n_shift][10]
+  const long long v = blockIdx.y;
+  variant_weights_lds(dist, strand_plus, shifts, n_shift, v, lut, lut_len, wsh);
+  __syncthreads();
+  const int f = 2 * (blockIdx.x * blockDim.x + threadIdx.x);
+  if (f >= nfeat) return;
   double a0[10], a1[10];
 #pragma unroll
   for (int k = 0; k < 10; ++k) a0[k] = a1[k] = 0.0;
-  // a chunk's loads go out before its products; the first chunk's before the weight barrier,
-  // so they overlap the exp-table prologue (sums still in shift order)
-  for (int j0 = 0; j0 < n_shift; j0 += kRedChunk) {
-    float2 e2[kRedChunk];
+  for (int j = 0; j < n_shift; ++j) {
+    const float2 e2 = *reinterpret_cast<const float2*>(eff + ((long long)j * n + v) * nfeat + f);
+    const double e0 = (double)e2.x, e1 = (double)e2.y;
 #pragma unroll
-    for (int u = 0; u < kRedChunk; ++u) {
-      const int j = min(j0 + u, n_shift - 1);
-      e2[u] = f < nfeat ? *reinterpret_cast<const float2*>(eff + ((long long)j * n + v) * nfeat + f) : float2{0.f, 0.f};
-    }
-    if (j0 == 0) {
-      __syncthreads();
-      if (f >= nfeat) return;
-    }
-#pragma unroll
-    for (int u = 0; u < kRedChunk; ++u) {
-      if (j0 + u < n_shift) {
-        const int j = j0 + u;
-        const double e0 = (double)e2[u].x, e1 = (double)e2[u].y;
-#pragma unroll
-        for (int k = 0; k < 10; ++k) {
-          a0[k] += e0 * wsh[j * 10 + k];
-          a1[k] += e1 * wsh[j * 10 + k];
-        }
-      }
+    for (int k = 0; k < 10; ++k) {
+      a0[k] += e0 * wsh[j * 10 + k];
+      a1[k] += e1 * wsh[j * 10 + k];
     }
   }
   double* o = out + v * 10LL * nfeat + f;
