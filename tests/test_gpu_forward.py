@@ -190,3 +190,21 @@ def test_conv_tile_choice_is_bitwise(monkeypatch):
         del m
     assert torch.equal(out["0"], out["256"])
     assert torch.equal(out["0"], out["384"])
+
+
+def test_forward_into_4byte_aligned_output_equals_aligned(model):
+    """A caller-owned output that is 4- but not 8-byte aligned takes fc2_reduce's one-value
+    kernel instead of the 2-wide one (expecto_beluga_forward_* write straight into `out`):
+    the same bits either way."""
+    import torch
+    from expecto_amd.encode import seqs_to_codes
+    seqs, _ = _golden_forward()
+    codes = torch.from_numpy(seqs_to_codes(seqs)).cuda()
+    eng = model.engine()
+    want = eng.forward_codes(codes).cpu().numpy()
+    rows = want.shape[0]
+    buf = torch.full((rows * 2002 + 1,), float("nan"), dtype=torch.float32, device="cuda")
+    out = buf[1:].view(rows, 2002)
+    assert out.data_ptr() % 8 == 4
+    eng.forward_codes(codes, out=out)
+    np.testing.assert_array_equal(out.cpu().numpy(), want)
