@@ -4,7 +4,7 @@
 // power-limited clock.  If the chip holds a higher clock on the 32x32x16 loop, the operand
 // delivery is a measurable share of the power the headline is bound by.
 //   hipcc --offload-arch=gfx950 -O3 tools/mfma_power_probe.hip -o tools/mfma_power_probe
-//   ./tools/mfma_power_probe [iters16]   -> one JSON line per (form, launch)
+//   ./tools/mfma_power_probe [iters] [zero_frac]   -> one JSON line per (form, launch)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -73,6 +73,8 @@ __global__ __launch_bounds__(256) void mfma32(const halfx8* __restrict__ in, int
 
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 3000000;
+  // optional: fraction of operand elements set to zero (ReLU-like sparsity of real activations)
+  const double zero_frac = argc > 2 ? atof(argv[2]) : 0.0;
   int ncu = 0;
   CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
   const int blocks = ncu * 4;   // 4 workgroups x 4 waves per CU = 4 waves per SIMD
@@ -86,6 +88,8 @@ int main(int argc, char** argv) {
     for (int e = 0; e < 8; ++e) {
       r = r * 1664525u + 1013904223u;
       h[i][e] = (_Float16)(((int)(r >> 9) % 2001 - 1000) * 1e-6f);   // random-looking, no overflow
+      r = r * 1664525u + 1013904223u;
+      if ((r >> 8) % 1000 < (unsigned)(zero_frac * 1000)) h[i][e] = (_Float16)0.f;
     }
   CHECK(hipMemcpy(in, h, sizeof(h), hipMemcpyHostToDevice));
   hipEvent_t e0, e1;
@@ -105,9 +109,10 @@ int main(int argc, char** argv) {
       float ms = 0.f;
       CHECK(hipEventElapsedTime(&ms, e0, e1));
       const double tf = flops / (ms * 1e-3) / 1e12;
-      printf("{\"form\": \"%s\", \"rep\": %d, \"ms\": %.2f, \"tflops\": %.1f, \"frac_of_2516.6\": %.4f, "
-             "\"clock_ghz_if_busy\": %.3f}\n",
-             form == 0 ? "16x16x32_f16" : "32x32x16_f16", rep, ms, tf, tf / 2516.5824, 2.4 * tf / 2516.5824);
+      printf("{\"form\": \"%s\", \"zero_frac\": %.2f, \"rep\": %d, \"ms\": %.2f, \"tflops\": %.1f, "
+             "\"frac_of_2516.6\": %.4f, \"clock_ghz_if_busy\": %.3f}\n",
+             form == 0 ? "16x16x32_f16" : "32x32x16_f16", zero_frac, rep, ms, tf, tf / 2516.5824,
+             2.4 * tf / 2516.5824);
       fflush(stdout);
     }
   }
