@@ -251,6 +251,7 @@ def time_steps(step, eng, steps, warmup, world, dev):
         events[slot].synchronize()
         if f16 and int(flags[slot][0]):
             fallbacks += 1
+            eng.count_fallback()
             with eng.precision_override("bf16x6"):
                 step(slot)
             torch.cuda.synchronize()

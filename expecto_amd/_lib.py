@@ -48,6 +48,7 @@ SIGNATURES = {
     "expecto_beluga_set_overflow_check": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "expecto_beluga_overflow_pending": (ctypes.c_int, [c_vp, c_vp]),
     "expecto_beluga_overflow_take": (ctypes.c_int, [c_vp, c_vp, c_vp]),
+    "expecto_beluga_count_fallback": (ctypes.c_int, [c_vp]),
     "expecto_beluga_set_profiling": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "expecto_beluga_layer_times": (ctypes.c_int, [c_vp, c_f64p, c_i64p, c_f64p, ctypes.c_int]),
     "expecto_variant_windows": (ctypes.c_int, [c_vp, ctypes.c_longlong, c_vp, c_vp, c_vp, ctypes.c_int, c_vp,

@@ -108,6 +108,11 @@ class BelugaEngine:
             _lib.check(self.lib.expecto_beluga_overflow_take(self.handle, ctypes.c_void_p(dst.data_ptr()),
                                                              _lib.stream_ptr(stream)), "overflow_take")
 
+    def count_fallback(self):
+        """Deferred mode: record that a batch flagged through ``overflow_take`` was recomputed in
+        bf16x6 (``f16_state()`` reports the count)."""
+        _lib.check(self.lib.expecto_beluga_count_fallback(self.handle), "count_fallback")
+
     def precision_override(self, precision: str):
         """Context manager: run the enclosed calls in another arithmetic, then restore."""
         import contextlib

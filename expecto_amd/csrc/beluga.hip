@@ -2210,6 +2210,12 @@ int expecto_beluga_overflow_take(expecto_beluga_t h, int* dst, void* stream) {
   return EXPECTO_OK;
 }
 
+int expecto_beluga_count_fallback(expecto_beluga_t h) {
+  EXPECTO_REQUIRE(h != nullptr, "null handle");
+  h->fallbacks += 1;
+  return EXPECTO_OK;
+}
+
 int expecto_beluga_overflow_pending(expecto_beluga_t h, void* stream) {
   EXPECTO_REQUIRE(h != nullptr, "null handle");
   if (!h->ovf) return 0;

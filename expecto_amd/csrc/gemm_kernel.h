@@ -1165,13 +1165,15 @@ __device__ __forceinline__ void gemm_fc_h3p_body(const GemmArgs& p, char* smem) 
     const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, 0x7fffffff, 0x00020000);
     auto issue = [&](int s, int slot) {
       if constexpr ((TM & 8) != 0) s = 0;
+      // probes (tools/gemm_bench): 16 = A pieces always from stage 0 (L2-hot A), 32 = B hot
+      const int sa = (TM & 16) ? 0 : s, sb = (TM & 32) ? 0 : s;
       char* base = smem + slot * FCP_STAGE;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) glds16(asrc[i] + (long long)s * ROW_KB, base + adst[i]);
+      for (int i = 0; i < 8; ++i) glds16(asrc[i] + (long long)sa * ROW_KB, base + adst[i]);
 #pragma unroll
       for (int j = 0; j < 5; ++j)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + 2 * FCP_APLANE + (pw + 4 * j) * 1024), 16,
-                                                 boff[j], (unsigned)(s * ROW_KB), 0, 0);
+                                                 boff[j], (unsigned)(sb * ROW_KB), 0, 0);
     };
     for (int s = 0; s < NS - 1; ++s) issue(min(s, nk - 1), s);
     if constexpr (PF)

@@ -290,7 +290,8 @@ __global__ void variant_reduce_kernel(const float* __restrict__ eff, const long 
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
       // host table exp(-c_k * fl) (numpy's exp, as predict.py:88-107) when given, else the device exp
-      const double e = lut ? lut[k * lut_len + (long long)fl] : exp(-decay[k] * fl);
+      // (a table too short for this distance: the device exp, never a read past its end)
+      const double e = lut && fl < (double)lut_len ? lut[k * lut_len + (long long)fl] : exp(-decay[k] * fl);
       wsh[j * 10 + k] = d <= 0 ? e : 0.0;
       wsh[j * 10 + 5 + k] = d >= 0 ? e : 0.0;
     }
@@ -326,7 +327,8 @@ __device__ __forceinline__ void variant_weights_lds(const long long* __restrict_
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
       // host table exp(-c_k * fl) (numpy's exp, as predict.py:88-107) when given, else the device exp
-      const double e = lut ? lut[k * lut_len + (long long)fl] : exp(-decay[k] * fl);
+      // (a table too short for this distance: the device exp, never a read past its end)
+      const double e = lut && fl < (double)lut_len ? lut[k * lut_len + (long long)fl] : exp(-decay[k] * fl);
       wsh[j * 10 + k] = d <= 0 ? e : 0.0;
       wsh[j * 10 + 5 + k] = d >= 0 ? e : 0.0;
     }
@@ -481,9 +483,13 @@ int expecto_fwd_rc_average(const float* x, int rows, int cols, float* out, void*
   return check_launch("fwd_rc_average");
 }
 
+// The reductions stage their [n_shift][10] f64 weights in dynamic LDS: at most 64 KiB per
+// workgroup without an opt-in attribute, so 819 shifts (the reference sweeps 9 to 201).
+constexpr int kMaxShifts = 65536 / (10 * (int)sizeof(double));
+
 int expecto_tss_reduce(const float* fwd, const float* rc, const double* weights, int n_genes, int n_shift, int nfeat,
                        double* out, void* stream) {
-  EXPECTO_REQUIRE(n_genes >= 0 && n_shift > 0 && n_shift <= 4096 && nfeat > 0, "bad shape");
+  EXPECTO_REQUIRE(n_genes >= 0 && n_shift > 0 && n_shift <= kMaxShifts && nfeat > 0, "bad shape (n_shift <= 819)");
   if (n_genes == 0) return EXPECTO_OK;
   EXPECTO_REQUIRE(n_genes <= 65535, "at most 65535 genes per call");
   EXPECTO_REQUIRE(fwd && rc && weights && out, "null argument");
@@ -504,7 +510,7 @@ int expecto_tss_reduce(const float* fwd, const float* rc, const double* weights,
 int expecto_variant_reduce_lut(const float* effects, const long long* dist, const uint8_t* strand_plus,
                                const int* shifts, int n_shift, int n, int nfeat, const double* exp_lut, int lut_len,
                                double* out, void* stream) {
-  EXPECTO_REQUIRE(n >= 0 && n_shift > 0 && n_shift <= 4096 && nfeat > 0, "bad shape (n_shift <= 4096)");
+  EXPECTO_REQUIRE(n >= 0 && n_shift > 0 && n_shift <= kMaxShifts && nfeat > 0, "bad shape (n_shift <= 819)");
   if (n == 0) return EXPECTO_OK;
   EXPECTO_REQUIRE(n <= 65535, "at most 65535 variants per call");
   EXPECTO_REQUIRE(effects && dist && strand_plus && shifts && out, "null argument");
@@ -540,7 +546,7 @@ int expecto_gblinear_predict(const double* X, long long n, long long ld, const i
 
 int expecto_shift_reduce(const float* fwd, const float* rc, const double* weights, int n_genes, int n_shift, int nfeat,
                          int flags, double* out, void* stream) {
-  EXPECTO_REQUIRE(n_genes >= 0 && n_shift > 0 && n_shift <= 4096 && nfeat >= 10, "bad shape");
+  EXPECTO_REQUIRE(n_genes >= 0 && n_shift > 0 && n_shift <= kMaxShifts && nfeat >= 10, "bad shape (n_shift <= 819)");
   EXPECTO_REQUIRE((flags & ~3) == 0, "bad flags");
   if (n_genes == 0) return EXPECTO_OK;
   EXPECTO_REQUIRE(n_genes <= 65535, "at most 65535 sequences per call");

@@ -144,7 +144,10 @@ class RowWriter:
     dtype, trailing dims of the dataset) at rows ``row0..`` in place.  Once every row is written
     the file is byte-identical to ``write`` of the full arrays."""
 
-    def __init__(self, path: str, specs: dict):
+    def __init__(self, path: str, specs: dict, create: bool = True):
+        """create=False attaches to a file another process created with the same specs (its
+        header is checked, nothing is truncated): several ranks then write disjoint rows of one
+        file, each with its own descriptor (pwrite at row offsets; no locking needed)."""
         import os
         self.names = sorted(specs)
         self.shapes = {n: tuple(int(x) for x in specs[n][0]) for n in self.names}
@@ -154,9 +157,20 @@ class RowWriter:
         head, addr, eof = _layout(self.names, [self.shapes[n] for n in self.names],
                                   [self.dtypes[n] for n in self.names])
         self.addr = dict(zip(self.names, addr))
-        self.fd = os.open(path, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o644)
-        os.pwrite(self.fd, head, 0)
-        os.ftruncate(self.fd, eof)
+        self.fd = None
+        if create:
+            self.fd = os.open(path, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o644)
+            os.pwrite(self.fd, head, 0)
+            os.ftruncate(self.fd, eof)
+        else:
+            fd = os.open(path, os.O_RDWR)
+            try:
+                if os.fstat(fd).st_size != eof or os.pread(fd, len(head), 0) != head:
+                    raise ValueError(f"{path}: not a row file of these datasets (header or size differ)")
+            except BaseException:
+                os.close(fd)
+                raise
+            self.fd = fd
 
     def write_rows(self, name: str, row0: int, block: np.ndarray) -> None:
         import os

@@ -182,6 +182,10 @@ int expecto_beluga_overflow_pending(expecto_beluga_t h, void* stream);
  * forward calls, *dst holds exactly that batch's overflow state once an event recorded after it
  * has completed (the stream runs in order), while later batches are already queued. */
 int expecto_beluga_overflow_take(expecto_beluga_t h, int* dst, void* stream);
+/* Deferred mode: the caller acted on a flag obtained through expecto_beluga_overflow_take and
+ * recomputed that batch with BF16X6; adds one to the count expecto_beluga_f16_fallbacks reports
+ * (expecto_beluga_overflow_pending counts its own). */
+int expecto_beluga_count_fallback(expecto_beluga_t h);
 
 /* Per-layer device time accumulated over forward calls while profiling is on (ms), launches
  * (`calls`) and executed multiply-adds (`macs`: GEMM M x N x K actually run, including the
@@ -227,7 +231,9 @@ int expecto_fwd_rc_average(const float* x, int rows, int cols, float* out, void*
 
 /* TSS reduction for n_genes genes: fwd and rc are [n_genes, n_shift, nfeat] fp32;
  * weights [10, n_shift] fp64; out [n_genes, 10*nfeat] fp64 with
- * out[g, k*nfeat + f] = sum_s weights[k,s] * (0.5f*(fwd[g,s,f] + rc[g,s,f])). */
+ * out[g, k*nfeat + f] = sum_s weights[k,s] * (0.5f*(fwd[g,s,f] + rc[g,s,f])).
+ * The reductions below stage their weights in 64 KiB of LDS: n_shift <= 819 (EXPECTO_EINVAL
+ * otherwise; the reference sweeps 9 to 201 shifts). */
 int expecto_tss_reduce(const float* fwd, const float* rc, const double* weights, int n_genes, int n_shift,
                        int nfeat, double* out, void* stream);
 
@@ -237,9 +243,10 @@ int expecto_tss_reduce(const float* fwd, const float* rc, const double* weights,
 int expecto_variant_reduce(const float* effects, const long long* dist, const uint8_t* strand_plus,
                            const int* shifts, int n_shift, int n, int nfeat, double* out, void* stream);
 /* The same with the decay factors from a table: exp_lut[k*lut_len + fl] = exp(-c_k * fl)
- * (c = 0.01, 0.02, 0.05, 0.1, 0.2; every fl = floor(|d|/200) < lut_len; DEVICE array) computed
- * by the caller with the reference's own exp (numpy, predict.py:88-107), so the features equal
- * the reference's bit for bit; expecto_variant_reduce uses the device exp (within 1 ulp). */
+ * (c = 0.01, 0.02, 0.05, 0.1, 0.2; DEVICE array) computed by the caller with the reference's
+ * own exp (numpy, predict.py:88-107), so the features equal the reference's bit for bit;
+ * expecto_variant_reduce uses the device exp (within 1 ulp).  A distance whose fl =
+ * floor(|d|/200) is >= lut_len takes the device exp too (never a read past the table). */
 int expecto_variant_reduce_lut(const float* effects, const long long* dist, const uint8_t* strand_plus,
                                const int* shifts, int n_shift, int n, int nfeat, const double* exp_lut, int lut_len,
                                double* out, void* stream);

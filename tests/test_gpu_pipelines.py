@@ -277,9 +277,11 @@ def test_second_stream_overlap_is_bitwise_equal(monkeypatch):
 def test_chromatin_cli_two_ranks_equals_one(workdir):
     """The CLI sharded over 2 ranks (torch.distributed.run; gloo, both ranks on this one GPU:
     the 8-GPU RCCL run is the driver's) and streamed in batches of 2 variants (uneven last
-    batches) writes the same files byte for byte as one rank in one batch: shards are contiguous
-    variant ranges, each batch is gathered to rank 0 and written at its rows; only rank 0 writes
-    snps_hg19.vcf.  One rank streaming 2-variant batches writes the same bytes too."""
+    batches) writes the same files byte for byte as one rank in one batch, in both output modes:
+    every rank writing its own rows into the files rank 0 created (default), and each batch
+    gathered to rank 0 which writes it.  Shards are contiguous variant ranges; only rank 0 writes
+    snps_hg19.vcf; no .part file is left.  One rank streaming 2-variant batches writes the same
+    bytes too."""
     import socket
     import subprocess
     import sys
@@ -294,24 +296,65 @@ def test_chromatin_cli_two_ranks_equals_one(workdir):
     chromatin.main([str(vcf), "--output_dir", str(one)] + common)
     one_b2 = workdir / "out_1rank_b2"
     chromatin.main([str(vcf), "--output_dir", str(one_b2), "--variant-batch", "2"] + common)
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    two = workdir / "out_2rank"
-    env = dict(os.environ, EXPECTO_DIST_BACKEND="gloo")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "expecto_amd.chromatin",
-                        str(vcf), "--output_dir", str(two), "--variant-batch", "2"] + common,
-                       env=env, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                       capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stderr[-3000:]
-    for name in ["snps_hg19.vcf"] + [f"snps.shift_{sh}.diff.h5" for sh in (0, -200, 200)]:
-        want = open(one / name, "rb").read()
-        assert open(two / name, "rb").read() == want, name
-        assert open(one_b2 / name, "rb").read() == want, name
-    a = h5.read(str(two / "snps.shift_200.diff.h5"))
-    assert a["ref"].shape == (12, 2002) and float(np.abs(a["ref"]).min()) > 0
+    names = ["snps_hg19.vcf"] + [f"snps.shift_{sh}.diff.h5" for sh in (0, -200, 200)]
+    for mode in ("rank", "gather"):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        two = workdir / f"out_2rank_{mode}"
+        env = dict(os.environ, EXPECTO_DIST_BACKEND="gloo")
+        r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                            "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "expecto_amd.chromatin",
+                            str(vcf), "--output_dir", str(two), "--variant-batch", "2", "--output-mode", mode] + common,
+                           env=env, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+        assert sorted(os.listdir(two)) == sorted(names), mode
+        for name in names:
+            want = open(one / name, "rb").read()
+            assert open(two / name, "rb").read() == want, (mode, name)
+            assert open(one_b2 / name, "rb").read() == want, name
+        a = h5.read(str(two / "snps.shift_200.diff.h5"))
+        assert a["ref"].shape == (12, 2002) and float(np.abs(a["ref"]).min()) > 0
+
+
+def test_chromatin_cli_failed_batch_leaves_no_output(workdir):
+    """A batch that fails after earlier batches were written (here: an invalid alt base in the
+    4th 2-variant batch -> KeyError, as encodeSeqs raises in the reference) leaves no
+    snps.shift_*.diff.h5 (nor .part) behind: the files are written as .part and renamed only
+    once every batch succeeded (the reference computes everything before it writes)."""
+    from expecto_amd import chromatin
+    vcf = workdir / "bad.vcf"
+    lines = [l for l in open(os.path.join(GOLDEN, "chromatin_vcf.txt")).read().splitlines()
+             if l and not l.startswith("#")]
+    snv = [l for l in lines if len(l.split("\t")[3]) == 1 and len(l.split("\t")[4]) == 1]
+    assert len(snv) >= 3
+    with open(vcf, "w") as f:
+        for l in snv[:3] * 2:
+            f.write(l + "\n")
+        c = snv[0].split("\t")
+        c[4] = "Z"
+        f.write("\t".join(c) + "\n")
+    out = workdir / "out_bad"
+    with pytest.raises(KeyError):
+        chromatin.main([str(vcf), "--output_dir", str(out), "--maxshift", "200", "--genome", str(workdir / "hg19.fa"),
+                        "--synthetic-weights", "0", "--max-batch", "40", "--variant-batch", "2"])
+    left = sorted(os.listdir(out))
+    assert left == ["snps_hg19.vcf"], left
+
+
+def test_chromatin_cli_batch_gb_caps_the_batch():
+    """--batch-gb lowers --variant-batch so one batch's y + diff of every shift fits the cap
+    (a 201-shift sweep at the default 4096 variants would pin ~79 GB)."""
+    from expecto_amd import chromatin
+    a = chromatin.build_parser().parse_args(["x.vcf"])
+    assert chromatin.batch_variants(a, 9) == 4096
+    per_variant = 6 * 201 * 2002 * 4
+    b = chromatin.batch_variants(a, 201)
+    assert b * per_variant <= 4 * (1 << 30) < (b + 1) * per_variant
+    a = chromatin.build_parser().parse_args(["x.vcf", "--batch-gb", "0"])
+    assert chromatin.batch_variants(a, 9) == 1
 
 
 def test_tss_compute_two_ranks_equals_one(workdir):

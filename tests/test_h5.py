@@ -61,3 +61,45 @@ def test_h5py_reads_our_files(tmp_path):
             "assert np.array_equal(f['diff'][6:12, :], (a-0.5)[6:12]); print('ok')")
     r = subprocess.run([H5PY_PY, "-c", code, p, str(tmp_path / "a.npy")], capture_output=True, text=True)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr
+
+
+def _attach_and_write(path, specs, blocks, q):
+    from expecto_amd import h5
+    try:
+        with h5.RowWriter(path, specs, create=False) as w:
+            for name, r0, blk in blocks:
+                w.write_rows(name, r0, blk)
+        q.put(None)
+    except Exception as e:   # noqa: BLE001
+        q.put(repr(e))
+
+
+def test_row_writer_shared_by_processes(tmp_path):
+    """The chromatin CLI's multi-rank output (--output-mode rank): one process creates the row
+    file, others attach (create=False) and pwrite disjoint row blocks through their own
+    descriptors; the result is byte-identical to writing the whole arrays at once.  Attaching
+    to a file of other datasets is refused."""
+    import multiprocessing as mp
+    from expecto_amd import h5
+    rng = np.random.default_rng(3)
+    full = {k: rng.standard_normal((12, 7)).astype(np.float32) for k in ("alt", "diff", "ref")}
+    ref_path = str(tmp_path / "whole.h5")
+    h5.write(ref_path, full)
+    specs = {k: ((12, 7), np.float32) for k in full}
+    path = str(tmp_path / "shared.h5")
+    h5.RowWriter(path, specs).close()
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    procs = []
+    for r0, r1 in ((0, 5), (5, 12)):   # two "ranks", each its own rows of every dataset
+        blocks = [(k, r0, full[k][r0:r1]) for k in full]
+        p = ctx.Process(target=_attach_and_write, args=(path, specs, blocks, q))
+        p.start()
+        procs.append(p)
+    errs = [q.get(timeout=60) for _ in procs]
+    for p in procs:
+        p.join(60)
+    assert errs == [None, None]
+    assert open(path, "rb").read() == open(ref_path, "rb").read()
+    with pytest.raises(ValueError):
+        h5.RowWriter(path, {k: ((13, 7), np.float32) for k in full}, create=False)

@@ -104,39 +104,46 @@ void fc1p_launch(const GemmArgs& a, unsigned nblk) { beluga_fc_h3p<7, EPI_PARTIA
 template <int TM, int NS = 3, int NB = 10, int NW = 4>
 void fc1r_launch(const GemmArgs& a, unsigned nblk) { beluga_fc_h3<7, EPI_PARTIAL, TM, NS, NB, NW><<<nblk, 64 * NW>>>(a); }
 
-int fc1_bench(int nb, int rounds, int splits) {
+int fc1_bench(int nb, int rounds, int splits, bool toe) {
   const int K = 67840, npad = 2080, ldc = 2016;
+  // toe: A rows gathered like the segment path's FC1 (a_rows): windows in groups of 100 whose
+  // conv6 rows start 25 rows apart (one pool2 phase of one 200-shift segment), so the A rows
+  // overlap 4.24-fold and their unique bytes are ~4x fewer than nb x K
+  const int grp = 100, grows = 25 * (grp - 1) + 106 + 8;
+  const long long xrows = toe ? (long long)(nb + grp - 1) / grp * grows * 640 / K + 2 : nb;
   float *X, *W, *C;
-  CK(hipMalloc(&X, (size_t)nb * K * 4));
+  CK(hipMalloc(&X, (size_t)xrows * K * 4));
   CK(hipMalloc(&W, (size_t)npad * K * 4));
   CK(hipMalloc(&C, (size_t)splits * nb * ldc * 4));
-  hash_fill<<<(unsigned)(((long long)nb * K + 255) / 256), 256>>>(X, (long long)nb * K, 0.f, 1.f, 1);
+  hash_fill<<<(unsigned)(((long long)xrows * K + 255) / 256), 256>>>(X, (long long)xrows * K, 0.f, 1.f, 1);
   hash_fill<<<(unsigned)(((long long)npad * K + 255) / 256), 256>>>(W, (long long)npad * K, -0.05f, 0.05f, 2);
   int* zs;
-  CK(hipMalloc(&zs, std::max(nb, npad) * 4));
-  CK(hipMemset(zs, 0, std::max(nb, npad) * 4));
+  CK(hipMalloc(&zs, std::max<long long>(xrows, npad) * 4));
+  CK(hipMemset(zs, 0, std::max<long long>(xrows, npad) * 4));
   _Float16 *Xh, *Bh;
-  CK(hipMalloc(&Xh, (size_t)nb * K * 4));
+  CK(hipMalloc(&Xh, (size_t)xrows * K * 4));
   CK(hipMalloc(&Bh, (size_t)npad * K * 4));
-  split_planes_h2<<<(unsigned)(((long long)nb * K / 4 + 255) / 256), 256>>>(X, nb, K, zs, Xh);
+  split_planes_h2<<<(unsigned)(((long long)xrows * K / 4 + 255) / 256), 256>>>(X, xrows, K, zs, Xh);
   split_planes_h2<<<(unsigned)(((long long)npad * K / 4 + 255) / 256), 256>>>(W, npad, K, zs, Bh);
+  long long* arows = nullptr;
+  if (toe) {
+    std::vector<long long> ar(nb);
+    for (int m = 0; m < nb; ++m) ar[m] = ((long long)(m / grp) * grows + 25LL * (m % grp)) * 640;
+    CK(hipMalloc(&arows, nb * 8));
+    CK(hipMemcpy(arows, ar.data(), nb * 8, hipMemcpyHostToDevice));
+  }
   CK(hipDeviceSynchronize());
   GemmArgs a{};
   a.A = (const float*)Xh; a.lda = K; a.M = nb; a.B = W; a.Bp = Bh; a.ldb = K; a.kper = K / splits; a.taps = 1;
   a.n_tiles = npad / GBN; a.m_tiles = (nb + X6P_BM - 1) / X6P_BM; a.m_fastest = 1; a.linear_order = 1;
-  a.C = C; a.ldc = ldc; a.n_store = ldc; a.split_stride = (long long)nb * ldc;
-  struct V { const char* name; void (*f)(const GemmArgs&, unsigned); int nb = 10; };
-  // block orders: m = M tiles fastest in dispatch order (the library's FC1 order), n = N tiles
-  // fastest in dispatch order, x = N tiles fastest per XCD (XCD-aware remap)
-  V vs[] = {{"h3q_m", fc1_launch<0>}, {"h3q_n", fc1_launch<0>}, {"h3q_x", fc1_launch<0>},
-            {"fcr_m", fc1r_launch<0>}, {"fcr_n", fc1r_launch<0>}, {"fcr_x", fc1r_launch<0>},
-            {"fcr_x_noload", fc1r_launch<2>}, {"fcr_x_hotAB", fc1r_launch<8>},
-            {"fc4_m", fc1r_launch<0, 4>}, {"fc4_x", fc1r_launch<0, 4>},
-            {"fcp_m", fc1p_launch<0>}, {"fcp_m_pf", fc1p_launch<256>}, {"fcp_x", fc1p_launch<0>},
-            {"fcp_x_pf", fc1p_launch<256>},
-            {"fcp_x_noload", fc1p_launch<2>},
-            {"fcp_x_hotAB", fc1p_launch<8>},
-            {"fcp_m_old", fc1p_launch<4096>}, {"fcp_x_old", fc1p_launch<4096>}};
+  a.C = C; a.ldc = ldc; a.n_store = ldc; a.split_stride = (long long)nb * ldc; a.a_rows = arows;
+  struct V { const char* name; void (*f)(const GemmArgs&, unsigned); };
+  // block orders: m = M tiles fastest in dispatch order, x = N tiles fastest per XCD (XCD-aware
+  // remap; the library's order for large M).  Probes (wrong results): hotA / hotB / hotAB = that
+  // operand's LDS-DMA always from K stage 0 (L2-hot), noload = no LDS-DMA in the loop.
+  V vs[] = {{"fcp_m", fc1p_launch<0>}, {"fcp_x", fc1p_launch<0>},
+            {"fcp_x_hotA", fc1p_launch<16>}, {"fcp_x_hotB", fc1p_launch<32>},
+            {"fcp_x_hotAB", fc1p_launch<8>}, {"fcp_x_noload", fc1p_launch<2>}};
   constexpr int NV = sizeof(vs) / sizeof(vs[0]);
   const size_t csz = (size_t)splits * nb * ldc;
   std::vector<float> ref(csz), out(csz);
@@ -147,19 +154,17 @@ int fc1_bench(int nb, int rounds, int splits) {
   for (int r = 0; r < rounds; ++r)
     for (int v = 0; v < NV; ++v) {
       CK(hipMemset(C, 0, csz * 4));
-      const char o = vs[v].name[3] == '_' ? vs[v].name[4] : vs[v].name[4] == '_' ? vs[v].name[5] : vs[v].name[4];
-      a.m_fastest = o == 'm';
-      a.linear_order = o != 'x';
-      a.n_tiles = (2016 + 16 * vs[v].nb - 1) / (16 * vs[v].nb);
+      a.m_fastest = vs[v].name[4] == 'm';
+      a.linear_order = vs[v].name[4] != 'x';
       const unsigned nblk = (unsigned)(a.m_tiles * a.n_tiles * splits);
       vs[v].f(a, nblk);
-      if (r == 0 && strstr(vs[v].name, "no") == nullptr) {
+      if (r == 0 && strstr(vs[v].name, "hot") == nullptr && strstr(vs[v].name, "no") == nullptr) {
         CK(hipDeviceSynchronize());
         CK(hipMemcpy(v == 0 ? ref.data() : out.data(), C, csz * 4, hipMemcpyDeviceToHost));
         if (v > 0) {
           size_t bad = 0;
           for (size_t i = 0; i < csz; ++i) bad += memcmp(&ref[i], &out[i], 4) != 0;
-          printf("variant %s vs h3q: %zu of %zu partials differ bitwise\n", vs[v].name, bad, csz);
+          printf("variant %s vs %s: %zu of %zu partials differ bitwise\n", vs[v].name, vs[0].name, bad, csz);
         }
       }
       CK(hipEventRecord(e0));
@@ -171,10 +176,11 @@ int fc1_bench(int nb, int rounds, int splits) {
       t[v].push_back(ms);
     }
   const double flops = 2.0 * nb * 2003.0 * K;
-  printf("shape fc1 windows %d splits %d (M=%d K=%d N=2003)\n", nb, splits, nb, K);
+  printf("shape fc1 windows %d splits %d %s (M=%d K=%d N=2003)\n", nb, splits, toe ? "toeplitz-rows" : "dense-rows",
+         nb, K);
   for (int v = 0; v < NV; ++v) {
     std::sort(t[v].begin(), t[v].end());
-    printf("  %-12s median %8.3f ms  %7.1f TFLOP/s fp32-equivalent\n", vs[v].name, t[v][t[v].size() / 2],
+    printf("  %-14s median %8.3f ms  %7.1f TFLOP/s fp32-equivalent\n", vs[v].name, t[v][t[v].size() / 2],
            flops / (t[v][t[v].size() / 2] * 1e-3) / 1e12);
   }
   return 0;
@@ -184,7 +190,8 @@ int main(int argc, char** argv) {
   const int nb = argc > 1 ? atoi(argv[1]) : 1000;
   const int rounds = argc > 2 ? atoi(argv[2]) : 5;
   const char* which = argc > 3 ? argv[3] : "conv2";
-  if (!strcmp(which, "fc1")) return fc1_bench(nb, rounds, argc > 4 ? atoi(argv[4]) : 20);
+  if (!strcmp(which, "fc1") || !strcmp(which, "fc1t"))
+    return fc1_bench(nb, rounds, argc > 4 ? atoi(argv[4]) : 8, which[3] == 't');
   struct Shape { const char* name; int cin, cout, s_in, t_valid, s_out, pool; double macs; };
   Shape shapes[] = {{"conv2", 320, 320, 2000, 496, 500, 1, 1986.0 * 320 * 2560},
                     {"conv3", 320, 480, 500, 489, 500, 0, 489.0 * 480 * 2560},
