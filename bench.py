@@ -22,7 +22,7 @@ shift over RCCL (the file-output exchange), both timed.  Rank 0 prints ONE JSON 
 N=1 extras, outside `value`: the headline in bf16x6 (fp32-faithful split), configs[1]
 (1k SNVs, shift 0), configs[2] (+-800 sweep), configs[4] TSS genes, the chromatin CLI end to
 end (streamed batches vs one batch: compute overlapped with the .diff.h5 writes), the HBM-bound
-reductions in GB/s, and the CPU port timed on host cores (P = 8 and 16 threads, batch 32 and 512).
+reductions in GB/s, and the CPU port timed on host cores (P = this job's CPU share and 8, batch 32 and 512).
 """
 from __future__ import annotations
 
@@ -96,18 +96,42 @@ def kernel_name(layer: str, precision: str, segments: bool = True) -> str:
 
 
 # ---- CPU baseline ---------------------------------------------------------------------------
+def host_cpu_share():
+    """CPUs this job may use: the affinity mask (os.sched_getaffinity) and the cgroup v2 / v1
+    CPU quota (cpu.max, cfs_quota_us / cfs_period_us), whichever is smaller.  os.cpu_count()
+    reports the whole machine (256 on the GPU box), not this job's share."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    share = aff if quota is None else max(1, min(aff, int(math.ceil(quota))))
+    return {"affinity_cpus": aff, "cgroup_cpus": quota, "host_cpu_count": os.cpu_count(), "share": share}
+
+
 def cpu_baseline(sd_cpu, codes: np.ndarray, seconds: float, windows_per_variant: int):
     """Oracle torch-CPU forward (the reference's CPU arithmetic, oneDNN fp32) on a bounded sample
-    of the headline's windows, at P = 8 and 16 host threads (16 = this job's CPU share of the
-    box; os.cpu_count() reports the whole machine) and batch 32 and 512.  Per
-    window the cost is linear, so windows/s extrapolates; variants/s = windows/s / 800 (the
-    reference forwards every window of a 200-window variant, geuvadis_sed_for_top_eqtls.py:80-98)."""
+    of the headline's windows, at P = this job's CPU share (affinity mask and cgroup quota,
+    host_cpu_share; SURVEY.md 8(d) "P = all physical cores" of what the job may use) and P = 8,
+    batch 32 and 512.  Per window the cost is linear, so windows/s extrapolates; variants/s =
+    windows/s / 800 (the reference forwards every window of a 200-window variant,
+    geuvadis_sed_for_top_eqtls.py:80-98).  `value` is the best setting; `cores` its thread count."""
     from oracle.beluga_np import forward_torch_cpu
     from expecto_amd.encode import codes_to_onehot
 
+    share = host_cpu_share()
     x_all = torch.from_numpy(codes_to_onehot(codes, with_rc=False).astype(np.float32)).unsqueeze(2)
     runs = {}
-    for threads in (16, 8):
+    for threads in sorted({share["share"], 8}, reverse=True):
         torch.set_num_threads(threads)
         forward_torch_cpu(sd_cpu, x_all[:4])                     # warm-up
         for batch in (32, 512):
@@ -119,16 +143,19 @@ def cpu_baseline(sd_cpu, codes: np.ndarray, seconds: float, windows_per_variant:
                 el = time.perf_counter() - t0
                 if el >= seconds:
                     break
-            runs[f"p{threads}_b{batch}"] = {"windows_per_s": done / el, "windows": done, "s": el}
-    best16 = max((v for k, v in runs.items() if k.startswith("p16")), key=lambda v: v["windows_per_s"])
-    b16 = max((k for k in runs if k.startswith("p16")), key=lambda k: runs[k]["windows_per_s"])
-    return {"value": best16["windows_per_s"] / windows_per_variant, "unit": "variants/s", "cores": 16,
-            "kind": "port", "windows_per_s": best16["windows_per_s"], "host_cpu_count": os.cpu_count(),
+            runs[f"p{threads}_b{batch}"] = {"windows_per_s": done / el, "windows": done, "s": el,
+                                            "threads": threads, "batch": batch}
+    best_k = max(runs, key=lambda k: runs[k]["windows_per_s"])
+    best = runs[best_k]
+    return {"value": best["windows_per_s"] / windows_per_variant, "unit": "variants/s", "cores": best["threads"],
+            "kind": "port", "windows_per_s": best["windows_per_s"], **share,
             "per_setting": {k: dict(v, variants_per_s=v["windows_per_s"] / windows_per_variant)
                             for k, v in runs.items()},
             "sample": f"seeded SNV ref windows of the headline workload; oracle/beluga_np.forward_torch_cpu "
-                      f"(torch CPU fp32, oneDNN) at 16 and 8 threads x batch 32 and 512, ~{seconds:.0f} s each; "
-                      f"value = best 16-thread setting ({b16}) / {windows_per_variant} windows per variant"}
+                      f"(torch CPU fp32, oneDNN) at P = {share['share']} (this job's CPU share: affinity "
+                      f"{share['affinity_cpus']}, cgroup quota {share['cgroup_cpus']}) and 8 threads x batch 32 "
+                      f"and 512, ~{seconds:.0f} s each; value = best setting ({best_k}) / {windows_per_variant} "
+                      f"windows per variant"}
 
 
 # ---- HBM-bound reductions -----------------------------------------------------------------

@@ -44,3 +44,13 @@ def test_committed_sq_counters_give_the_held_clock():
     held = bench.pmc_held_clock(key, bench.kernel_name("conv2", "f16x3"))
     assert held is not None, "re-take profiles: tools/profile_round.sh + collect_profiles.py"
     assert 0.3 < held["mfma_busy"] <= 1.0 and 1.0 < held["held_clock_ghz"] < 2.6
+
+
+def test_cpu_baseline_share_is_this_jobs_cpus():
+    """cpu_baseline's P is the job's CPU share (affinity mask, cgroup quota), not os.cpu_count()
+    of the whole machine."""
+    import bench
+    s = bench.host_cpu_share()
+    assert 1 <= s["share"] <= s["affinity_cpus"] <= (os.cpu_count() or s["affinity_cpus"])
+    if s["cgroup_cpus"] is not None:
+        assert s["share"] <= max(1, int(-(-s["cgroup_cpus"] // 1)))
