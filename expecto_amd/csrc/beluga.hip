@@ -791,17 +791,35 @@ __global__ void act_max(const float* __restrict__ A, long long groups, int s_row
   if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
 }
 
-// seeded random A/G/C/T codes (calibration windows)
-__global__ void random_codes(uint8_t* __restrict__ codes, long long n, unsigned seed) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  unsigned x = (unsigned)i * 2654435761u ^ seed;
+__device__ __forceinline__ unsigned mix32(unsigned x) {
   x ^= x >> 16;
   x *= 0x7feb352du;
   x ^= x >> 15;
   x *= 0x846ca68bu;
   x ^= x >> 16;
-  codes[i] = (uint8_t)(x & 3u);
+  return x;
+}
+
+// Seeded calibration windows (A/G/C/T codes), a mix of what real genomes hold: half i.i.d.
+// random windows, a quarter low-complexity tandem repeats (per 256-bp stretch one motif of
+// period 1-6 repeated: homopolymer runs, (CA)n, (CAG)n, (GGGGCC)n-like), a quarter tandem copies
+// of a block of 64-320 bp.  Repeats make every filter that matches the repeat fire at every
+// position of a window, which random windows never do, so the f16x3 scales cover them too.
+__global__ void calib_codes(uint8_t* __restrict__ codes, long long n, unsigned seed) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const unsigned w = (unsigned)(i / 2000), p = (unsigned)(i % 2000);
+  const unsigned kind = mix32(w * 0x9e3779b9u ^ seed) & 3u;
+  unsigned src = (unsigned)i;
+  if (kind == 2) {                 // tandem repeat of a short motif, a new motif every 256 bp
+    const unsigned h = mix32((w << 4 | (p >> 8)) * 0x85ebca6bu ^ seed);
+    const unsigned period = 1 + h % 6;
+    src = w * 2000u + (p >> 8) * 256u + (p % period);
+  } else if (kind == 3) {          // tandem copies of one block
+    const unsigned len = 64 + mix32(w ^ seed ^ 0xabcdu) % 257;
+    src = w * 2000u + p % len;
+  }
+  codes[i] = (uint8_t)(mix32(src * 2654435761u ^ seed) & 3u);
 }
 
 }  // namespace expecto
@@ -1791,8 +1809,8 @@ int f16_calibrate(expecto_beluga* h, hipStream_t st) {
   unsigned* amax = reinterpret_cast<unsigned*>(buf + (size_t)nb * kNFeat + (size_t)nb * kLen / 4);
   EXPECTO_HIP_CHECK(hipMemsetAsync(amax, 0, 8 * sizeof(unsigned), st));
   const long long nc = (long long)nb * kLen;
-  random_codes<<<dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st>>>(codes, nc, 0x5eed1234u);
-  if ((rc = check_launch("random_codes"))) return rc;
+  calib_codes<<<dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st>>>(codes, nc, 0x5eed1234u);
+  if ((rc = check_launch("calib_codes"))) return rc;
   const int saved = g_precision;
   const bool prof = h->profiling;
   h->profiling = false;

@@ -49,6 +49,9 @@ class VariantSet:
     def __len__(self):
         return len(self.chrom)
 
+    def slice(self, a: int, b: int) -> "VariantSet":
+        return VariantSet(self.chrom[a:b], self.pos[a:b], self.ref[a:b], self.alt[a:b])
+
 
 def fetch_window(fasta, chrom, pos, ref, allele, shift, inputsize=2000) -> str:
     """fetchSeqs for one allele (chromatin.py:202-209)."""
@@ -323,6 +326,41 @@ class VariantPipeline:
                                       out=yi.view(4 * S * ni, 2002))
             out.index_copy_(3, prep["ind_idx"], yi)
         return out
+
+    def recompute_overflowed(self, vs: VariantSet, shifts, out: torch.Tensor, rows: str = "shift",
+                             parts: int = 8) -> int:
+        """Release-point recovery of a batch whose deferred f16x3 overflow flag fired (the engine
+        in deferred mode, ``overflow_take``): instead of recomputing the whole batch in bf16x6,
+        rerun it in f16x3 as `parts` variant slices with one flag each -- an output row depends
+        only on its own window, so the rerun reproduces the batch's bits and only locates the
+        overflow -- then recompute just the flagged slices in bf16x6 into `out`.  Cost 1 + 2f
+        batch-times for a flagged fraction f, against 2 for the whole batch.  Returns the number
+        of slices recomputed (each counted by the engine's fallback counter)."""
+        eng = self.engine
+        n = len(vs)
+        if n == 0:
+            return 0
+        bounds = np.unique(np.linspace(0, n, min(parts, n) + 1).round().astype(int))
+        k = len(bounds) - 1
+        flags = torch.zeros(k, dtype=torch.int32).pin_memory()
+        preps = []
+        for i in range(k):
+            prep = self.prepare(vs.slice(int(bounds[i]), int(bounds[i + 1])), shifts, rows)
+            preps.append(prep)
+            self.predict(prep)
+            eng.overflow_take(flags[i:i + 1])
+        torch.cuda.current_stream().synchronize()
+        dim = 3 if rows == "shift" else 2
+        redone = 0
+        for i in range(k):
+            if not int(flags[i]):
+                continue
+            with eng.precision_override("bf16x6"):
+                y = self.predict(preps[i])
+            out.narrow(dim, int(bounds[i]), int(bounds[i + 1] - bounds[i])).copy_(y)
+            eng.count_fallback()
+            redone += 1
+        return redone
 
     def sed_features(self, y: torch.Tensor, weights: torch.Tensor, out: torch.Tensor | None = None,
                      legacy: bool = True) -> torch.Tensor:

@@ -3,7 +3,10 @@
 There is no network for hg19 or the real VCFs, so benchmarks and tests use:
 
 * a genome of ``n_contigs`` contigs named ``chr1..``: i.i.d. A/C/G/T with 10 %
-  lowercase and 1 % N (``numpy.random.default_rng(seed)``);
+  lowercase and 1 % N (``numpy.random.default_rng(seed)``), optionally repeat-rich
+  (``repeats=True``: about half the sequence in hg19-like low-complexity elements --
+  homopolymer runs, di/tri/hexa-nucleotide tandem repeats, tandem copies of 300-bp blocks,
+  copies of an interspersed ~300-bp family consensus, long N gaps -- soft-masked);
 * biallelic SNVs uniform in ``[margin, len - margin]`` with ref = the genome base
   (upper case) and alt uniform over the other three bases;
 * variant->TSS distances uniform over [-20000, 20000] and a random strand.
@@ -15,7 +18,7 @@ import numpy as np
 _BASES = np.frombuffer(b"ACGT", np.uint8)
 
 
-def genome_bytes(n_contigs: int = 24, contig_len: int = 2_000_000, seed: int = 0) -> dict:
+def genome_bytes(n_contigs: int = 24, contig_len: int = 2_000_000, seed: int = 0, repeats: bool = False) -> dict:
     """name -> bytes of the contig sequence (ASCII)."""
     rng = np.random.default_rng(seed)
     out = {}
@@ -25,8 +28,46 @@ def genome_bytes(n_contigs: int = 24, contig_len: int = 2_000_000, seed: int = 0
         s = np.where(low, s + 32, s).astype(np.uint8)            # lowercase
         nmask = rng.random(contig_len) < 0.01
         s = np.where(nmask, np.uint8(ord("N")), s).astype(np.uint8)
+        if repeats:
+            add_repeats(s, np.random.default_rng([seed, i, 1]))
         out[f"chr{i + 1}"] = s.tobytes()
     return out
+
+
+_MOTIFS = [b"A", b"T", b"G", b"C", b"CA", b"TG", b"AT", b"GC", b"CAG", b"CGG", b"GAA", b"CTG", b"GGGGCC", b"TTAGGG"]
+
+
+def add_repeats(s: np.ndarray, rng, cover: float = 0.5, gap_every: int = 1_000_000) -> np.ndarray:
+    """Overwrite about `cover` of the uint8 ASCII sequence `s` in place with low-complexity
+    elements (hg19 is ~50 % repeats): homopolymer runs (10-300 bp), di/tri/hexa-nucleotide
+    tandem repeats (20-900 bp), 2-5 tandem copies of a 300-bp block of the sequence itself,
+    copies of one seeded ~300-bp interspersed family consensus with 10 % point changes, all
+    soft-masked (lowercase); plus one N gap (1-20 kb) per `gap_every` bases."""
+    n = s.size
+    family = _BASES[rng.integers(0, 4, 300)]
+    done = 0
+    while done < cover * n:
+        kind = rng.integers(0, 4)
+        p = int(rng.integers(0, n))
+        if kind == 0:                                   # tandem repeat of a short motif
+            m = np.frombuffer(_MOTIFS[int(rng.integers(0, len(_MOTIFS)))], np.uint8)
+            ln = int(rng.integers(10, 300)) if m.size == 1 else int(rng.integers(20, 900))
+            el = np.resize(m, ln)
+        elif kind == 1:                                 # tandem copies of a 300-bp block
+            blk = s[p:p + 300].copy()
+            el = np.tile(blk, int(rng.integers(2, 6)))
+        else:                                           # interspersed family copy (Alu-like)
+            el = family.copy()
+            mut = rng.random(el.size) < 0.10
+            el[mut] = _BASES[rng.integers(0, 4, int(mut.sum()))]
+            el = el[:int(rng.integers(150, 301))]
+        el = el[:max(0, n - p)]
+        s[p:p + el.size] = np.where(np.isin(el, _BASES), el + 32, el)    # soft-masked
+        done += el.size
+    for g in range(max(1, n // gap_every)):
+        p, ln = int(rng.integers(0, n)), int(rng.integers(1000, 20000))
+        s[p:p + ln] = ord("N")
+    return s
 
 
 def write_fasta(path: str, genome: dict, width: int = 60) -> None:

@@ -32,7 +32,7 @@ def test_reported_kernel_names_exist_in_the_committed_kernel_trace():
 
 def test_committed_traffic_matches_the_default_workload_key():
     import bench
-    key = {"workload": "sed200", "variants": bench.N200, "precision": "f16x3", "max_batch": bench.MAX_BATCH}
+    key = bench.profile_key()
     traffic, src = bench.pmc_traffic(key, bench.kernel_name("conv2", "f16x3"))
     assert traffic is not None and traffic > 0, "re-take profiles: tools/profile_round.sh + collect_profiles.py"
     assert src.startswith("profiles/")
@@ -40,7 +40,7 @@ def test_committed_traffic_matches_the_default_workload_key():
 
 def test_committed_sq_counters_give_the_held_clock():
     import bench
-    key = {"workload": "sed200", "variants": bench.N200, "precision": "f16x3", "max_batch": bench.MAX_BATCH}
+    key = bench.profile_key()
     held = bench.pmc_held_clock(key, bench.kernel_name("conv2", "f16x3"))
     assert held is not None, "re-take profiles: tools/profile_round.sh + collect_profiles.py"
     assert 0.3 < held["mfma_busy"] <= 1.0 and 1.0 < held["held_clock_ghz"] < 2.6

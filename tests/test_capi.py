@@ -91,3 +91,16 @@ def test_production_forward_has_no_host_sync():
             assert bad not in body, (fn, bad)
     rc = _function_body(src, "run_checked")
     assert rc.index("h->ovf_deferred") < rc.index("hipStreamSynchronize")
+
+
+def test_product_gemm_header_holds_only_launched_kernels():
+    """Every __global__ kernel of the library's GEMM header is launched by the library; the
+    probe-only shapes live in tools/gemm_probes.h."""
+    import re
+    csrc = os.path.join(REPO, "expecto_amd", "csrc")
+    hdr = open(os.path.join(csrc, "gemm_kernel.h")).read()
+    lib = open(os.path.join(csrc, "beluga.hip")).read() + open(os.path.join(csrc, "reduce.hip")).read()
+    kernels = re.findall(r"__global__\s+(?:__launch_bounds__\([^)]*\)\s+)?void\s+(\w+)", hdr)
+    assert kernels
+    for k in kernels:
+        assert re.search(rf"\b{k}\s*(<[^;]*?>)?\s*<<<", lib), f"{k} is declared in gemm_kernel.h but never launched"

@@ -1,4 +1,6 @@
-// A/B micro-benchmark of beluga_gemm variants on the conv2 / conv4 / fc1 shapes (gfx950).
+// A/B micro-benchmark of beluga_gemm variants on the conv2 / conv4 / fc1 shapes (gfx950):
+// the library's kernels (expecto_amd/csrc/gemm_kernel.h) against the probe-only ones
+// (tools/gemm_probes.h) and their timing probes (TM bits, wrong results).
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/gemm_bench.hip -o tools/gemm_bench
 // Run:   tools/gemm_bench [windows=1000] [rounds=5]
 // Interleaved rounds in one process (cdna_hip_programming.md rule 24); outputs of every
@@ -16,7 +18,7 @@
 #include <string>
 #include <vector>
 
-#include "../expecto_amd/csrc/gemm_kernel.h"
+#include "gemm_probes.h"   // the library's kernel header + the probe-only kernels
 
 using namespace expecto;
 
@@ -248,14 +250,11 @@ int main(int argc, char** argv) {
     vs.push_back(mk6q<2, EPI_RELU_POOL4>("x6q"));
     vs.push_back(mkc3<2, EPI_RELU_POOL4>("h3c"));
     vs.push_back(mkr3<2, EPI_RELU_POOL4>("h3r"));
-    vs.push_back(mkr3<2, EPI_RELU_POOL4, 512>("h3r_oldswz"));
     vs.push_back(mks3<2, EPI_RELU_POOL4, 4, 0>("h3s4"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4>("h3p"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 256, 4>("h3p4_pf"));
-    vs.push_back(mkp3<2, EPI_RELU_POOL4, 256 | 512, 4>("h3p4_pf_oldswz"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 0, 4>("h3p4"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 256 | 2048, 4>("h3p4_pf_noepi"));
-    vs.push_back(mkp3<2, EPI_RELU_POOL4, 256 | 4096, 4>("h3p4_pf_oldovf"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 2>("h3p_noglds"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 8>("h3p_hotAB"));
     vs.push_back(mks3<2, EPI_RELU_POOL4, 6, 0>("h3s6"));
@@ -268,19 +267,11 @@ int main(int argc, char** argv) {
     vs.push_back(mk6q<3, EPI_RELU>("x6q"));
     vs.push_back(mkc3<3, EPI_RELU>("h3c"));
     vs.push_back(mkr3<3, EPI_RELU>("h3r"));
-    vs.push_back(mkr3<3, EPI_RELU, 512>("h3r_oldswz"));
     vs.push_back(mks3<3, EPI_RELU, 4, 0>("h3s4"));
     vs.push_back(mkp3<3, EPI_RELU>("h3p"));
     vs.push_back(mkp3<3, EPI_RELU, 256, 4>("h3p4_pf"));
-    vs.push_back(mkp3<3, EPI_RELU, 256 | 512, 4>("h3p4_pf_oldswz"));
     vs.push_back(mkp3<3, EPI_RELU, 0, 4>("h3p4"));
     vs.push_back(mkp3<3, EPI_RELU, 256 | 2048, 4>("h3p4_pf_noepi"));
-    vs.push_back(mkp3<3, EPI_RELU, 256 | 4096, 4>("h3p4_pf_oldovf"));
-    vs.push_back(mkp3<3, EPI_RELU, 256 | 8192, 4>("h3p4_pf_nostore"));
-    vs.push_back(mkp3<3, EPI_RELU, 256 | 16384, 4>("h3p4_pf_nosplit"));
-    vs.push_back(mkp3<3, EPI_RELU, 256 | 8192 | 16384, 4>("h3p4_pf_nostore_nosplit"));
-    vs.push_back(mkp3<3, EPI_RELU, 256 | 32768, 4>("h3p4_pf_ntstore"));
-    vs.push_back(mkp3<3, EPI_RELU, 256 | 65536, 4>("h3p4_pf_canon"));
     vs.push_back(mks3<3, EPI_RELU, 6, 0>("h3s6"));
   }
   auto args_for = [&](int bm, float* C) {
