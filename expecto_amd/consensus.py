@@ -1,9 +1,13 @@
 """Personal-genome / eQTL 200-shift scoring on the GPU: drop-ins for the reference
-``geuvadis_sed_for_top_eqtls.py`` and ``geuvadis_predict_consensus.py`` CLIs (SURVEY.md §8f
-row 2).
+``geuvadis_sed_for_top_eqtls.py``, ``geuvadis_predict_consensus.py``,
+``geuvadis_predict_ref_all_genes.py``, ``geuvadis_predict_consensus_for_top_eqtls.py`` and
+``merge_geuvadis_predict_consensus.py`` CLIs:
 
-Both score 393,216-bp consensus sequences (Enformer length) whose TSS sits at index
-``len(seq) // 2``: 200 Beluga windows at ``tss + shift*strand`` for
+    python -m expecto_amd.consensus {sed|consensus|ref_all_genes|top_eqtls|merge} ...
+
+They score consensus sequences -- 393,216-bp Enformer records whose TSS sits at index
+``len(seq) // 2``, or (top_eqtls) Basenji records with the TSS at ``(len - 1) // 2`` on + and
+``len // 2`` on - -- with 200 Beluga windows at ``tss + shift*strand`` for
 ``shift in range(-20000, 20000, 200)`` (``get_seq_shifts_for_sample_seq``), each on the window
 and its reverse complement (``encodeSeqs``), fwd/rc averaged in float64, reduced with the
 10 exp-decay position weights, written in the legacy 20030-feature layout (a zero column
@@ -43,9 +47,11 @@ REDUCE_F64AVG, REDUCE_LEGACY20030 = 1, 2
 
 # ---- FASTA (Bio.SeqIO 'fasta' subset) -------------------------------------------------------
 def parse_fasta(path: str):
-    """(id, sequence) per record: id = first word of the header, sequence lines joined."""
+    """(id, sequence) per record: id = first word of the header, sequence lines joined
+    (``.gz`` paths are read through gzip, as the reference's ``gzip.open(..., 'rt')``)."""
+    import gzip
     rid, parts = None, []
-    with open(path) as f:
+    with (gzip.open(path, "rt") if str(path).endswith(".gz") else open(path)) as f:
         for line in f:
             if line.startswith(">"):
                 if rid is not None:
@@ -100,9 +106,11 @@ class ConsensusScorer:
         self.lib = _lib.load()
         self.w_d = torch.from_numpy(tss_pos_weights(self.shifts)).to(self.dev)
 
-    def _geometry(self, seq_len: int, strand: int):
-        """Segment start (index into the sequence) and per-window offsets inside it."""
-        tss_i = seq_len // 2
+    def _geometry(self, seq_len: int, strand: int, tss_i: int | None = None):
+        """Segment start (index into the sequence) and per-window offsets inside it (TSS at
+        tss_i, default len // 2)."""
+        if tss_i is None:
+            tss_i = seq_len // 2
         starts = tss_i + self.shifts * strand - (WINDOW // 2 - 1)      # get_seq_shifts_for_sample_seq
         lo = int(starts.min())
         L = int(starts.max()) - lo + WINDOW
@@ -111,21 +119,21 @@ class ConsensusScorer:
             raise AssertionError(f"Expected seq of length f{WINDOW} but got a window outside the sequence")
         return lo, L, (starts - lo).astype(np.int32)
 
-    def _segments(self, seqs, strands):
-        geo = [self._geometry(len(s), st) for s, st in zip(seqs, strands)]
+    def _segments(self, seqs, strands, tss=None):
+        geo = [self._geometry(len(s), st, None if tss is None else tss[i]) for i, (s, st) in enumerate(zip(seqs, strands))]
         L = max(g[1] for g in geo)
         codes = np.full((len(seqs), L), 4, np.uint8)
         for i, (s, (lo, Li, _)) in enumerate(zip(seqs, geo)):
             codes[i, :Li] = seq_codes(s[lo:lo + Li], Li)
         return geo, L, torch.from_numpy(codes).to(self.dev)
 
-    def predict(self, seqs, strands) -> torch.Tensor:
-        """[2 (fwd, rc), n, S, 2002] fp32 window predictions."""
+    def predict(self, seqs, strands, tss=None) -> torch.Tensor:
+        """[2 (fwd, rc), n, S, 2002] fp32 window predictions (TSS indices `tss`, default len // 2)."""
         n, S = len(seqs), len(self.shifts)
         y = torch.empty((2, n, S, 2002), dtype=torch.float32, device=self.dev)
         if n == 0:
             return y
-        geo, L, codes = self._segments(seqs, strands)
+        geo, L, codes = self._segments(seqs, strands, tss)
         win_seg = np.repeat(np.arange(n, dtype=np.int32), S)
         win_off = np.concatenate([g[2] for g in geo])
         self.engine.forward_segments(codes, L, win_seg, win_off, None, _lib.STRAND_BOTH, out=y.view(2 * n * S, 2002))
@@ -345,6 +353,174 @@ def consensus_main(argv=None):
         h5.write(f'{preds_dir}/{gene}.h5', {'expecto_preds': expecto_preds, 'record_ids': ids})
 
 
+# ---- geuvadis_predict_ref_all_genes.py ----------------------------------------------------
+def ref_all_genes_main(argv=None, capture: dict | None = None):
+    """geuvadis_predict_ref_all_genes.py main() (:23-101): the reference-genome consensus
+    ``{consensus_dir}/{gene}/ref.fa`` of every gene in the genes table (gene symbol, else the
+    Ensembl id), 200 shifts x fwd/rc on the segment path, float64 fwd/rc mean, legacy 20030
+    features, gblinear score; writes ``ref_preds.csv`` (columns genes, ref_preds).  ``capture``
+    (tests) receives the window predictions and features per batch."""
+    p = argparse.ArgumentParser(description='Predict expression for consensus sequences using ExPecto')
+    p.add_argument('expecto_model')
+    p.add_argument('consensus_dir')
+    p.add_argument('genes_file')
+    p.add_argument('--beluga_model', type=str, default='./resources/deepsea.beluga.pth')
+    p.add_argument('--batch_size', action="store", dest="batch_size", type=int, default=1024,
+                   help="Batch size for neural network predictions.")
+    p.add_argument('-o', dest="out_dir", type=str, default='temp_sed_for_top_eqtls', help='Output directory')
+    _extra_args(p)
+    args = p.parse_args(argv)
+    os.makedirs(args.out_dir, exist_ok=True)
+    model = _load_beluga(args)
+    bst = GBLinear.load(args.expecto_model.strip())
+    genes_df = pd.read_csv(args.genes_file, names=['ens_id', 'chrom', 'bp', 'gene_symbol', 'strand'], index_col=False)
+    genes_df['gene_symbol'] = genes_df['gene_symbol'].fillna(genes_df['ens_id'])
+    genes_df = genes_df.set_index('gene_symbol')
+    scorer = ConsensusScorer(model.engine())
+    preds, batch = [], []
+
+    def flush():
+        if not batch:
+            return
+        y = scorer.predict([b[0] for b in batch], [b[1] for b in batch])
+        x = scorer.features(y)
+        preds.extend(bst.predict(x).cpu().numpy()[:, None])     # one (1,) array per gene, as the reference
+        if capture is not None:
+            capture.setdefault("y", []).append(y.cpu().numpy())
+            capture.setdefault("x", []).append(x.cpu().numpy())
+        batch.clear()
+
+    for gene in genes_df.index:
+        strand = genes_df.loc[gene, 'strand']
+        _, seq = read_one_consensus(f'{args.consensus_dir}/{gene.lower()}/ref.fa')
+        batch.append((seq, _strand_sign(strand)))
+        if len(batch) >= args.seq_batch:
+            flush()
+    flush()
+    expecto_ref_preds = np.array(preds).squeeze()
+    df = pd.DataFrame({"genes": np.array(genes_df.index.values), "ref_preds": expecto_ref_preds})
+    df.to_csv(f'{args.out_dir}/ref_preds.csv', header=True, index=False)
+    return df
+
+
+# ---- geuvadis_predict_consensus_for_top_eqtls.py -------------------------------------------
+TOP_EQTL_GENES = ['HLA-B', 'HLA-C', 'RPL28', 'CPAMD8', 'TMEM121B', 'SCN11A']   # the script's list (:72-73)
+
+
+def top_eqtl_tss(seq_len: int, strand: str) -> int:
+    """TSS index of a Basenji consensus record (get_seq_shifts_for_sample_seq, :160-168)."""
+    return (seq_len - 1) // 2 if strand == '+' else seq_len // 2
+
+
+def sample_seq_for_expecto(seq: str, strand: str, shifts=SHIFTS, windowsize: int = WINDOW) -> str:
+    """get_sample_seq_for_expecto (:143-152): the 41,800-bp span the 200 windows cover."""
+    sign = _strand_sign(strand)
+    tss_i = top_eqtl_tss(len(seq), strand)
+    c = tss_i + np.asarray(shifts) * sign
+    out = seq[min(c - int(windowsize / 2 - 1)):max(c + int(windowsize / 2) + 1)]
+    assert len(out) == 41800, "length of sequence should be 41800 to match ExPecto receptive field"
+    return out
+
+
+def top_eqtls_main(argv=None, capture: dict | None = None):
+    """geuvadis_predict_consensus_for_top_eqtls.py main() (:23-128): for each gene of the
+    script's list, every record of ``{consensus_dir}/{gene}/{gene}.fa.gz`` (upper-cased; the
+    strand is the id's second-to-last '|' field) through 200 shifts x fwd/rc, float64 mean,
+    legacy 20030 features, gblinear score -> ``{out}/{gene}/{gene}.h5`` with ``preds``,
+    ``record_ids`` and the 41,800-bp ``seqs``.  The eQTL table and VCF are read and joined as
+    the script does (the join is validated m:1, its result otherwise unused).
+    Deviation: the script builds the legacy feature layout with np.zeros((1, 10, 1)), which
+    only concatenates for files of ONE record (numpy raises for more); here every record gets
+    its zero column (geuvadis_predict_consensus.py's corrected form, same values for one record).
+    ``--genes`` (extra) replaces the fixed list."""
+    p = argparse.ArgumentParser(description='Predict expression for consensus sequences using ExPecto')
+    p.add_argument('expecto_model')
+    p.add_argument('consensus_dir')
+    p.add_argument('eqtls_df_file')
+    p.add_argument('snps_vcf')
+    p.add_argument('--beluga_model', type=str, default='./resources/deepsea.beluga.pth')
+    p.add_argument('--batch_size', action="store", dest="batch_size", type=int, default=1024,
+                   help="Batch size for neural network predictions.")
+    p.add_argument('-o', dest="out_dir", type=str, default='temp_predict_consensus', help='Output directory')
+    p.add_argument('--genes', type=str, default=None, help="comma-separated genes (default: the script's six)")
+    _extra_args(p)
+    args = p.parse_args(argv)
+    os.makedirs(args.out_dir, exist_ok=True)
+    model = _load_beluga(args)
+    bst = GBLinear.load(args.expecto_model.strip())
+    eur = pd.read_csv(args.eqtls_df_file)
+    eur['gene_symbol'] = eur['name'].fillna(eur['geneID'])
+    eur['SNPpos'] = eur['SNPpos'].astype(int).astype(str)
+    eur = eur.set_index('chr' + eur['CHR_SNP'].astype(str) + '_' + eur['SNPpos'])
+    vcf_df = pd.read_csv(args.snps_vcf, sep='\t', comment='#', header=None).iloc[:, 0:5]
+    vcf_df.columns = ['SNP_CHROM', 'SNP_POS', 'ID', 'REF', 'ALT']
+    vcf_df.index = vcf_df.iloc[:, 0] + '_' + vcf_df.iloc[:, 1].astype(str)
+    vcf_df = vcf_df.drop_duplicates()
+    eur.merge(vcf_df, left_index=True, right_index=True, validate='m:1', how='inner')
+    genes = args.genes.split(",") if args.genes else TOP_EQTL_GENES
+    scorer = ConsensusScorer(model.engine())
+    print("Predicting chromatin for all samples for all genes...")
+    for gene in genes:
+        gene = gene.lower()
+        preds_dir = f'{args.out_dir}/{gene}'
+        os.makedirs(preds_dir, exist_ok=True)
+        ids, seqs, strands = [], [], []
+        for rid, seq in parse_fasta(f'{args.consensus_dir}/{gene}/{gene}.fa.gz'):
+            ids.append(rid)
+            seqs.append(seq.upper())
+            strands.append(rid.split('|')[-2])
+        sample_seqs = [sample_seq_for_expecto(s, st) for s, st in zip(seqs, strands)]
+        feats = []
+        for b0 in range(0, len(seqs), args.seq_batch):
+            sl = slice(b0, b0 + args.seq_batch)
+            y = scorer.predict(seqs[sl], [_strand_sign(st) for st in strands[sl]],
+                               [top_eqtl_tss(len(s), st) for s, st in zip(seqs[sl], strands[sl])])
+            feats.append(scorer.features(y))
+            if capture is not None:
+                capture.setdefault("y", []).append(y.cpu().numpy())
+        x = torch.cat(feats) if feats else torch.empty((0, 20030), dtype=torch.float64, device=scorer.dev)
+        if capture is not None:
+            capture.setdefault("x", []).append(x.cpu().numpy())
+        expecto_preds = bst.predict(x).cpu().numpy()
+        h5.write(f'{preds_dir}/{gene}.h5', {'preds': expecto_preds, 'record_ids': np.array(ids, 'S'),
+                                             'seqs': np.array(sample_seqs, 'S')})
+
+
+# ---- merge_geuvadis_predict_consensus.py ---------------------------------------------------
+def parse_record_id(x: bytes) -> str:
+    """b'chr19:58832097-58897632|NA20828|-|1pIu' -> 'NA20828|1pIu' (:48-55)."""
+    x = x.decode("utf-8").split("|")
+    return f"{x[1]}|{x[3]}"
+
+
+def merge_main(argv=None):
+    """merge_geuvadis_predict_consensus.py main() (:12-45): stack the per-gene ``preds`` of
+    ``{batch_dir}/*/*.h5`` (natsorted; every file must carry the same samples) into
+    ``{out}/expecto_preds.h5`` with ``record_ids``, ``genes`` (file stems) and ``preds``.
+    Host only: no device work."""
+    p = argparse.ArgumentParser(description='Merge output batches of geuvadis_predict_consensus.py')
+    p.add_argument("--batch_dir", dest="batch_dir", type=str)
+    p.add_argument("--n_genes", dest="n_genes", type=int, default=3259, help="Expected number of genes")
+    p.add_argument('-o', dest="out_dir", type=str, default='merge_geuvadis_predict_consensus', help='Output directory')
+    args = p.parse_args(argv)
+    os.makedirs(args.out_dir, exist_ok=True)
+    h5_files = natsorted(glob.glob(f"{args.batch_dir}/*/*.h5"))
+    assert len(h5_files) == args.n_genes, f"Expected {args.n_genes} genes but got {len(h5_files)} h5 files"
+    record_ids, preds = None, []
+    for f in h5_files:
+        d = h5.read(f)
+        cur = np.array([parse_record_id(x) for x in d["record_ids"]])
+        if record_ids is None:
+            record_ids = cur
+        else:
+            assert (record_ids == cur).all()
+        preds.append(np.array(d["preds"]))
+    preds = np.stack(preds)
+    genes = [Path(x).stem for x in h5_files]
+    h5.write(f"{args.out_dir}/expecto_preds.h5", {"record_ids": np.array(record_ids, 'S'),
+                                                  "genes": np.array(genes, 'S'), "preds": preds})
+
+
 def _legacy_features_f64(preds: torch.Tensor, w_d: torch.Tensor) -> torch.Tensor:
     """--exp_only: features from stored float64 averaged predictions [n, S, F] (shifts summed in order)."""
     n, S, F = preds.shape
@@ -356,9 +532,12 @@ def _legacy_features_f64(preds: torch.Tensor, w_d: torch.Tensor) -> torch.Tensor
     return out.reshape(n, -1)
 
 
+COMMANDS = {"sed": sed_main, "consensus": consensus_main, "ref_all_genes": ref_all_genes_main,
+            "top_eqtls": top_eqtls_main, "merge": merge_main}
+
 if __name__ == "__main__":
     import sys
-    if len(sys.argv) > 1 and sys.argv[1] in ("sed", "consensus"):
-        (sed_main if sys.argv[1] == "sed" else consensus_main)(sys.argv[2:])
+    if len(sys.argv) > 1 and sys.argv[1] in COMMANDS:
+        COMMANDS[sys.argv[1]](sys.argv[2:])
     else:
-        raise SystemExit("usage: python -m expecto_amd.consensus {sed|consensus} ...")
+        raise SystemExit(f"usage: python -m expecto_amd.consensus {{{'|'.join(COMMANDS)}}} ...")

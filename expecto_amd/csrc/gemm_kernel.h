@@ -50,6 +50,7 @@ struct GemmArgs {
   int* ovf;                 // f16x3: set to 1 when a stored activation does not fit fp16
   const unsigned* ks_mask;  // split-K planes GEMM: bit ks of ks_mask[m_tile] = compute that slab
                             // (others keep the partials already in C: alt FC1 of SNV pairs)
+  int m_group;              // FC m_fastest 3: M tiles per dispatch group (see gemm_fc_h3p_body)
 };
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -780,6 +781,20 @@ __device__ __forceinline__ void gemm_fc_h3p_body(const GemmArgs& p, char* smem) 
     const unsigned j = (unsigned)((bid - ks * per_ks) >> 3);
     mt = (long long)(j / (unsigned)p.n_tiles) * 8 + (bid & 7u);
     nt = (int)(j % (unsigned)p.n_tiles);
+  } else if (p.m_fastest == 3) {
+    // grouped: per split-K slab, groups of m_group M tiles; inside a group N tiles outer and M
+    // tiles inner, so the ~32 workgroups an XCD runs at once (the XCD remap keeps lin
+    // contiguous per XCD) cover ~m_group M tiles x 32/m_group N tiles: a weight tile is read
+    // by m_group concurrent M tiles instead of ~2.5 (N tiles fastest), an activation tile by
+    // 32/m_group N tiles instead of all 13
+    const long long per_ks = p.m_tiles * p.n_tiles;
+    ks = (int)(lin / per_ks);
+    const long long r = lin - ks * per_ks;
+    const long long g = r / ((long long)p.m_group * p.n_tiles);
+    const int i = (int)(r - g * p.m_group * p.n_tiles);
+    const int gm = (int)min((long long)p.m_group, p.m_tiles - g * p.m_group);
+    nt = i / gm;
+    mt = g * p.m_group + i % gm;
   } else if (p.m_fastest) {
     mt = lin % p.m_tiles;
     const long long rest = lin / p.m_tiles;

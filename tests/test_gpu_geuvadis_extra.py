@@ -1,0 +1,99 @@
+"""GPU: the remaining geuvadis CLIs of expecto_amd.consensus against the reference scripts run
+on the same seeded inputs (tests/golden/make_golden_geuvadis_extra.py; inputs regenerated here):
+
+* ``ref_all_genes`` vs geuvadis_predict_ref_all_genes.py (:23-101): per-window 200-shift
+  predictions (captured reference Beluga forwards: every 8th window, every 5th feature, full-row
+  sums) and the 20030 features at the parity bar, ``ref_preds.csv`` scores within the bound
+  test_gpu_consensus._score_bound derives, our scoring bit for bit the restated GBLinear::Pred.
+* ``top_eqtls`` vs geuvadis_predict_consensus_for_top_eqtls.py (:23-128): the same for its
+  six genes, plus ``record_ids``, the 41,800-bp ``seqs`` (SHA-1 equal) and the stdout line.
+* ``merge`` over our top_eqtls outputs vs merge_geuvadis_predict_consensus.py over the
+  reference's: record ids and genes equal, scores within the same bound.
+"""
+import hashlib
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, assert_close
+
+pytestmark = pytest.mark.gpu
+sys.path.insert(0, GOLDEN)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def inputs(tmp_path_factory):
+    import make_golden_geuvadis_extra as mg
+    d = tmp_path_factory.mktemp("geuv")
+    return d, mg.write_inputs(str(d)), mg
+
+
+def _check_windows(y, gold, key, gi):
+    win = y.reshape(400, 2002)                                    # 200 fwd then 200 rc, as encodeSeqs
+    assert_close(win[::8, ::5], gold[f"{key}_win_{gi}"], what=f"{key} {gi} window predictions")
+    np.testing.assert_allclose(win.astype(np.float64).sum(1), gold[f"{key}_winsum_{gi}"], rtol=2e-6, atol=0,
+                               err_msg=f"{key} {gi} row sums")
+    return (win[:200].astype(np.float64) + win[200:]) / 2
+
+
+def test_ref_all_genes_matches_reference(inputs):
+    import pandas as pd
+    from expecto_amd import consensus
+    from expecto_amd.features import tss_pos_weights
+    from expecto_amd.xgblinear import GBLinear
+    from oracle.gblinear_np import predict as gblinear_ref
+    from test_gpu_consensus import _score_bound
+    d, p, mg = inputs
+    gold = np.load(os.path.join(GOLDEN, "geuvadis_extra.npz"))
+    cap = {}
+    out = d / "ref_out"
+    consensus.ref_all_genes_main([p["model"], p["ref_dir"], p["genes_csv"], "--synthetic-weights", "0", "-o",
+                                  str(out), "--seq-batch", "2"], capture=cap)
+    y = np.concatenate(cap["y"], axis=1)                          # [2, G, 200, 2002]
+    x = np.concatenate(cap["x"], axis=0)                          # [G, 20030]
+    got = pd.read_csv(out / "ref_preds.csv")
+    want = pd.read_csv(os.path.join(GOLDEN, "geuvadis_ref_preds.csv"))
+    assert list(got.columns) == ["genes", "ref_preds"] and list(got["genes"]) == list(want["genes"])
+    m = GBLinear.load(p["model"])
+    w = tss_pos_weights()
+    for gi in range(len(mg.REF_GENES)):
+        pbar = _check_windows(y[:, gi], gold, "ref", gi)
+        assert_close(x[gi, ::4], gold[f"ref_feat_{gi}"], what=f"ref {gi} features")
+        s = float(got["ref_preds"][gi])
+        assert np.float32(s) == gblinear_ref(x[gi][None], m.weights[:, 0], m.bias[0], m.base_score)[0]
+        assert abs(s - float(want["ref_preds"][gi])) <= _score_bound(m, x[gi], pbar, w), gi
+
+
+def test_top_eqtls_and_merge_match_reference(inputs, capsys):
+    from expecto_amd import consensus, h5
+    from expecto_amd.features import tss_pos_weights
+    from expecto_amd.xgblinear import GBLinear
+    from test_gpu_consensus import _score_bound
+    d, p, mg = inputs
+    gold = np.load(os.path.join(GOLDEN, "geuvadis_extra.npz"))
+    cap = {}
+    out = d / "top_out"
+    consensus.top_eqtls_main([p["model"], p["top_dir"], p["eqtls_csv"], p["vcf"], "--synthetic-weights", "0", "-o",
+                              str(out)], capture=cap)
+    assert capsys.readouterr().out == gold["top_stdout"].item().decode()
+    m = GBLinear.load(p["model"])
+    w = tss_pos_weights()
+    for gi, g in enumerate(mg.TOP_GENES):
+        gene = g.lower()
+        pbar = _check_windows(cap["y"][gi][:, 0], gold, "top", gi)
+        x = cap["x"][gi]
+        assert_close(x[0, ::4], gold[f"top_feat_{gi}"], what=f"top {gene} features")
+        r = h5.read(str(out / gene / f"{gene}.h5"))
+        assert list(r["record_ids"]) == list(gold[f"top_ids_{gi}"])
+        assert [hashlib.sha1(bytes(s)).hexdigest().encode() for s in r["seqs"]] == list(gold[f"top_seq_sha1_{gi}"])
+        assert r["preds"].dtype == np.float32 and r["preds"].shape == gold[f"top_preds_{gi}"].shape
+        assert abs(float(r["preds"][0]) - float(gold[f"top_preds_{gi}"][0])) <= _score_bound(m, x[0], pbar, w), gene
+    merged = d / "merged"
+    consensus.merge_main(["--batch_dir", str(out), "--n_genes", str(len(mg.TOP_GENES)), "-o", str(merged)])
+    r = h5.read(str(merged / "expecto_preds.h5"))
+    assert list(r["record_ids"]) == list(gold["merge_record_ids"]) and list(r["genes"]) == list(gold["merge_genes"])
+    assert r["preds"].shape == gold["merge_preds"].shape
+    np.testing.assert_allclose(r["preds"], gold["merge_preds"], rtol=0, atol=2e-3)

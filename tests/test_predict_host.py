@@ -111,3 +111,32 @@ def test_closest_genes_match_reference(tmp_path, rf):
         ext = "tsv" if name == "closest_genes" else "vcf"
         got = open(out / f"{name}.{ext}").read()
         assert got == open(os.path.join(GOLDEN, "extra", f"{name}{tag}.{ext}")).read(), name
+
+
+def test_merge_geuvadis_consensus_matches_reference(tmp_path):
+    """merge_geuvadis_predict_consensus.py (host only) on per-gene files holding the reference
+    for_top_eqtls outputs (tests/golden/geuvadis_extra.npz): the merged record ids, genes and
+    preds equal the reference merge's bit for bit; a sample mismatch between genes or a wrong
+    gene count fails as the script's asserts do."""
+    import os
+    import numpy as np
+    import pytest
+    from conftest import GOLDEN
+    from expecto_amd import consensus, h5
+    gold = np.load(os.path.join(GOLDEN, "geuvadis_extra.npz"))
+    genes = ['hla-b', 'hla-c', 'rpl28', 'cpamd8', 'tmem121b', 'scn11a']
+    for gi, g in enumerate(genes):
+        os.makedirs(tmp_path / "out" / g)
+        h5.write(str(tmp_path / "out" / g / f"{g}.h5"), {"preds": gold[f"top_preds_{gi}"],
+                                                         "record_ids": gold[f"top_ids_{gi}"],
+                                                         "seqs": np.array([b"ACGT"], "S")})
+    consensus.merge_main(["--batch_dir", str(tmp_path / "out"), "--n_genes", "6", "-o", str(tmp_path / "m")])
+    r = h5.read(str(tmp_path / "m" / "expecto_preds.h5"))
+    for k in ("record_ids", "genes", "preds"):
+        assert r[k].dtype == gold[f"merge_{k}"].dtype and np.array_equal(r[k], gold[f"merge_{k}"]), k
+    with pytest.raises(AssertionError):
+        consensus.merge_main(["--batch_dir", str(tmp_path / "out"), "--n_genes", "5", "-o", str(tmp_path / "m2")])
+    h5.write(str(tmp_path / "out" / "hla-b" / "hla-b.h5"), {"preds": gold["top_preds_0"],
+                                                            "record_ids": np.array([b"chr6:1-2|NA1|+|x"], "S")})
+    with pytest.raises(AssertionError):
+        consensus.merge_main(["--batch_dir", str(tmp_path / "out"), "--n_genes", "6", "-o", str(tmp_path / "m3")])

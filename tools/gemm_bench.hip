@@ -143,7 +143,11 @@ int fc1_bench(int nb, int rounds, int splits, bool toe) {
   // block orders: m = M tiles fastest in dispatch order, x = N tiles fastest per XCD (XCD-aware
   // remap; the library's order for large M).  Probes (wrong results): hotA / hotB / hotAB = that
   // operand's LDS-DMA always from K stage 0 (L2-hot), noload = no LDS-DMA in the loop.
+  // g<k>: grouped order (m_fastest 3) with k M tiles per group
   V vs[] = {{"fcp_m", fc1p_launch<0>}, {"fcp_x", fc1p_launch<0>},
+            {"fcp_g3", fc1p_launch<0>}, {"fcp_g4", fc1p_launch<0>}, {"fcp_g5", fc1p_launch<0>},
+            {"fcp_g6", fc1p_launch<0>}, {"fcp_g8", fc1p_launch<0>},
+            {"fcp_g5_hotB", fc1p_launch<32>},
             {"fcp_x_hotA", fc1p_launch<16>}, {"fcp_x_hotB", fc1p_launch<32>},
             {"fcp_x_hotAB", fc1p_launch<8>}, {"fcp_x_noload", fc1p_launch<2>}};
   constexpr int NV = sizeof(vs) / sizeof(vs[0]);
@@ -156,8 +160,9 @@ int fc1_bench(int nb, int rounds, int splits, bool toe) {
   for (int r = 0; r < rounds; ++r)
     for (int v = 0; v < NV; ++v) {
       CK(hipMemset(C, 0, csz * 4));
-      a.m_fastest = vs[v].name[4] == 'm';
-      a.linear_order = vs[v].name[4] != 'x';
+      a.m_fastest = vs[v].name[4] == 'm' ? 1 : vs[v].name[4] == 'g' ? 3 : 0;
+      a.m_group = vs[v].name[4] == 'g' ? vs[v].name[5] - '0' : 0;
+      a.linear_order = vs[v].name[4] == 'm';
       const unsigned nblk = (unsigned)(a.m_tiles * a.n_tiles * splits);
       vs[v].f(a, nblk);
       if (r == 0 && strstr(vs[v].name, "hot") == nullptr && strstr(vs[v].name, "no") == nullptr) {
