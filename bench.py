@@ -469,44 +469,68 @@ def tss_workload(eng, genome, dg, dev, genes=96, steps=2):
             "projected_20k_genes_s_1gpu": 20000 / gps, "projected_20k_genes_s_8gpu_weak": 20000 / gps / 8}
 
 
+def _cli_run(d, fa, vcf, name, vb, runs=2):
+    """chromatin.run over `vcf` into d/name (stdout swallowed: bench prints one JSON line); the
+    fastest of `runs` runs' LAST_RUN timings (the first also pays pinned-buffer allocation)."""
+    import contextlib
+    import io
+    from expecto_amd import chromatin
+    args = chromatin.build_parser().parse_args(
+        [vcf, "--genome", fa, "--synthetic-weights", "0", "--output_dir", os.path.join(d, name), "--variant-batch",
+         str(vb), "--max-batch", str(MAX_BATCH)])
+    out = []
+    for _ in range(runs):
+        with contextlib.redirect_stdout(io.StringIO()):
+            chromatin.run(args)
+        out.append(dict(chromatin.LAST_RUN))
+    return min(out, key=lambda r: r["loop_s"])
+
+
 def cli_streamed(genome, n=8192):
     """The chromatin CLI end to end (chromatin.py:243-286) on configs[2]'s +-800 sweep of n
     seeded SNVs: device forward + diff + D2H into pinned buffers + the .diff.h5 row writes of
     every shift, streamed in batches of n/4 (batch k+1 computes while batch k is written, the
     overflow flag read at the release point) against one batch (no overlap).  Batch-loop wall
     time (model / genome setup excluded); variants on chr23/chr24 are filtered as chromatin.py
-    does (CHRS).  Files go to a temporary directory, removed afterwards."""
-    import contextlib
-    import io
+    does (CHRS).  Files go to a temporary directory, removed afterwards.
+    `cfg3_rank`: the same CLI at configs[3]'s per-rank shape (12,500 SNVs x 9 shifts = 1/8 of
+    100k), streamed in the default 4,096-variant batches, once: under --output-mode rank every
+    rank of an 8-GPU run does exactly this (its own rows into the shared files, no collective),
+    so its loop time is the 8-GPU CLI's; write_share = host row-write seconds / loop seconds."""
     import shutil
     import tempfile
-    from expecto_amd import chromatin
     d = tempfile.mkdtemp(prefix="expecto_cli_")
     try:
         fa = os.path.join(d, "genome.fa")
         synthetic.write_fasta(fa, genome)
-        with open(os.path.join(d, "snvs.vcf"), "w") as f:
+        vcf = os.path.join(d, "snvs.vcf")
+        with open(vcf, "w") as f:
             for c, p, r, a in synthetic.snvs(genome, n, seed=77):
                 f.write(f"{c}\t{p}\t.\t{r}\t{a}\n")
         out = {}
         for name, vb in (("streamed", n // 4), ("one_batch", n)):
-            args = chromatin.build_parser().parse_args(
-                [os.path.join(d, "snvs.vcf"), "--genome", fa, "--synthetic-weights", "0", "--output_dir",
-                 os.path.join(d, name), "--variant-batch", str(vb), "--max-batch", str(MAX_BATCH)])
-            runs = []
-            for _ in range(2):   # the first run also pays pinned-buffer allocation: keep the faster
-                with contextlib.redirect_stdout(io.StringIO()):   # the CLI's stdout lines; bench prints one JSON line
-                    chromatin.run(args)
-                runs.append(dict(chromatin.LAST_RUN))
-            st = min(runs, key=lambda r: r["loop_s"])
+            st = _cli_run(d, fa, vcf, name, vb)
             out[name] = {"loop_s": st["loop_s"], "variants_per_s": st["variants"] / st["loop_s"],
                          "batches": st["batches"], "host_launch_s": st["launch_s"], "host_wait_s": st["wait_s"],
                          "host_write_s": st["write_s"]}
-        nv = chromatin.LAST_RUN["variants"]
+            shutil.rmtree(os.path.join(d, name), ignore_errors=True)
+        nv = st["variants"]
         out["variants"] = nv
         out["h5_bytes_written"] = 9 * 3 * 2 * nv * 2002 * 4
         out["what"] = ("chromatin CLI batch loop, +-800 sweep: forward + diff + D2H + snps.shift_*.diff.h5 rows; "
                        "streamed = 4 batches overlapping compute with the previous batch's writes")
+        vcf3 = os.path.join(d, "cfg3.vcf")
+        with open(vcf3, "w") as f:
+            for c, p, r, a in synthetic.snvs(genome, CFG3_PER_RANK, seed=78):
+                f.write(f"{c}\t{p}\t.\t{r}\t{a}\n")
+        st = _cli_run(d, fa, vcf3, "cfg3", 4096, runs=1)
+        out["cfg3_rank"] = {"variants": st["variants"], "shifts": st["shifts"], "batches": st["batches"],
+                            "loop_s": st["loop_s"], "variants_per_s": st["variants"] / st["loop_s"],
+                            "host_launch_s": st["launch_s"], "host_wait_s": st["wait_s"],
+                            "host_write_s": st["write_s"], "write_share": st["write_s"] / st["loop_s"],
+                            "h5_bytes_written": 9 * 3 * 2 * st["variants"] * 2002 * 4,
+                            "what": "configs[3] per-rank shape through the CLI (1 GPU, --output-mode rank: what each "
+                                    "of 8 ranks does in parallel; unmeasured on 8 GPUs)"}
         return out
     finally:
         shutil.rmtree(d, ignore_errors=True)

@@ -397,6 +397,63 @@ __global__ __launch_bounds__(256) void pool4_phases_h2(const float* __restrict__
   *reinterpret_cast<halfx8*>(dst + 64) = ol;
 }
 
+// pool4_phases_h2 for all n_ph phases of a segment in ONE pass: a thread takes pooled row g of
+// every phase, so it reads the union of the phases' input rows once -- rows 4g + pmin ..
+// 4g + pmax + 3 (the 200-bp shift sweep has phases {0, 2}: 6 rows instead of 2 x 4) -- and
+// pools each phase from those registers with the same decode, fmaxf order and canonical re-split
+// as pool4_phases_h2 (bitwise equal).  ph: the present phases, ascending (ph.x = pmin).
+__global__ __launch_bounds__(256) void pool4_phases_h2m(const float* __restrict__ in, int s_in, int t_in, int C,
+                                                         int n_ph, int4 ph, int s_out, float* __restrict__ out) {
+  const int c8 = threadIdx.x & 63;
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long long seg = blockIdx.y;
+  const int pmin = ph.x;
+  const int pmax = n_ph == 1 ? ph.x : n_ph == 2 ? ph.y : n_ph == 3 ? ph.z : ph.w;
+  if (c8 >= C / 8 || g >= (t_in - pmin) / 4) return;
+  const long long rb = (long long)C * 4;   // bytes per row
+  const int cofs = (c8 >> 2) * 128 + (c8 & 3) * 16;
+  const char* src = reinterpret_cast<const char*>(in) + (seg * s_in + pmin + 4LL * g) * rb + cofs;
+  const int nr = min(pmax - pmin + 4, t_in - pmin - 4 * g);   // rows of the union inside the layer
+  halfx8 hi[7], lo[7];
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    if (j < nr) {
+      hi[j] = *reinterpret_cast<const halfx8*>(src + j * rb);
+      lo[j] = *reinterpret_cast<const halfx8*>(src + j * rb + 64);
+    }
+  }
+  float fv[7][8];                          // decoded union rows
+#pragma unroll
+  for (int j = 0; j < 7; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) fv[j][e] = j < nr ? (float)hi[j][e] + (float)lo[j][e] : 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i >= n_ph) break;
+    const int p = i == 0 ? ph.x : i == 1 ? ph.y : i == 2 ? ph.z : ph.w;
+    if (g >= (t_in - p) / 4) continue;
+    const int o = p - pmin;                // first union row of this phase's window (0..3)
+    halfx8 oh, ol;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float m = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        // union row o + j (o is wave-uniform: selects, not a register-indexed read)
+        const float v = o == 0 ? fv[j][e] : o == 1 ? fv[j + 1][e] : o == 2 ? fv[j + 2][e] : fv[j + 3][e];
+        m = j == 0 ? v : fmaxf(m, v);
+      }
+      _Float16 h, l;
+      split_h2(m, h, l);
+      oh[e] = h;
+      ol[e] = l;
+    }
+    char* dst = reinterpret_cast<char*>(out) + ((seg * n_ph + i) * s_out + g) * rb + cofs;
+    *reinterpret_cast<halfx8*>(dst) = oh;
+    *reinterpret_cast<halfx8*>(dst + 64) = ol;
+  }
+}
+
 // FC1 row table of the windows of one segment chunk: window m of the chunk reads conv6
 // rows [off6, off6+106) of block (segment, pool2 phase).
 // (widx: optional list of window indices; row m then serves window widx[m].)
@@ -926,6 +983,8 @@ struct expecto_beluga {
   int conv_tile = 0;                  // f16x3 conv M tile: 0 = auto (conv_tile_rows), 256 or 384
   int seg_chunk_windows = 0;          // segment path: windows per chunk cap (0 = none; tuning knob)
   int cus = 0;                        // compute units of the device (workgroups per round)
+  bool persist = true;                // f16x3 256-row conv tiles on the persistent kernel (same bits)
+  bool pool_one_pass = true;          // segment path: pool2 of all phases in one pass (same bits)
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, int>> pending;  // (layer, event index of start)
@@ -1084,8 +1143,10 @@ int conv_tile_rows(const expecto_beluga* h, int l, bool pool, long long M, int n
   return cost(384, 1.0) <= cost(256, 1.02) ? 384 : 256;
 }
 
+// persist > 0 (f16x3 256-row conv tiles): one persistent workgroup per CU, at most `persist`
+// workgroups (a multiple of 8, so a tile keeps the XCD of a one-tile-per-workgroup launch)
 template <int LAYER, int EPI>
-int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
+int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0, int persist = 0) {
   if (bm == 0) bm = (int)gemm_bm();
   const long long nblk = a.m_tiles * a.n_tiles * splits;
   EXPECTO_REQUIRE(nblk > 0 && nblk < (1LL << 31), "gemm grid out of range");
@@ -1109,8 +1170,12 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
       // LDS-DMA), 384-row tiles (conv2) on the 4-wave 96-row kernel
       if (bm == 384)
         beluga_conv_h3r<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
-      else   // 4-deep B ring, next-stage fragments read before the stage barrier (TM 256)
-        beluga_conv_h3p<LAYER, EPI, 256, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
+      else if constexpr (EPI == EPI_RELU || EPI == EPI_RELU_POOL4) {
+        if (persist > 0)   // the same tiles, workgroups looping over them
+          beluga_conv_h3pp<LAYER, EPI><<<dim3((unsigned)std::min<long long>(nblk, persist)), dim3(512), 0, st>>>(a);
+        else   // 4-deep B ring, next-stage fragments read before the stage barrier (TM 256)
+          beluga_conv_h3p<LAYER, EPI, 256, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
+      }
     } else {   // FC layers: producer / consumer waves, both operands through an LDS ring (same bits)
       beluga_fc_h3p<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
     }
@@ -1165,15 +1230,16 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
   a.s_out = s_out;
   LayerTimer lt(h, l + 1, st);
   if (h->profiling) h->macs[h->timer_base + l + 1] += (double)a.M * g.cout * a.kper;
+  const int pg = h->persist ? std::max(8, (h->cus > 0 ? h->cus : 256) / 8 * 8) : 0;
   if (pool) {
     EXPECTO_REQUIRE(s_in % 4 == 0, "pool epilogue needs 4-aligned row groups");
-    return l == 0 ? launch_gemm<2, EPI_RELU_POOL4>(a, 1, st, bm) : launch_gemm<4, EPI_RELU_POOL4>(a, 1, st, bm);
+    return l == 0 ? launch_gemm<2, EPI_RELU_POOL4>(a, 1, st, bm, pg) : launch_gemm<4, EPI_RELU_POOL4>(a, 1, st, bm, pg);
   }
   switch (l) {
-    case 1: return launch_gemm<3, EPI_RELU>(a, 1, st, bm);
-    case 2: return launch_gemm<4, EPI_RELU>(a, 1, st, bm);
-    case 3: return launch_gemm<5, EPI_RELU>(a, 1, st, bm);
-    default: return launch_gemm<6, EPI_RELU>(a, 1, st, bm);
+    case 1: return launch_gemm<3, EPI_RELU>(a, 1, st, bm, pg);
+    case 2: return launch_gemm<4, EPI_RELU>(a, 1, st, bm, pg);
+    case 3: return launch_gemm<5, EPI_RELU>(a, 1, st, bm, pg);
+    default: return launch_gemm<6, EPI_RELU>(a, 1, st, bm, pg);
   }
 }
 
@@ -1581,7 +1647,10 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
       if (pr && ((rc = st_wait(h->pev[6])) || (rc = alt_gemm(2, 1, kA4u, kW4u, false, h->D1)))) return rc;
       {  // pool2 phases (Q -> P)
         LayerTimer lt(h, 3, st);
-        if (act_fmt() == 2) {
+        if (act_fmt() == 2 && h->pool_one_pass) {   // all phases in one pass over the conv4 rows
+          dim3 grid((g.S5 + 3) / 4, ns);
+          pool4_phases_h2m<<<grid, dim3(256), 0, st>>>(h->Q, g.T4, g.T4, 480, n_ph, ph4, g.S5, h->P);
+        } else if (act_fmt() == 2) {
           dim3 grid((g.S5 + 3) / 4, ns * n_ph);
           pool4_phases_h2<<<grid, dim3(256), 0, st>>>(h->Q, g.T4, g.T4, 480, n_ph, ph4, g.S5, h->P);
         } else {
@@ -1981,6 +2050,8 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   if (const char* e = getenv("EXPECTO_FC1_M_ORDER_MB")) h->fc1_m_order_mb = atof(e);   // same bits either way
   if (const char* e = getenv("EXPECTO_FC1_ORDER")) h->fc1_order = atoi(e);              // same bits either way
   if (const char* e = getenv("EXPECTO_OVERLAP")) h->overlap = atoi(e) != 0;   // same bits either way
+  if (const char* e = getenv("EXPECTO_CONV_PERSIST")) h->persist = atoi(e) != 0;   // same bits either way
+  if (const char* e = getenv("EXPECTO_POOL_ONE_PASS")) h->pool_one_pass = atoi(e) != 0;   // same bits either way
   if (const char* e = getenv("EXPECTO_SEG_CHUNK_WINDOWS")) h->seg_chunk_windows = atoi(e);   // same bits either way
   if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)
     const int v = atoi(e);

@@ -69,6 +69,14 @@ Variant mkp3(const char* name) {
   return {name, X6P_BM, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3p<L, EPI, TM, NSB><<<nblk, 512>>>(a); }};
 }
 
+// persistent producer / consumer (grid = 256 workgroups, one per CU, looping over tiles)
+template <int L, int EPI, int TM = 0>
+Variant mkpp(const char* name) {
+  return {name, X6P_BM, [](const GemmArgs& a, unsigned nblk) {
+            beluga_conv_h3pp<L, EPI, TM><<<std::min(nblk, 256u), 512>>>(a);
+          }};
+}
+
 template <int L, int EPI, int MB, int STG, int TM = 0>
 Variant mks3(const char* name) {
   return {name, 64 * MB, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3s<L, EPI, TM, MB, STG><<<nblk, 512>>>(a); }};
@@ -258,6 +266,8 @@ int main(int argc, char** argv) {
     vs.push_back(mks3<2, EPI_RELU_POOL4, 4, 0>("h3s4"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4>("h3p"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 256, 4>("h3p4_pf"));
+    vs.push_back(mkpp<2, EPI_RELU_POOL4>("h3pp"));
+    vs.push_back(mkpp<2, EPI_RELU_POOL4, 2048>("h3pp_noepi"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 0, 4>("h3p4"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 256 | 2048, 4>("h3p4_pf_noepi"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 2>("h3p_noglds"));
@@ -275,6 +285,8 @@ int main(int argc, char** argv) {
     vs.push_back(mks3<3, EPI_RELU, 4, 0>("h3s4"));
     vs.push_back(mkp3<3, EPI_RELU>("h3p"));
     vs.push_back(mkp3<3, EPI_RELU, 256, 4>("h3p4_pf"));
+    vs.push_back(mkpp<3, EPI_RELU>("h3pp"));
+    vs.push_back(mkpp<3, EPI_RELU, 2048>("h3pp_noepi"));
     vs.push_back(mkp3<3, EPI_RELU, 0, 4>("h3p4"));
     vs.push_back(mkp3<3, EPI_RELU, 256 | 2048, 4>("h3p4_pf_noepi"));
     vs.push_back(mks3<3, EPI_RELU, 6, 0>("h3s6"));
