@@ -87,8 +87,8 @@ def kernel_name(layer: str, precision: str, segments: bool = True) -> str:
     if precision == "bf16x6":
         return f"beluga_gemm_x6q<{l}, {e}, 0>"
     if precision == "f16x3":
-        if l in (7, 8):
-            return f"beluga_fc_h3p<{l}, {e}, 0, 3>"
+        if l in (7, 8):   # split-K FC GEMMs on 336-column tiles (beluga_fc_h3w)
+            return f"beluga_fc_h3w<{l}, {e}, 0>"
         if l in (2, 5):   # conv2, conv5: 384-row tiles (the others: producer/consumer 256-row tiles)
             return f"beluga_conv_h3r<{l}, {e}, 0>"
         return f"beluga_conv_h3p<{l}, {e}, 256, 4>"

@@ -979,11 +979,13 @@ struct expecto_beluga {
   int fc_splits = kFcSplitsDefault;   // FC1 split-K slabs: a divisor of 2120 K blocks, <= 32
   int fc2_splits = kFc2SplitsDefault; // FC2 split-K slabs: a divisor of 63 K blocks
   double fc1_m_order_mb = 80.0;       // FC1 dispatch: M tiles fastest while one split's A is <= this
-  int fc1_order = 0;                  // 2: slab-outermost, XCD-owned M tiles for large M (EXPECTO_FC1_ORDER)
+  int fc1_order = 3;                  // FC1 dispatch order (EXPECTO_FC1_ORDER): 3 grouped M tiles (default),
+                                      // 0 M-fastest / N-fastest by A-slab size, 2 slab-outermost
+  int fc1_m_group = 8;                // order 3: M tiles per group (EXPECTO_FC1_M_GROUP)
+  bool fc_wide = true;                // f16x3 FC split-K GEMMs on 336-column tiles (EXPECTO_FC_WIDE; same bits)
   int conv_tile = 0;                  // f16x3 conv M tile: 0 = auto (conv_tile_rows), 256 or 384
   int seg_chunk_windows = 0;          // segment path: windows per chunk cap (0 = none; tuning knob)
   int cus = 0;                        // compute units of the device (workgroups per round)
-  bool persist = true;                // f16x3 256-row conv tiles on the persistent kernel (same bits)
   bool pool_one_pass = true;          // segment path: pool2 of all phases in one pass (same bits)
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;
@@ -1143,10 +1145,8 @@ int conv_tile_rows(const expecto_beluga* h, int l, bool pool, long long M, int n
   return cost(384, 1.0) <= cost(256, 1.02) ? 384 : 256;
 }
 
-// persist > 0 (f16x3 256-row conv tiles): one persistent workgroup per CU, at most `persist`
-// workgroups (a multiple of 8, so a tile keeps the XCD of a one-tile-per-workgroup launch)
 template <int LAYER, int EPI>
-int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0, int persist = 0) {
+int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
   if (bm == 0) bm = (int)gemm_bm();
   const long long nblk = a.m_tiles * a.n_tiles * splits;
   EXPECTO_REQUIRE(nblk > 0 && nblk < (1LL << 31), "gemm grid out of range");
@@ -1170,12 +1170,15 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0, int p
       // LDS-DMA), 384-row tiles (conv2) on the 4-wave 96-row kernel
       if (bm == 384)
         beluga_conv_h3r<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
-      else if constexpr (EPI == EPI_RELU || EPI == EPI_RELU_POOL4) {
-        if (persist > 0)   // the same tiles, workgroups looping over them
-          beluga_conv_h3pp<LAYER, EPI><<<dim3((unsigned)std::min<long long>(nblk, persist)), dim3(512), 0, st>>>(a);
-        else   // 4-deep B ring, next-stage fragments read before the stage barrier (TM 256)
-          beluga_conv_h3p<LAYER, EPI, 256, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
-      }
+      else   // 4-deep B ring, next-stage fragments read before the stage barrier (TM 256)
+        beluga_conv_h3p<LAYER, EPI, 256, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
+    } else if constexpr (EPI == EPI_PARTIAL) {
+      // FC split-K partials: 336-column tiles on 8 MFMA waves when the caller tiled N that way
+      // (fc_wide_tiles), else 160-column producer / consumer tiles (same bits either way)
+      if ((long long)a.n_tiles * FCW_BN >= a.n_store && (long long)(a.n_tiles - 1) * FCW_BN < a.n_store)
+        beluga_fc_h3w<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
+      else
+        beluga_fc_h3p<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
     } else {   // FC layers: producer / consumer waves, both operands through an LDS ring (same bits)
       beluga_fc_h3p<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
     }
@@ -1230,16 +1233,15 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
   a.s_out = s_out;
   LayerTimer lt(h, l + 1, st);
   if (h->profiling) h->macs[h->timer_base + l + 1] += (double)a.M * g.cout * a.kper;
-  const int pg = h->persist ? std::max(8, (h->cus > 0 ? h->cus : 256) / 8 * 8) : 0;
   if (pool) {
     EXPECTO_REQUIRE(s_in % 4 == 0, "pool epilogue needs 4-aligned row groups");
-    return l == 0 ? launch_gemm<2, EPI_RELU_POOL4>(a, 1, st, bm, pg) : launch_gemm<4, EPI_RELU_POOL4>(a, 1, st, bm, pg);
+    return l == 0 ? launch_gemm<2, EPI_RELU_POOL4>(a, 1, st, bm) : launch_gemm<4, EPI_RELU_POOL4>(a, 1, st, bm);
   }
   switch (l) {
-    case 1: return launch_gemm<3, EPI_RELU>(a, 1, st, bm, pg);
-    case 2: return launch_gemm<4, EPI_RELU>(a, 1, st, bm, pg);
-    case 3: return launch_gemm<5, EPI_RELU>(a, 1, st, bm, pg);
-    default: return launch_gemm<6, EPI_RELU>(a, 1, st, bm, pg);
+    case 1: return launch_gemm<3, EPI_RELU>(a, 1, st, bm);
+    case 2: return launch_gemm<4, EPI_RELU>(a, 1, st, bm);
+    case 3: return launch_gemm<5, EPI_RELU>(a, 1, st, bm);
+    default: return launch_gemm<6, EPI_RELU>(a, 1, st, bm);
   }
 }
 
@@ -1251,13 +1253,21 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
 // h1 rows (FC1 output, FC2 input) start `rows` rows into the h1 buffer
 float* h1_rows(expecto_beluga* h, long long rows) { return h->h1 + rows * kHidLd * act_bytes() / 4; }
 
+// FC split-K GEMMs on 336-column tiles (beluga_fc_h3w): f16x3 only (the other arithmetics keep
+// their 160-column kernels).  tools/gemm_bench fc1 (8,192 segment-like rows, 8 slabs, one box,
+// fp32-eq TF/s): 485 vs 449.5 (160-column tiles, N fastest) / 464.6 (grouped M tiles); bitwise
+// equal.  Their N order is the XCD-remapped N-fastest one (m_fastest 0): 6 N tiles of one M
+// tile share its A rows, ~5.3 M tiles per XCD share a weight tile.
+bool fc_wide_tiles(const expecto_beluga* h) { return h->fc_wide && g_precision == EXPECTO_PRECISION_F16X3; }
+
 // FC1 (split-K slabs into `part`) + fc1_reduce (bias, ReLU, activation planes) into h1.
 int run_fc1(expecto_beluga* h, const float* act, const long long* a_rows, int nb, float* h1, hipStream_t st,
             const unsigned* ks_mask = nullptr, double slab_frac = 1.0, long long part_rows = 0) {
   if (part_rows <= 0) part_rows = nb;
   int rc;
   const long long m_tiles = (nb + gemm_bm() - 1) / gemm_bm();
-  const int n_tiles1 = npad_of(kFc1Out) / GBN;
+  const bool wide = fc_wide_tiles(h);
+  const int n_tiles1 = wide ? (kHidLd + FCW_BN - 1) / FCW_BN : npad_of(kFc1Out) / GBN;
   const int splits = h->fc_splits;
   {
     GemmArgs a{};
@@ -1282,6 +1292,19 @@ int run_fc1(expecto_beluga* h, const float* act, const long long* a_rows, int nb
     a.linear_order = a.m_fastest;   // N tiles fastest: XCD-aware remap (consecutive tiles share an XCD)
     if (h->fc1_order == 2 && !a.m_fastest && m_tiles % 8 == 0 && planes_gemm() && g_precision == EXPECTO_PRECISION_F16X3)
       a.m_fastest = 2;              // slab-outermost, XCD-owned M tiles (gemm_fc_h3p_body)
+    // round 3 default: grouped order (gemm_fc_h3p_body m_fastest 3; XCD remap, so an XCD's ~32
+    // concurrent workgroups cover m_group M tiles x ~32/m_group N tiles of one split-K slab):
+    // tools/gemm_bench fc1 (segment-like a_rows, 8 slabs), one box, fp32-eq TF/s: 8,192 rows
+    // 460 vs 433 (N fastest) / 441 (M fastest), 2,816 rows 434 vs 411 / 397; same bits
+    if (h->fc1_order == 3 && g_precision == EXPECTO_PRECISION_F16X3) {
+      a.m_fastest = 3;
+      a.m_group = h->fc1_m_group;
+      a.linear_order = 0;
+    }
+    if (wide) {   // 336-column tiles: N fastest per XCD (orders measured equal within 1 %)
+      a.m_fastest = 0;
+      a.linear_order = 0;
+    }
     a.C = h->part;
     a.ldc = kHidLd;
     a.n_store = kHidLd;
@@ -1322,12 +1345,14 @@ int run_fc2(expecto_beluga* h, const float* h1, int nb, float* y, hipStream_t st
     a.ldb = kHidLd;
     a.kper = kHidLd / h->fc2_splits;
     a.taps = 1;
-    a.n_tiles = npad_of(kNFeat) / GBN;
+    const bool wide = fc_wide_tiles(h) && h->fc2_splits > 1;
+    a.n_tiles = wide ? (kNFeat + FCW_BN - 1) / FCW_BN : npad_of(kNFeat) / GBN;
     a.m_tiles = m_tiles;
     // M tiles fastest while the A slab is small; N tiles fastest (XCD-aware remap: an XCD runs
     // the 13 N tiles of its A tiles back to back) for the large unsplit launches of the segment
     // path, whose h1 rows (up to fc2_rows x 8 KB) would otherwise be streamed once per N tile
     a.m_fastest = (double)m_tiles * gemm_bm() * (kHidLd / h->fc2_splits) * 4.0 <= h->fc1_m_order_mb * (1 << 20) ? 1 : 0;
+    if (wide) a.m_fastest = 0;
     a.C = h->part2;
     a.ldc = kHidLd;
     a.n_store = kNFeat;
@@ -2049,8 +2074,9 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   }
   if (const char* e = getenv("EXPECTO_FC1_M_ORDER_MB")) h->fc1_m_order_mb = atof(e);   // same bits either way
   if (const char* e = getenv("EXPECTO_FC1_ORDER")) h->fc1_order = atoi(e);              // same bits either way
+  if (const char* e = getenv("EXPECTO_FC1_M_GROUP")) h->fc1_m_group = std::max(1, atoi(e));   // same bits
+  if (const char* e = getenv("EXPECTO_FC_WIDE")) h->fc_wide = atoi(e) != 0;                   // same bits
   if (const char* e = getenv("EXPECTO_OVERLAP")) h->overlap = atoi(e) != 0;   // same bits either way
-  if (const char* e = getenv("EXPECTO_CONV_PERSIST")) h->persist = atoi(e) != 0;   // same bits either way
   if (const char* e = getenv("EXPECTO_POOL_ONE_PASS")) h->pool_one_pass = atoi(e) != 0;   // same bits either way
   if (const char* e = getenv("EXPECTO_SEG_CHUNK_WINDOWS")) h->seg_chunk_windows = atoi(e);   // same bits either way
   if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)

@@ -111,6 +111,8 @@ template <int TM>
 void fc1_launch(const GemmArgs& a, unsigned nblk) { beluga_gemm_h3q<7, EPI_PARTIAL, TM, 3><<<nblk, 256>>>(a); }
 template <int TM, int NS = 3>
 void fc1p_launch(const GemmArgs& a, unsigned nblk) { beluga_fc_h3p<7, EPI_PARTIAL, TM, NS><<<nblk, 512>>>(a); }
+template <int TM>
+void fc1w_launch(const GemmArgs& a, unsigned nblk) { beluga_fc_h3w<7, EPI_PARTIAL, TM><<<nblk, 512>>>(a); }
 template <int TM, int NS = 3, int NB = 10, int NW = 4>
 void fc1r_launch(const GemmArgs& a, unsigned nblk) { beluga_fc_h3<7, EPI_PARTIAL, TM, NS, NB, NW><<<nblk, 64 * NW>>>(a); }
 
@@ -157,7 +159,9 @@ int fc1_bench(int nb, int rounds, int splits, bool toe) {
             {"fcp_g6", fc1p_launch<0>}, {"fcp_g8", fc1p_launch<0>},
             {"fcp_g5_hotB", fc1p_launch<32>},
             {"fcp_x_hotA", fc1p_launch<16>}, {"fcp_x_hotB", fc1p_launch<32>},
-            {"fcp_x_hotAB", fc1p_launch<8>}, {"fcp_x_noload", fc1p_launch<2>}};
+            {"fcp_x_hotAB", fc1p_launch<8>}, {"fcp_x_noload", fc1p_launch<2>},
+            {"fcw_x", fc1w_launch<0>}, {"fcw_m", fc1w_launch<0>}, {"fcw_g4", fc1w_launch<0>},
+            {"fcw_x_hotB", fc1w_launch<32>}, {"fcw_x_noload", fc1w_launch<2>}};
   constexpr int NV = sizeof(vs) / sizeof(vs[0]);
   const size_t csz = (size_t)splits * nb * ldc;
   std::vector<float> ref(csz), out(csz);
@@ -171,6 +175,7 @@ int fc1_bench(int nb, int rounds, int splits, bool toe) {
       a.m_fastest = vs[v].name[4] == 'm' ? 1 : vs[v].name[4] == 'g' ? 3 : 0;
       a.m_group = vs[v].name[4] == 'g' ? vs[v].name[5] - '0' : 0;
       a.linear_order = vs[v].name[4] == 'm';
+      a.n_tiles = vs[v].name[2] == 'w' ? 6 : npad / GBN;   // fcw: 336-column tiles
       const unsigned nblk = (unsigned)(a.m_tiles * a.n_tiles * splits);
       vs[v].f(a, nblk);
       if (r == 0 && strstr(vs[v].name, "hot") == nullptr && strstr(vs[v].name, "no") == nullptr) {
@@ -268,6 +273,7 @@ int main(int argc, char** argv) {
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 256, 4>("h3p4_pf"));
     vs.push_back(mkpp<2, EPI_RELU_POOL4>("h3pp"));
     vs.push_back(mkpp<2, EPI_RELU_POOL4, 2048>("h3pp_noepi"));
+    vs.push_back(mkpp<2, EPI_RELU_POOL4, 4096>("h3pp_stagger"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 0, 4>("h3p4"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 256 | 2048, 4>("h3p4_pf_noepi"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 2>("h3p_noglds"));
@@ -287,6 +293,7 @@ int main(int argc, char** argv) {
     vs.push_back(mkp3<3, EPI_RELU, 256, 4>("h3p4_pf"));
     vs.push_back(mkpp<3, EPI_RELU>("h3pp"));
     vs.push_back(mkpp<3, EPI_RELU, 2048>("h3pp_noepi"));
+    vs.push_back(mkpp<3, EPI_RELU, 4096>("h3pp_stagger"));
     vs.push_back(mkp3<3, EPI_RELU, 0, 4>("h3p4"));
     vs.push_back(mkp3<3, EPI_RELU, 256 | 2048, 4>("h3p4_pf_noepi"));
     vs.push_back(mks3<3, EPI_RELU, 6, 0>("h3s6"));

@@ -6,6 +6,8 @@
 //   beluga_conv_h3s  8-wave (two per SIMD) conv tiles, optionally staggered partners
 //   beluga_gemm_h3q  the planes GEMM at PL 2 (f16x3 without the chunk slab)
 //   beluga_conv_h3q  the chunk-slab conv body at 256-row tiles, 4 waves
+//   beluga_conv_h3pp persistent producer / consumer conv workgroups (round 3: hides the
+//                    per-tile prologue, +1-3 % without epilogue, not the epilogue itself)
 #pragma once
 #include "../expecto_amd/csrc/gemm_kernel.h"
 
@@ -678,5 +680,311 @@ __global__ __launch_bounds__(256, 1) void beluga_conv_h3q(GemmArgs p) {
   gemm_conv_h3_body<LAYER, EPI, TM, NSB>(p, smem);
 }
 
+
+// ---- f16x3 conv GEMM, persistent producer / consumer workgroups -------------------------
+// gemm_conv_h3p_body (NSB 4, PF) with one workgroup per CU looping over tiles (virtual block
+// v = blockIdx.x + k * gridDim.x, mapped to (M tile, N tile) by the same XCD remap as a
+// one-tile-per-workgroup launch of all tiles; gridDim.x a multiple of 8 keeps v's XCD).  The B
+// ring and the slab double buffer run on a global stage / chunk counter across tiles, so the
+// producers stage the next tile's chunk-0 slab and its first 3 B stages during the current
+// tile's last chunk, and the consumers start the next tile right after their epilogue instead
+// of behind a new workgroup's prologue.  The epilogue's global stores (160 KB per tile; every CU
+// stores at once when tiles run in lockstep rounds) then drain while the next tile's MFMAs run:
+// a consumer wave issues no vector-memory loads, so it never waits for them.
+// Epilogue staging: 16-row passes, per wave 16 x 656 B in LDS the producers do not touch
+// until every consumer has passed one extra barrier per tile ("E"): waves 0-2 in the slab the
+// tile's last chunk used, wave 3 in the B ring slot of the tile's last stage.  Producers enter
+// barrier E first thing in every tile but the first, before issuing that tile's slab pieces of
+// chunk 1 (which go to that slab) and B stage 3 (which goes to that slot).
+// Same products and k order per output as every f16x3 conv kernel: bitwise equal.
+// Measured (profiles/r03/gemm_bench_fc1_order_convpp.txt): conv2 551 vs 546, conv3 474 vs 481,
+// conv4 548 vs 540, conv5 495 vs 503, conv6 498 vs 500 fp32-eq TF/s against the per-tile
+// kernel, the 200-window pipeline unchanged (996-998 vs 995-999 variants/s); TM 4096 (odd
+// workgroups start half a tile late, so the CUs' epilogue store bursts alternate) slower still.
+// Not used by the library.
+template <int MB16 = 4>
+__device__ __forceinline__ void epilogue_relu_h2_q16(const GemmArgs& p, const floatx4v (&acc)[4][10], long long mw,
+                                                     int n0, int lane, char* lds) {
+  const int fr = lane & 15, fq = lane >> 4;
+  const long long w0 = mw / p.s_in;
+  const int t0 = (int)(mw - w0 * p.s_in);
+  const long long ldb = p.ldc >> 5;
+  float vmax = 0.f;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) {
+#pragma unroll
+    for (int nb = 0; nb < 10; ++nb) {
+      const int n = n0 + nb * 16 + fr;
+      const float cso = n < p.n_store ? p.col_scale[n] * p.out_scale : 0.f;
+      const float bo = n < p.n_store ? p.bias[n] * p.out_scale : 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float x = fmaxf(fmaf(acc[mb][nb][j], cso, bo), 0.f);
+        vmax = fmaxf(vmax, x);
+        _Float16 hi, lo;
+        split_h2p(x, hi, lo);
+        char* d = lds + (4 * fq + j) * H3E_ROW + (nb >> 1) * 128 + ((nb & 1) * 16 + fr) * 2;
+        *(_Float16*)d = hi;
+        *(_Float16*)(d + 64) = lo;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll 5
+    for (int i = 0; i < 10; ++i) {
+      const int k = i * 64 + lane, row = k / 40, ch = k - row * 40;
+      const long long m = mw + mb * 16 + row;
+      if (m < p.M) {
+        long long w;
+        int tpos;
+        row_wt(w0, t0, mb * 16 + row, p.s_in, w, tpos);
+        if (tpos < p.t_valid && n0 + (ch >> 3) * 32 < p.n_store) {
+          char* g = (char*)p.C + ((w * p.s_out + tpos) * ldb + (n0 >> 5)) * 128 + ch * 16;
+          *(floatx4v*)g = *(const floatx4v*)(lds + row * H3E_ROW + ch * 16);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  if (!(vmax < 65504.f)) *p.ovf = 1;
+}
+
+// (mt, nt) of virtual block v of a launch of `nv` blocks (the XCD remap of the conv kernels)
+__device__ __forceinline__ void conv_tile_of(const GemmArgs& p, unsigned v, unsigned nv, long long& mt, int& nt) {
+  const unsigned xcd = v & 7u, q = nv >> 3, rr = nv & 7u;
+  const unsigned lin = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (v >> 3);
+  nt = (int)(lin % (unsigned)p.n_tiles);
+  mt = (long long)(lin / (unsigned)p.n_tiles) % p.m_tiles;
+}
+
+template <int LAYER, int EPI, int TM>
+__device__ __forceinline__ void gemm_conv_h3pp_body(const GemmArgs& p, char* smem) {
+  static_assert(EPI == EPI_RELU || EPI == EPI_RELU_POOL4, "conv epilogues only");
+  constexpr int NSB = 4;
+  using G = SlabGeo<4>;
+  constexpr int ROW_KB = 128;
+  constexpr int NAP = (G::PIECES + 3) / 4;            // slab pieces per producer wave and chunk (9)
+  const unsigned nv = (unsigned)(p.m_tiles * p.n_tiles), gstep = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kb_total = (int)(p.ldb / GBK);
+  const long long lda_kb = p.lda / GBK;
+  const int nchunk = (int)lda_kb;
+  const int nk = nchunk * 8;
+  auto swz = [](int r) { return conv_swz<TM>(r); };
+  char* const aslab = smem;
+  char* const bring = smem + 2 * G::ASLAB;
+  const int ntile = (int)((nv - blockIdx.x + gstep - 1) / gstep);   // tiles of this workgroup (>= 1)
+  if constexpr ((TM & 4096) != 0) {   // probe: odd workgroups start half a tile late (epilogues out of phase)
+    if (blockIdx.x & 1)
+      for (int i = 0; i < nk; ++i) __builtin_amdgcn_s_sleep(15);
+  }
+
+  if (wave >= 4) {
+    // ---------------- producer: all LDS-DMA issue, on a global stage / chunk counter ----------------
+    const int pw = wave - 4;
+    const long long last_row = p.M - 1 + 7;
+    unsigned boffs[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int g = pw + 4 * j;
+      const int pl = g / 10, r = 16 * (g % 10) + (lane >> 2);
+      const int c = (lane & 3) ^ swz(r);
+      boffs[j] = (unsigned)((long long)r * kb_total * ROW_KB + pl * 64 + 16 * c);
+    }
+    // per-tile sources (tile k of this workgroup)
+    auto a_base = [&](int k, unsigned (&aoff)[NAP]) -> __amdgpu_buffer_rsrc_t {
+      long long mt;
+      int nt;
+      conv_tile_of(p, blockIdx.x + (unsigned)k * gstep, nv, mt, nt);
+      const long long m0 = mt * G::BM;
+#pragma unroll
+      for (int i = 0; i < NAP; ++i) {
+        const int P = min(pw + 4 * i, G::PIECES - 1), g = P >> 1, pl = P & 1;
+        const int r = 16 * g + (lane >> 2);
+        const long long m = min(m0 + r, last_row);
+        const int c = (lane & 3) ^ swz(r);
+        aoff[i] = (unsigned)((m - m0) * lda_kb * ROW_KB + pl * 64 + 16 * c);
+      }
+      return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.A + m0 * lda_kb * ROW_KB), (short)0, 0x7fffffff,
+                                               0x00020000);
+    };
+    auto b_base = [&](int k) -> __amdgpu_buffer_rsrc_t {
+      long long mt;
+      int nt;
+      conv_tile_of(p, blockIdx.x + (unsigned)k * gstep, nv, mt, nt);
+      return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.Bp + (long long)nt * GBN * kb_total * ROW_KB),
+                                               (short)0, 0x7fffffff, 0x00020000);
+    };
+    unsigned aoff_c[NAP], aoff_n[NAP];
+    __amdgpu_buffer_rsrc_t ars_c = a_base(0, aoff_c), ars_n = ars_c;
+    __amdgpu_buffer_rsrc_t brs_c = b_base(0), brs_n = brs_c;
+    if (ntile > 1) {
+      ars_n = a_base(1, aoff_n);
+      brs_n = b_base(1);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NAP; ++i) aoff_n[i] = aoff_c[i];
+    }
+    auto issue_a = [&](const __amdgpu_buffer_rsrc_t& rs, const unsigned (&aoff)[NAP], int chunk, int gchunk, int i0,
+                       int ni) {
+      char* base = aslab + (gchunk & 1) * G::ASLAB;
+      const int src_chunk = (TM & 8) ? 0 : chunk;
+      for (int i = i0; i < i0 + ni; ++i) {
+        const int P = min(pw + 4 * i, G::PIECES - 1);
+        char* dst = base + (P & 1) * G::APLANE + (P >> 1) * 1024;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)dst, 16, aoff[i], (unsigned)(src_chunk * ROW_KB), 0, 0);
+      }
+    };
+    // B of global stage gs into its ring slot; past this workgroup's last stage the data is the
+    // last stage's again (dummy reissues keep every stage's piece count uniform for the counted
+    // vmcnt; they land in the slots of stages that never come, never in the last stage's slot,
+    // which wave 3's epilogue uses)
+    const long long gs_last = (long long)ntile * nk - 1;
+    auto issue_b = [&](long long gs, int kt) {
+      char* base = bring + (int)(gs % NSB) * H3C_BSTAGE;
+      if (gs > gs_last) gs = gs_last;
+      const int k = (int)(gs / nk), s = (TM & 8) ? 0 : (int)(gs - (long long)k * nk);
+      const __amdgpu_buffer_rsrc_t& rs = k == kt ? brs_c : brs_n;
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(base + (pw + 4 * j) * 1024), 16, boffs[j],
+                                                 (unsigned)(s * ROW_KB), 0, 0);
+    };
+    issue_a(ars_c, aoff_c, 0, 0, 0, NAP);
+    issue_b(0, 0);
+    issue_b(1, 0);
+    issue_b(2, 0);
+    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");    // stages 0 and 1 landed
+    __builtin_amdgcn_s_barrier();
+    for (int kt = 0; kt < ntile; ++kt) {
+      if (kt > 0) {
+        __builtin_amdgcn_s_barrier();                   // E: the consumers' epilogue left the LDS
+        ars_c = ars_n;
+        brs_c = brs_n;
+#pragma unroll
+        for (int i = 0; i < NAP; ++i) aoff_c[i] = aoff_n[i];
+        if (kt + 1 < ntile) {
+          ars_n = a_base(kt + 1, aoff_n);
+          brs_n = b_base(kt + 1);
+        }
+      }
+      for (int c = 0; c < nchunk; ++c) {
+        const int gc = kt * nchunk + c;
+        const bool last_c = c + 1 == nchunk;
+        const bool more_a = !(TM & 2) && (!last_c || kt + 1 < ntile);
+        for (int t = 0; t < 8; ++t) {
+          const long long gs = (long long)kt * nk + c * 8 + t;
+          if (more_a && t < 6) {                        // slab pieces 2,2,2,1,1,1,0,0
+            const int i0 = t < 3 ? 2 * t : t + 3, ni = t < 3 ? 2 : 1;
+            if (last_c)
+              issue_a(ars_n, aoff_n, 0, gc + 1, i0, ni);   // the next tile's chunk 0
+            else
+              issue_a(ars_c, aoff_c, c + 1, gc + 1, i0, ni);
+          }
+          if (!(TM & 2)) issue_b(gs + NSB - 1, kt);
+          asm volatile("s_waitcnt vmcnt(5)" ::: "memory");   // all but this stage's pieces
+          __builtin_amdgcn_s_barrier();
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
+
+  // ---------------- consumer: LDS reads, MFMAs, epilogue ----------------
+  const int fr = lane & 15, fq = lane >> 4;
+  const int brow = fr * 64 + 16 * (fq ^ swz(fr));
+  auto read_a = [&](const char* slab, int t, bf16x8 (&a)[4][3]) {
+    const int rr2 = fr + t;
+    const int off = (wave * 64 + rr2) * 64 + 16 * (fq ^ swz(rr2));
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      a[mb][0] = *(const bf16x8*)(slab + off + mb * 1024);
+      a[mb][1] = *(const bf16x8*)(slab + off + mb * 1024 + G::APLANE);
+    }
+  };
+  auto read_b = [&](const char* base, int nb, bf16x8 (&b)[3]) {
+    const char* br = base + brow + nb * 1024;
+    b[0] = *(const bf16x8*)(br);
+    b[1] = *(const bf16x8*)(br + X6P_B_PLANE);
+  };
+  auto pin = [&]() {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if ((i & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+    }
+  };
+  __builtin_amdgcn_s_barrier();                         // slab 0 and B stages 0, 1 landed
+  asm volatile("" ::: "memory");
+  bf16x8 as[4][3];
+  bf16x8 b0[3], b1[3];
+  for (int kt = 0; kt < ntile; ++kt) {
+    long long mt;
+    int nt;
+    conv_tile_of(p, blockIdx.x + (unsigned)kt * gstep, nv, mt, nt);
+    const long long m0 = mt * G::BM;
+    const int n0 = nt * GBN;
+    floatx4v acc[4][10];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 10; ++nb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[mb][nb][r] = 0.f;
+    const long long gs0 = (long long)kt * nk;
+    read_a(aslab + ((kt * nchunk) & 1) * G::ASLAB, 0, as);
+    read_b(bring + (int)(gs0 % NSB) * H3C_BSTAGE, 0, b0);
+    for (int c = 0; c < nchunk; ++c) {
+      const int gc = kt * nchunk + c;
+      const char* slab = aslab + (gc & 1) * G::ASLAB;
+      for (int t = 0; t < 8; ++t) {
+        const long long gs = gs0 + c * 8 + t;
+        const char* base = bring + (int)(gs % NSB) * H3C_BSTAGE;
+        const bool tile_end = c + 1 == nchunk && t == 7;
+#pragma unroll
+        for (int nb = 0; nb < 10; ++nb) {
+          if (nb + 1 < 10) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
+#pragma unroll
+          for (int mb = 0; mb < 4; ++mb) acc[mb][nb] = planes_mfma<2>(acc[mb][nb], as[mb], (nb & 1) ? b1 : b0);
+          pin();
+        }
+        if (!tile_end) {      // next stage's first fragments (landed at barrier s-1), read before barrier s
+          if (t < 7)
+            read_a(slab, t + 1, as);
+          else
+            read_a(aslab + ((gc + 1) & 1) * G::ASLAB, 0, as);   // next slab landed by tap 6's barrier
+          read_b(bring + (int)((gs + 1) % NSB) * H3C_BSTAGE, 0, b0);
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+    }
+    // epilogue: waves 0-2 stage in the slab of the tile's last chunk, wave 3 in its last B slot
+    const long long gl = gs0 + nk - 1;
+    char* e = wave < 3 ? aslab + ((kt * nchunk + nchunk - 1) & 1) * G::ASLAB + wave * 16 * H3E_ROW
+                       : bring + (int)(gl % NSB) * H3C_BSTAGE;
+    if constexpr ((TM & 2048) != 0) {   // timing probe (wrong results): no epilogue, one store per lane
+      float t = 0.f;
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 10; ++nb) t += acc[mb][nb][0] + acc[mb][nb][1] + acc[mb][nb][2] + acc[mb][nb][3];
+      p.C[(m0 + wave * 64 + lane) % p.M] = t;
+    } else if constexpr (EPI == EPI_RELU) {
+      epilogue_relu_h2_q16(p, acc, m0 + wave * 64, n0, lane, e);
+    } else {
+      epilogue_pool_h2_lds<4, LAYER == 4>(p, acc, m0 + wave * 64, n0, lane, e);
+    }
+    if (kt + 1 < ntile) __builtin_amdgcn_s_barrier();   // E
+  }
+}
+
+template <int LAYER, int EPI, int TM = 0>
+__global__ __launch_bounds__(512, 1) void beluga_conv_h3pp(GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[h3c_lds<4>()];
+  gemm_conv_h3pp_body<LAYER, EPI, TM>(p, smem);
+}
 
 }  // namespace expecto

@@ -38,7 +38,7 @@ def main():
         i += 1
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
-    genome = synthetic.genome_bytes(n_contigs=24, contig_len=2_000_000, seed=0)
+    genome = synthetic.genome_bytes(n_contigs=24, contig_len=2_000_000, seed=0, repeats=True)   # = bench.py
     fasta = Fasta.from_dict(genome)
     dg = DeviceGenome(fasta, device=dev)
     settings = list(itertools.product(*knobs)) if knobs else [()]
