@@ -404,7 +404,8 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
 // TM: timing-only probes for tools/gemm_bench (wrong results; production launches TM 0, the
 // producer / consumer conv kernel TM 256): 2 = no LDS-DMA in the loop, 4 = no barrier in the
 // loop, 8 = LDS-DMA always from stage 0's (L2-hot) addresses; beluga_fc_h3p also 16 / 32 = only
-// the A / B pieces L2-hot; beluga_conv_h3p 2048 = no epilogue.
+// the A / B pieces L2-hot; beluga_conv_h3p 2048 = no epilogue; the f16x3 conv kernels 8192 =
+// round 2's per-column epilogue factor loads (epi_factors).
 // 16x16x32 lane layout: A/B lane l holds row/col (l & 15), k = 8*(l >> 4)..+7; C lane l
 // holds col (l & 15), rows 4*(l >> 4)..+3.  The 16 lanes of one ds_read_b128 lane group then
 // read mixed chunks, so LDS-DMA pieces (lane-linear 1 KiB = 16 rows x 64 B) are placed with an
@@ -1205,12 +1206,44 @@ constexpr int h3c_lds_mb() { return 2 * SlabGeo<MB>::ASLAB + NSB * H3C_BSTAGE; }
 // (Measured and not kept, tools/gemm_bench + the same-box pipeline A/B tools/ab_bench.sh:
 // streamed (nontemporal) stores and the plain split gained 1.6-4.1 % on conv3 / conv5 / conv6
 // alone but moved no layer time of the 200-window pipeline; streamed stores cost conv1 6 %.)
-template <int MB = 4>
+// Per-column epilogue factors of a lane's 10 columns n0 + 16 nb + (lane & 15): the column scale
+// and the bias, each x out_scale (0 past n_store).  All 20 loads are issued before the first use
+// (clamped, unconditional indices), so the wave waits for them ONCE.  Round 2 loaded them per
+// column block under an n < n_store branch, right before use: 20-40 loads per tile each followed
+// by s_waitcnt vmcnt(0) -- which also waited for the epilogue's own earlier global stores --
+// i.e. 20-40 serialized memory latencies per tile (BATCH false: that form, a timing probe).
+template <bool BATCH = true>
+__device__ __forceinline__ void epi_factors(const GemmArgs& p, int n0, int fr, float (&cso)[10], float (&bo)[10]) {
+  float c[10], b[10];
+#pragma unroll
+  for (int nb = 0; nb < 10; ++nb) {
+    const int n = n0 + nb * 16 + fr;
+    if constexpr (BATCH) {
+      const int nc = min(n, p.n_store - 1);
+      c[nb] = p.col_scale[nc];
+      b[nb] = p.bias[nc];
+    } else {
+      c[nb] = n < p.n_store ? p.col_scale[n] : 0.f;
+      b[nb] = n < p.n_store ? p.bias[n] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int nb = 0; nb < 10; ++nb) {
+    const bool in = n0 + nb * 16 + fr < p.n_store;
+    // fmaxf(acc*cs + b, 0) * osc with the power-of-2 scales folded: the same value
+    cso[nb] = in ? c[nb] * p.out_scale : 0.f;
+    bo[nb] = in ? b[nb] * p.out_scale : 0.f;
+  }
+}
+
+template <int MB = 4, bool BATCH = true>
 __device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const floatx4v (&acc)[MB][10], long long mw,
                                                      int n0, int lane, char* lds) {
   const int fr = lane & 15, fq = lane >> 4;
   const long long w0 = mw / p.s_in;
   const int t0 = (int)(mw - w0 * p.s_in);
+  float csov[10], bov[10];
+  epi_factors<BATCH>(p, n0, fr, csov, bov);
   // overflow: a running max per lane and ONE flag store at the end (a per-value conditional
   // store compiled to a branch and exec-mask juggling around every value: ~4 instructions each)
   float vmax = 0.f;
@@ -1218,10 +1251,7 @@ __device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const fl
   for (int half = 0; half < MB / 2; ++half) {
 #pragma unroll
     for (int nb = 0; nb < 10; ++nb) {
-      const int n = n0 + nb * 16 + fr;
-      // fmaxf(acc*cs + b, 0) * osc with the power-of-2 scales folded: the same value
-      const float cso = n < p.n_store ? p.col_scale[n] * p.out_scale : 0.f;
-      const float bo = n < p.n_store ? p.bias[n] * p.out_scale : 0.f;
+      const float cso = csov[nb], bo = bov[nb];
 #pragma unroll
       for (int mh = 0; mh < 2; ++mh) {
         const int mb = 2 * half + mh;
@@ -1277,17 +1307,17 @@ __device__ __forceinline__ int conv_swz(int r) {
 // The wave's 4*MB pooled rows x 160 columns are split into its private LDS area in the planes
 // layout, then stored as 16-B chunks (one contiguous 640-B run per pooled row) instead of two
 // 2-byte stores per value.  Same values as gemm_epilogue16<EPI_RELU_POOL4, 2>.
-template <int MB, bool CANON = false>
+template <int MB, bool CANON = false, bool BATCH = true>
 __device__ __forceinline__ void epilogue_pool_h2_lds(const GemmArgs& p, const floatx4v (&acc)[MB][10], long long mw,
                                                      int n0, int lane, char* lds) {
   static_assert(4 * MB <= 32, "pooled rows per wave exceed the LDS area");
   const int fr = lane & 15, fq = lane >> 4;
+  float csov[10], bov[10];
+  epi_factors<BATCH>(p, n0, fr, csov, bov);
   float vmax = 0.f;   // overflow: running max, one flag store at the end
 #pragma unroll
   for (int nb = 0; nb < 10; ++nb) {
-    const int n = n0 + nb * 16 + fr;
-    const float cso = n < p.n_store ? p.col_scale[n] * p.out_scale : 0.f;
-    const float bo = n < p.n_store ? p.bias[n] * p.out_scale : 0.f;
+    const float cso = csov[nb], bo = bov[nb];
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
       const float mx = fmaxf(fmaxf(acc[mb][nb][0], acc[mb][nb][1]), fmaxf(acc[mb][nb][2], acc[mb][nb][3]));
@@ -1502,9 +1532,10 @@ __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if constexpr (EPI == EPI_RELU)
-      epilogue_relu_h2_lds<MB>(p, acc, m0 + wave * 16 * MB, n0, lane, smem + wave * H3E_WAVE);
+      epilogue_relu_h2_lds<MB, (TM & 8192) == 0>(p, acc, m0 + wave * 16 * MB, n0, lane, smem + wave * H3E_WAVE);
     else
-      epilogue_pool_h2_lds<MB, LAYER == 4>(p, acc, m0 + wave * 16 * MB, n0, lane, smem + wave * H3E_WAVE);
+      epilogue_pool_h2_lds<MB, LAYER == 4, (TM & 8192) == 0>(p, acc, m0 + wave * 16 * MB, n0, lane,
+                                                             smem + wave * H3E_WAVE);
   } else {
     gemm_epilogue16<EPI, 2, 10, MB>(p, acc, m0 + wave * 16 * MB, n0, 0, lane);
   }
@@ -1732,9 +1763,9 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
   if constexpr (EPI == EPI_RELU || EPI == EPI_RELU_POOL4) {
     __builtin_amdgcn_s_barrier();                     // producers drained their tail pieces
     if constexpr (EPI == EPI_RELU)
-      epilogue_relu_h2_lds<4>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
+      epilogue_relu_h2_lds<4, (TM & 8192) == 0>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
     else
-      epilogue_pool_h2_lds<4, LAYER == 4>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
+      epilogue_pool_h2_lds<4, LAYER == 4, (TM & 8192) == 0>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
   } else {
     gemm_epilogue16<EPI, 2, 10, 4>(p, acc, m0 + wave * 64, n0, 0, lane);
   }

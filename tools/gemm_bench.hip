@@ -271,6 +271,8 @@ int main(int argc, char** argv) {
     vs.push_back(mks3<2, EPI_RELU_POOL4, 4, 0>("h3s4"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4>("h3p"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 256, 4>("h3p4_pf"));
+    vs.push_back(mkp3<2, EPI_RELU_POOL4, 256 | 8192, 4>("h3p4_pf_oldepi"));
+    vs.push_back(mkr3<2, EPI_RELU_POOL4, 8192>("h3r_oldepi"));
     vs.push_back(mkpp<2, EPI_RELU_POOL4>("h3pp"));
     vs.push_back(mkpp<2, EPI_RELU_POOL4, 2048>("h3pp_noepi"));
     vs.push_back(mkpp<2, EPI_RELU_POOL4, 4096>("h3pp_stagger"));
@@ -291,6 +293,8 @@ int main(int argc, char** argv) {
     vs.push_back(mks3<3, EPI_RELU, 4, 0>("h3s4"));
     vs.push_back(mkp3<3, EPI_RELU>("h3p"));
     vs.push_back(mkp3<3, EPI_RELU, 256, 4>("h3p4_pf"));
+    vs.push_back(mkp3<3, EPI_RELU, 256 | 8192, 4>("h3p4_pf_oldepi"));
+    vs.push_back(mkr3<3, EPI_RELU, 8192>("h3r_oldepi"));
     vs.push_back(mkpp<3, EPI_RELU>("h3pp"));
     vs.push_back(mkpp<3, EPI_RELU, 2048>("h3pp_noepi"));
     vs.push_back(mkpp<3, EPI_RELU, 4096>("h3pp_stagger"));

@@ -18,5 +18,5 @@ run() {  # name timeout cmd...
 [[ ${STEPS:-tests,sweep,fcw} == *fcw* ]] && run fcw 240 tools/gemm_bench 8192 5 fc1t 8
 [[ ${STEPS:-tests,sweep,fcw} == *fcw* ]] && run stagger3 240 env VARIANT=h3c,h3p4_pf,h3pp,h3pp_stagger,h3p4_pf_noepi tools/gemm_bench 2000 5 conv3
 [[ ${STEPS:-tests,sweep,fcw} == *fcw* ]] && run stagger6 240 env VARIANT=h3c,h3p4_pf,h3pp,h3pp_stagger,h3p4_pf_noepi tools/gemm_bench 2000 5 conv6
-[[ ${STEPS:-tests,sweep,fcw} == *sweep* ]] && run sweep 600 python -u tools/knob_sweep.py EXPECTO_FC1_ORDER=0,3 EXPECTO_CONV_PERSIST=0,1 EXPECTO_POOL_ONE_PASS=0,1 --steps 5 --rounds 2
+[[ ${STEPS:-tests,sweep,fcw} == *sweep* ]] && run sweep 600 python -u tools/knob_sweep.py ${SWEEP:-EXPECTO_FC_WIDE=0,1 EXPECTO_CONV_TILE=0,256} --steps 5 --rounds 3
 echo done >> $OUT/steps_b.log
