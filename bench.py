@@ -89,9 +89,7 @@ def kernel_name(layer: str, precision: str, segments: bool = True) -> str:
     if precision == "f16x3":
         if l in (7, 8):   # split-K FC GEMMs on 336-column tiles (beluga_fc_h3w)
             return f"beluga_fc_h3w<{l}, {e}, 0>"
-        if l in (2, 5):   # conv2, conv5: 384-row tiles (the others: producer/consumer 256-row tiles)
-            return f"beluga_conv_h3r<{l}, {e}, 0>"
-        return f"beluga_conv_h3p<{l}, {e}, 256, 4>"
+        return f"beluga_conv_h3p<{l}, {e}, 256, 4>"   # producer / consumer 256-row tiles (every conv layer)
     return f"beluga_gemm<{l}, {e}, 4, 2, 32, 1>"
 
 

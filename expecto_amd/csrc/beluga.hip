@@ -1136,13 +1136,17 @@ float exp2i(int e) { return std::ldexp(1.0f, e); }
 int conv_tile_rows(const expecto_beluga* h, int l, bool pool, long long M, int n_tiles) {
   if (g_precision != EXPECTO_PRECISION_F16X3) return (int)gemm_bm();
   if (h->conv_tile) return h->conv_tile;
-  if (!(l == 0 || l == 3)) return 256;   // 384-row tiles: conv2 (pool) and conv5
+  // round 3 (tools/gemm_bench 2000 windows, two boxes): the producer / consumer 256-row kernel at
+  // or above h3r on every layer (conv2 546 / 560 vs 535 / 558, conv5 503 / 512 vs 485 / 507), and
+  // the 200-window pipeline +0.3-0.5 % with EXPECTO_CONV_TILE=256 (tools/knob_sweep.py, three
+  // alternating rounds): 384-row tiles only where they need clearly fewer rounds of 256
+  // workgroups (the small alt-delta launches of the pair path)
   const int cus = h->cus > 0 ? h->cus : 256;
   auto cost = [&](int bm, double per_row) {
     const long long blocks = (M + bm - 1) / bm * n_tiles;
     return (double)((blocks + cus - 1) / cus) * bm * per_row;
   };
-  return cost(384, 1.0) <= cost(256, 1.02) ? 384 : 256;
+  return cost(384, 1.0) * 1.1 <= cost(256, 1.0) ? 384 : 256;
 }
 
 template <int LAYER, int EPI>

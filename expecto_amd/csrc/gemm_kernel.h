@@ -429,6 +429,17 @@ __device__ __forceinline__ void gemm_epilogue16(const GemmArgs& p, const floatx4
   const int fr = lane & 15, fq = lane >> 4;
   const long long w0 = mw / p.s_in;
   const int t0 = (int)(mw - w0 * p.s_in);
+  // the lane's per-column bias / scale, loaded together up front (clamped indices; columns past
+  // n_store are skipped below) rather than one load + wait per use (see epi_factors)
+  float bnv[NB], csv[NB];
+  if constexpr (EPI != EPI_PARTIAL) {
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int n = min(n0 + nb * 16 + fr, p.n_store - 1);
+      bnv[nb] = p.bias[n];
+      csv[nb] = FMT == 2 ? p.col_scale[n] : 1.f;
+    }
+  }
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
     const long long m4 = mw + mb * 16 + 4 * fq;   // first of this lane's 4 rows (multiple of 4)
@@ -453,9 +464,9 @@ __device__ __forceinline__ void gemm_epilogue16(const GemmArgs& p, const floatx4
       for (int nb = 0; nb < NB; ++nb) {
         const int n = n0 + nb * 16 + fr;
         if (n >= p.n_store) continue;
-        const float bn = p.bias[n];
+        const float bn = bnv[nb];
         // f16x3: acc * 2^-(s_in + s_w[n]) is exact (power of 2), so the value equals the unscaled sum
-        const float cs = FMT == 2 ? p.col_scale[n] : 1.f;
+        const float cs = csv[nb];
         float mx = fmaxf(fmaxf(acc[mb][nb][0], acc[mb][nb][1]), fmaxf(acc[mb][nb][2], acc[mb][nb][3]));
         if (FMT == 2) mx *= cs;
         store_act<FMT>(p.C, w * p.s_out + tp, p.ldc, n, fmaxf(mx + bn, 0.f), p.out_scale, p.ovf);
@@ -474,8 +485,8 @@ __device__ __forceinline__ void gemm_epilogue16(const GemmArgs& p, const floatx4
         for (int nb = 0; nb < NB; ++nb) {
           const int n = n0 + nb * 16 + fr;
           if (n >= p.n_store) continue;
-          const float bn = p.bias[n];
-          const float cs = FMT == 2 ? p.col_scale[n] : 1.f;
+          const float bn = bnv[nb];
+          const float cs = csv[nb];
           const float a = FMT == 2 ? acc[mb][nb][j] * cs : acc[mb][nb][j];
           const float v = a + bn;
           if (EPI == EPI_SIGMOID)
