@@ -388,8 +388,8 @@ def pmc_traffic(key, kernel):
         if t.get("profile_key") != key:
             continue
         for name, v in t["kernels"].items():
-            if kernel in name:
-                return v["hbm_bytes"], t["source"]
+            if kernel in name:   # the layer's full launches (the alt-delta launches share the kernel)
+                return v.get("main_hbm_bytes", v["hbm_bytes"]), t["source"]
     return None, None
 
 

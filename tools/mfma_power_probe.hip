@@ -23,7 +23,11 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
     }                                                                              \
   } while (0)
 
-// 8 independent 16x16x32 chains (8 x 16 cycles covers the MFMA dependency latency)
+// 8 independent 16x16x32 chains (8 x 16 cycles covers the MFMA dependency latency).
+// ORD 0: A and B operands both change from one MFMA to the next (round 2's probe); ORD 1: the
+// B operand stays for 4 consecutive MFMAs (A changes), the order a GEMM unit gets when its
+// 3 split products are issued product-major over the 4 row blocks instead of row-block-major.
+template <int ORD>
 __global__ __launch_bounds__(256) void mfma16(const halfx8* __restrict__ in, int iters, float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   halfx8 a[4], b[4];   // 4 operand pairs rotating over the chains: the datapath sees changing data
@@ -37,7 +41,8 @@ __global__ __launch_bounds__(256) void mfma16(const halfx8* __restrict__ in, int
   for (int c = 0; c < 8; ++c) acc[c] = floatx4{0.f, 0.f, 0.f, 0.f};
   for (int it = 0; it < iters; ++it) {
 #pragma unroll
-    for (int c = 0; c < 8; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c & 3], b[(c + 1) & 3], acc[c], 0, 0, 0);
+    for (int c = 0; c < 8; ++c)
+      acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c & 3], ORD == 0 ? b[(c + 1) & 3] : b[c >> 2], acc[c], 0, 0, 0);
   }
   float s = 0.f;
 #pragma unroll
@@ -97,12 +102,14 @@ int main(int argc, char** argv) {
   CHECK(hipEventCreate(&e1));
   const double flops = (double)blocks * 4 /*waves*/ * iters * 8.0 * 16384.0;
   for (int rep = 0; rep < 3; ++rep) {
-    for (int form = 0; form < 2; ++form) {
+    for (int form = 0; form < 3; ++form) {
       CHECK(hipEventRecord(e0, 0));
       if (form == 0)
-        mfma16<<<blocks, 256>>>(in, iters, out);
-      else
+        mfma16<0><<<blocks, 256>>>(in, iters, out);
+      else if (form == 1)
         mfma32<<<blocks, 256>>>(in, iters, out);
+      else
+        mfma16<1><<<blocks, 256>>>(in, iters, out);
       CHECK(hipGetLastError());
       CHECK(hipEventRecord(e1, 0));
       CHECK(hipEventSynchronize(e1));
@@ -111,7 +118,8 @@ int main(int argc, char** argv) {
       const double tf = flops / (ms * 1e-3) / 1e12;
       printf("{\"form\": \"%s\", \"zero_frac\": %.2f, \"rep\": %d, \"ms\": %.2f, \"tflops\": %.1f, "
              "\"frac_of_2516.6\": %.4f, \"clock_ghz_if_busy\": %.3f}\n",
-             form == 0 ? "16x16x32_f16" : "32x32x16_f16", zero_frac, rep, ms, tf, tf / 2516.5824,
+             form == 0 ? "16x16x32_f16" : form == 1 ? "32x32x16_f16" : "16x16x32_f16_stableB", zero_frac, rep, ms,
+             tf, tf / 2516.5824,
              2.4 * tf / 2516.5824);
       fflush(stdout);
     }
