@@ -408,16 +408,23 @@ def pmc_held_clock(key, kernel):
             if json.load(open(path)).get("profile_key") != key:
                 continue
             sq = [r for r in csv.DictReader(open(os.path.join(d, "pmc_sq.csv"))) if kernel in r["kernel"]]
-            st = [r for r in csv.DictReader(open(os.path.join(d, "kernel_stats.csv"))) if kernel in r["Name"]]
+            lg = os.path.join(d, "launch_groups.csv")
+            if os.path.exists(lg):   # the full-size launches (largest grid) of the kernel
+                st = sorted((r for r in csv.DictReader(open(lg)) if kernel in r["kernel"]),
+                            key=lambda r: -int(r["grid_size"]))[:1]
+                ns = float(st[0]["avg_ns"]) if st else None
+            else:
+                st = [r for r in csv.DictReader(open(os.path.join(d, "kernel_stats.csv"))) if kernel in r["Name"]]
+                ns = float(st[0]["AverageNs"]) if st else None
         except (OSError, ValueError, KeyError):
             continue
-        if not sq or not st:
+        if not sq or not ns:
             continue
         g = float(sq[0]["GRBM_GUI_ACTIVE"]) / 8
         busy = float(sq[0]["SQ_VALU_MFMA_BUSY_CYCLES"]) / 1024 / g
-        clock = g / (float(st[0]["AverageNs"]) * 1e-9) / 1e9
+        clock = g / (ns * 1e-9) / 1e9
         return {"mfma_busy": busy, "held_clock_ghz": clock, "frac_ceiling_at_held_clock": clock / 2.4,
-                "source": os.path.relpath(os.path.join(d, "pmc_sq.csv"), REPO)}
+                "avg_launch_ns_rocprof": ns, "source": os.path.relpath(os.path.join(d, "pmc_sq.csv"), REPO)}
     return None
 
 

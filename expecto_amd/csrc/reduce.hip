@@ -236,24 +236,35 @@ __global__ void tss_reduce2_kernel(const float* __restrict__ fwd, const float* _
                                    double* __restrict__ out) {
 #pragma clang fp contract(off)   // products rounded before the sum, as numpy
   extern __shared__ double wsh[];  // [10][n_shift]
-  for (int i = threadIdx.x; i < 10 * n_shift; i += blockDim.x) wsh[i] = weights[i];
-  __syncthreads();
   const int f = 2 * (blockIdx.x * blockDim.x + threadIdx.x);
   const long long g = blockIdx.y;
-  if (f >= nfeat) return;
-  double a0[10], a1[10];
-#pragma unroll
-  for (int k = 0; k < 10; ++k) a0[k] = a1[k] = 0.0;
+  const bool act = f < nfeat;
   const long long h2 = nfeat / 2;
   const float2* pf = reinterpret_cast<const float2*>(fwd + g * n_shift * nfeat + f);
   const float2* pr = reinterpret_cast<const float2*>(rc + g * n_shift * nfeat + f);
-  for (int s0 = 0; s0 < n_shift; s0 += kRedChunk) {   // a chunk's loads first, sums in shift order
-    float2 x[kRedChunk], y[kRedChunk];
+  // round 3: the first chunk's loads go out before the weight staging and its barrier
+  float2 x[kRedChunk], y[kRedChunk];
 #pragma unroll
-    for (int u = 0; u < kRedChunk; ++u) {
-      if (s0 + u < n_shift) {
-        x[u] = pf[(s0 + u) * h2];
-        y[u] = pr[(s0 + u) * h2];
+  for (int u = 0; u < kRedChunk; ++u) {
+    if (act && u < n_shift) {
+      x[u] = pf[u * h2];
+      y[u] = pr[u * h2];
+    }
+  }
+  for (int i = threadIdx.x; i < 10 * n_shift; i += blockDim.x) wsh[i] = weights[i];
+  __syncthreads();
+  if (!act) return;
+  double a0[10], a1[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) a0[k] = a1[k] = 0.0;
+  for (int s0 = 0; s0 < n_shift; s0 += kRedChunk) {   // a chunk's loads first, sums in shift order
+    if (s0 > 0) {
+#pragma unroll
+      for (int u = 0; u < kRedChunk; ++u) {
+        if (s0 + u < n_shift) {
+          x[u] = pf[(s0 + u) * h2];
+          y[u] = pr[(s0 + u) * h2];
+        }
       }
     }
 #pragma unroll

@@ -90,7 +90,9 @@ def main():
     trace = os.path.join(src, f"prof_{a.tag}", "run_kernel_trace.csv")
     if os.path.exists(trace):
         launch_groups(trace, os.path.join(dst, "launch_groups.csv"))
-    sq = per_kernel(os.path.join(src, f"pmc_sq_{a.tag}", "run_counter_collection.csv"))
+    # SQ / GRBM counters of the full-size launches (the held clock and MFMA-busy of a layer's
+    # launch; the alt-delta launches share the kernel)
+    sq = per_kernel(os.path.join(src, f"pmc_sq_{a.tag}", "run_counter_collection.csv"), main_only=True)
     prof_bench = bench_line(os.path.join(src, f"prof_{a.tag}.log"))
     traffic = {}
     with open(os.path.join(dst, "pmc_traffic.csv"), "w", newline="") as f:
