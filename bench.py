@@ -183,6 +183,7 @@ def hbm_reductions(dev):
     plus = rng.integers(0, 2, n_var).astype(bool)
     sh = shift_order(800)
     vout = torch.empty((n_var, 10 * F), dtype=torch.float64, device=dev)
+    vtab = features.variant_tables(dist, plus, sh, dev)   # inputs resident: not part of the timing
     # the headline step's own reduction (geuvadis_sed_for_top_eqtls.py:83-121): one allele of
     # the 96-variant step, float64 fwd/rc mean, legacy 20030 layout
     from expecto_amd import _lib
@@ -195,7 +196,7 @@ def hbm_reductions(dev):
     for name, fn, nbytes in (
             ("fp64_fill_ceiling", lambda: vout.zero_(), n_var * 10 * F * 8),   # write-only reference
             ("tss_reduce", lambda: features.tss_reduce(fwd, rc, w, out), 2 * G * S * F * 4 + G * 10 * F * 8),
-            ("variant_reduce", lambda: features.variant_features(eff, dist, plus, sh, vout),
+            ("variant_reduce", lambda: features.variant_reduce(eff, vtab, vout),
              S9 * n_var * F * 4 + n_var * 10 * F * 8),
             ("sed_shift_reduce_96", sed_reduce, 2 * NS * S * F * 4 + NS * 10 * (F + 1) * 8)):
         fn()
@@ -210,7 +211,7 @@ def hbm_reductions(dev):
         gbs = nbytes / (ms * 1e-3) / 1e9
         res[name] = {"ms": ms, "bytes": nbytes, "GB_per_s": gbs, "peak_GB_per_s": HBM_PEAK_GBS,
                      "frac": gbs / HBM_PEAK_GBS}
-    del fwd, rc, eff, out, vout, sfwd, src, sout
+    del fwd, rc, eff, out, vout, sfwd, src, sout, vtab
     torch.cuda.empty_cache()
     return res
 

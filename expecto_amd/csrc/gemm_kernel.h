@@ -401,6 +401,7 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
   __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)lds_dst, 16, 0, 0);
 }
 
+
 // TM: timing-only probes for tools/gemm_bench (wrong results; production launches TM 0, the
 // producer / consumer conv kernel TM 256): 2 = no LDS-DMA in the loop, 4 = no barrier in the
 // loop, 8 = LDS-DMA always from stage 0's (L2-hot) addresses; beluga_fc_h3p also 16 / 32 = only
@@ -1117,15 +1118,25 @@ __device__ __forceinline__ void gemm_fc_h3w_body(const GemmArgs& p, char* smem) 
   for (int s = 0; s < nk; ++s) {
     const char* base = smem + (s & 1) * FCW_STAGE;
     char* nbase = smem + ((s + 1) & 1) * FCW_STAGE;
-    const bool more = s + 1 < nk && !(TM & 2);
+    // the next stage's pieces are issued unconditionally (the last stage re-fetches its own K block
+    // into the free buffer, drained before the epilogue): a runtime `more` test compiled to a branch
+    // around every piece, and the block boundaries made the LDS-read waits lgkmcnt(0)
+    const int s_next = min(s + 1, nk - 1);
+    constexpr bool more = !(TM & 2);
     read_b(base, 0, b0);
     read_a(base, as);
 #pragma unroll
     for (int nb = 0; nb < FCW_NB; ++nb) {
       const int k = nb * 10 / FCW_NB;                   // units 0, 2, 4, ... issue pieces 0..9
       const bool issue = more && (nb * 10 % FCW_NB) < 10;
-      if (issue) issue_piece(s + 1, nbase, k);
+      if (issue) issue_piece(s_next, nbase, k);
       if (nb + 1 < FCW_NB) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
+      // nothing crosses this point: the next unit's fragment reads stay ahead of this unit's
+      // MFMAs in their own registers.  Without it the scheduler (minimising registers) read
+      // every fragment right before its MFMA into the previous unit's registers, and the
+      // lgkmcnt(0) before each use exposed the full LDS latency (gemm_bench fc1 8192 rows:
+      // 499 vs 474 fp32-eq TF/s; without LDS-DMA 630 vs 533)
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb) acc[mb][nb] = planes_mfma<2>(acc[mb][nb], as[mb], (nb & 1) ? b1 : b0);
       pin(issue ? 1 : 0);

@@ -231,7 +231,7 @@ __device__ __forceinline__ void store_nt2(double* p, double a, double b) {
 // output): float2 loads and double2 stores, so each wave moves 512 B per load instruction and
 // 1 KB per store, and half as many workgroups redo the per-gene weight staging.  Per output the
 // same shift-sequential products and sums: bitwise equal to tss_reduce_kernel.
-__global__ void tss_reduce2_kernel(const float* __restrict__ fwd, const float* __restrict__ rc,
+__global__ __launch_bounds__(1024) void tss_reduce2_kernel(const float* __restrict__ fwd, const float* __restrict__ rc,
                                    const double* __restrict__ weights, int n_shift, int nfeat,
                                    double* __restrict__ out) {
 #pragma clang fp contract(off)   // products rounded before the sum, as numpy
@@ -507,9 +507,12 @@ int expecto_tss_reduce(const float* fwd, const float* rc, const double* weights,
   const bool v2 = nfeat % 2 == 0 && ((reinterpret_cast<uintptr_t>(fwd) | reinterpret_cast<uintptr_t>(rc)) & 7) == 0 &&
                   (reinterpret_cast<uintptr_t>(out) & 15) == 0;
   if (v2) {
-    dim3 grid((nfeat / 2 + 255) / 256, n_genes);
-    tss_reduce2_kernel<<<grid, dim3(256), 10 * n_shift * sizeof(double), as_stream(stream)>>>(fwd, rc, weights,
-                                                                                             n_shift, nfeat, out);
+    // 1024-thread workgroups: one per gene streams whole 8-KB rows (2002 features) and stages the
+    // weights once per gene (tools/reduce_probe: 0.68 vs 0.66 of 8 TB/s for 256 threads; a
+    // loads-and-stores-only kernel of the same pattern reaches 0.68-0.69)
+    dim3 grid((nfeat / 2 + 1023) / 1024, n_genes);
+    tss_reduce2_kernel<<<grid, dim3(1024), 10 * n_shift * sizeof(double), as_stream(stream)>>>(fwd, rc, weights,
+                                                                                              n_shift, nfeat, out);
   } else {
     dim3 grid((nfeat + 255) / 256, n_genes);
     tss_reduce_kernel<<<grid, dim3(256), 10 * n_shift * sizeof(double), as_stream(stream)>>>(fwd, rc, weights, n_shift,

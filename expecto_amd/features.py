@@ -54,16 +54,30 @@ def fwd_rc_average(x: torch.Tensor, out: torch.Tensor | None = None):
 def variant_features(effects: torch.Tensor, dist, strand_plus, shifts, out: torch.Tensor | None = None):
     """effects [S, n, F] fp32 (device, fwd/rc averaged, shift order), dist [n] (pos - TSS),
     strand_plus [n] bool -> [n, 10*F] fp64 (predict.py:87-124 layout: index k*F + f)."""
+    return variant_reduce(effects, variant_tables(dist, strand_plus, shifts, effects.device), out)
+
+
+def variant_tables(dist, strand_plus, shifts, device) -> tuple:
+    """The per-batch inputs of ``variant_reduce`` on the device: dist [n] int64, strand [n] u8,
+    shifts [S] int32 and the host exp table ``decay_table`` (numpy's exp, as the reference)."""
+    d = torch.as_tensor(np.asarray(dist, np.int64), device=device)
+    sp = torch.as_tensor(np.asarray(strand_plus, np.uint8), device=device)
+    sh = torch.as_tensor(np.asarray(list(shifts), np.int32), device=device)
+    lut = torch.from_numpy(decay_table(dist, strand_plus, shifts)).to(device)
+    return d, sp, sh, lut
+
+
+def variant_reduce(effects: torch.Tensor, tables: tuple, out: torch.Tensor | None = None):
+    """``variant_features`` on tables already resident (``variant_tables``): one launch per
+    65,535 variants (the grid's y limit)."""
     lib = _lib.load()
     S, n, F = effects.shape
-    dev = effects.device
+    d, sp, sh, lut = tables
+    if d.shape != (n,) or sp.shape != (n,) or sh.shape != (S,):
+        raise RuntimeError("variant_reduce: table shapes do not match the effects")
     effects = effects.contiguous()
-    d = torch.as_tensor(np.asarray(dist, np.int64), device=dev)
-    sp = torch.as_tensor(np.asarray(strand_plus, np.uint8), device=dev)
-    sh = torch.as_tensor(np.asarray(list(shifts), np.int32), device=dev)
     if out is None:
-        out = torch.empty((n, 10 * F), dtype=torch.float64, device=dev)
-    lut = torch.from_numpy(decay_table(dist, strand_plus, shifts)).to(dev)
+        out = torch.empty((n, 10 * F), dtype=torch.float64, device=effects.device)
     for v0 in range(0, n, 65535):
         v1 = min(n, v0 + 65535)
         eff = effects[:, v0:v1].contiguous() if (v0 or v1 != n) else effects

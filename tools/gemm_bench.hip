@@ -161,7 +161,8 @@ int fc1_bench(int nb, int rounds, int splits, bool toe) {
             {"fcp_x_hotA", fc1p_launch<16>}, {"fcp_x_hotB", fc1p_launch<32>},
             {"fcp_x_hotAB", fc1p_launch<8>}, {"fcp_x_noload", fc1p_launch<2>},
             {"fcw_x", fc1w_launch<0>}, {"fcw_m", fc1w_launch<0>}, {"fcw_g4", fc1w_launch<0>},
-            {"fcw_x_hotB", fc1w_launch<32>}, {"fcw_x_noload", fc1w_launch<2>}};
+            {"fcw_x_hotB", fc1w_launch<32>}, {"fcw_x_noload", fc1w_launch<2>},
+            };
   constexpr int NV = sizeof(vs) / sizeof(vs[0]);
   const size_t csz = (size_t)splits * nb * ldc;
   std::vector<float> ref(csz), out(csz);
