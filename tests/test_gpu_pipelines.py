@@ -344,6 +344,44 @@ def test_chromatin_cli_failed_batch_leaves_no_output(workdir):
     assert left == ["snps_hg19.vcf"], left
 
 
+def test_chromatin_cli_overflowed_batches_are_recomputed(workdir, monkeypatch):
+    """The streamed CLI's f16x3 overflow recovery: with every activation pushed past
+    fp16's range (calibration target 2^20) every 2-variant batch flags; complete() recomputes the
+    flagged variant slices in bf16x6 before the batch's rows are written, so the files equal a
+    bf16x6 run byte for byte and the engine counts one fallback per recomputed slice."""
+    from expecto_amd import chromatin
+    vcf = workdir / "ovf.vcf"
+    with open(vcf, "w") as f:
+        f.write("##fileformat=VCFv4.1\n")
+        f.write(open(os.path.join(GOLDEN, "chromatin_vcf.txt")).read())
+    common = ["--maxshift", "200", "--genome", str(workdir / "hg19.fa"), "--synthetic-weights", "0",
+              "--max-batch", "40", "--variant-batch", "2"]
+    monkeypatch.setenv("EXPECTO_PRECISION", "bf16x6")
+    ref = workdir / "out_bf16x6"
+    chromatin.main([str(vcf), "--output_dir", str(ref)] + common)
+    monkeypatch.setenv("EXPECTO_PRECISION", "f16x3")
+    real, engines = chromatin.load_model, []
+
+    def forced(args):
+        m = real(args)
+        eng = m.engine()
+        eng.set_f16_target(20)
+        engines.append((eng, eng.f16_state()[0]))
+        return m
+    monkeypatch.setattr(chromatin, "load_model", forced)
+    out = workdir / "out_f16_forced"
+    chromatin.main([str(vcf), "--output_dir", str(out)] + common)
+    run = dict(chromatin.LAST_RUN)
+    assert run["batches"] > 1 and run["recomputed_batches"] == run["batches"], run
+    eng, fb0 = engines[0]
+    assert eng.f16_state()[0] - fb0 == run["recomputed_slices"] >= run["batches"], run
+    eng.set_f16_target(10)
+    names = sorted(os.listdir(ref))
+    assert sorted(os.listdir(out)) == names
+    for name in names:
+        assert open(out / name, "rb").read() == open(ref / name, "rb").read(), name
+
+
 def test_chromatin_cli_batch_gb_caps_the_batch():
     """--batch-gb lowers --variant-batch so one batch's y + diff of every shift fits the cap
     (a 201-shift sweep at the default 4096 variants would pin ~79 GB)."""
