@@ -27,7 +27,7 @@ def init(backend: str | None = None):
         if backend is None:
             backend = os.environ.get("EXPECTO_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
-            torch.cuda.set_device(local)
+            torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
         dist.init_process_group(backend=backend)
     return rank, world, local
 
