@@ -77,6 +77,11 @@ Variant mkpp(const char* name) {
           }};
 }
 
+template <int L, int EPI, int TM = 0, int NSB = 4>
+Variant mkp32(const char* name) {
+  return {name, X6P_BM, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3p32<L, EPI, TM, NSB><<<nblk, 512>>>(a); }};
+}
+
 template <int L, int EPI, int MB, int STG, int TM = 0>
 Variant mks3(const char* name) {
   return {name, 64 * MB, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3s<L, EPI, TM, MB, STG><<<nblk, 512>>>(a); }};
@@ -95,6 +100,11 @@ static void fill(float* d, size_t n, float lo, float hi, unsigned seed) {
   std::uniform_real_distribution<float> u(lo, hi);
   for (auto& x : h) x = u(g);
   CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+}
+
+__global__ void relu_inplace(float* d, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) d[i] = fmaxf(d[i], 0.f);
 }
 
 __global__ void hash_fill(float* d, long long n, float lo, float hi, unsigned seed) {
@@ -232,7 +242,10 @@ int main(int argc, char** argv) {
   const size_t csz = (size_t)nb * sh.s_out * sh.cout;
   CK(hipMalloc(&C0, csz * 4));
   CK(hipMalloc(&C1, csz * 6));   // x6q writes bf16 planes (6 B per element)
-  fill(X, xa, 0.f, 1.f, 1);
+  // RELU_X=1: activations like a ReLU layer's output (half of them zero), as the conv layers see
+  const bool relu_x = getenv("RELU_X") != nullptr;
+  fill(X, xa, relu_x ? -1.f : 0.f, 1.f, 1);
+  if (relu_x) relu_inplace<<<(unsigned)((xa + 255) / 256), 256>>>(X, (long long)xa);
   fill(W, (size_t)npad * K, -0.05f, 0.05f, 2);
   fill(bias, npad, -0.1f, 0.1f, 3);
 
@@ -272,6 +285,7 @@ int main(int argc, char** argv) {
     vs.push_back(mks3<2, EPI_RELU_POOL4, 4, 0>("h3s4"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4>("h3p"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 256, 4>("h3p4_pf"));
+    vs.push_back(mkp32<2, EPI_RELU_POOL4, 256, 4>("h3p4_pf_32"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 256 | 8192, 4>("h3p4_pf_oldepi"));
     vs.push_back(mkr3<2, EPI_RELU_POOL4, 8192>("h3r_oldepi"));
     vs.push_back(mkpp<2, EPI_RELU_POOL4>("h3pp"));
@@ -294,6 +308,7 @@ int main(int argc, char** argv) {
     vs.push_back(mks3<3, EPI_RELU, 4, 0>("h3s4"));
     vs.push_back(mkp3<3, EPI_RELU>("h3p"));
     vs.push_back(mkp3<3, EPI_RELU, 256, 4>("h3p4_pf"));
+    vs.push_back(mkp32<3, EPI_RELU, 256, 4>("h3p4_pf_32"));
     vs.push_back(mkp3<3, EPI_RELU, 256 | 8192, 4>("h3p4_pf_oldepi"));
     vs.push_back(mkr3<3, EPI_RELU, 8192>("h3r_oldepi"));
     vs.push_back(mkpp<3, EPI_RELU>("h3pp"));

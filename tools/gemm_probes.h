@@ -987,4 +987,225 @@ __global__ __launch_bounds__(512, 1) void beluga_conv_h3pp(GemmArgs p) {
   gemm_conv_h3pp_body<LAYER, EPI, TM>(p, smem);
 }
 
+
+// ---- timing probe (wrong results): the producer / consumer conv kernel with 32x32x16 MFMAs ----
+// beluga_conv_h3p with each consumer unit's 12 v_mfma_f32_16x16x32_f16 issued as 6
+// v_mfma_f32_32x32x16_f16 on the same fragment registers: the same FLOPs, LDS reads, loads and
+// epilogue (fed the 32x32 accumulators as they lie), so gemm_bench compares the two MFMA forms at
+// equal data movement (MI355X_MICROARCH.md 'DVFS give-back' item 7).
+typedef float floatx16v __attribute__((ext_vector_type(16)));
+template <int LAYER, int EPI, int TM, int NSB>
+__device__ __forceinline__ void gemm_conv_h3p32_body(const GemmArgs& p, char* smem) {
+  static_assert(NSB == 3 || NSB == 4, "B ring depth");
+  // PF (NSB 4): producers keep one stage less in flight, so at the end of stage s the consumers
+  // can already read stage s+1's first B fragments (and, at a chunk's last tap, the next slab's
+  // A fragments) and start it right after the barrier without an LDS round trip.
+  constexpr bool PF = NSB == 4 && (TM & 256) != 0;
+  using G = SlabGeo<4>;
+  constexpr int ROW_KB = 128;
+  constexpr int NAP = (G::PIECES + 3) / 4;            // slab pieces per producer wave and chunk (9)
+  const unsigned nblk = gridDim.x, bid = blockIdx.x;
+  const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
+  const unsigned lin = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int nt = (int)(lin % (unsigned)p.n_tiles);
+  const long long mt = (long long)(lin / (unsigned)p.n_tiles) % p.m_tiles;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const long long m0 = mt * G::BM;
+  const int n0 = nt * GBN;
+  const int kb_total = (int)(p.ldb / GBK);
+  const long long lda_kb = p.lda / GBK;
+  const int nchunk = (int)lda_kb;
+  const int nk = nchunk * 8;
+  auto swz = [](int r) { return conv_swz<TM>(r); };
+  char* const aslab = smem;
+  char* const bring = smem + 2 * G::ASLAB;
+
+  if (wave >= 4) {
+    // ---------------- producer: all LDS-DMA issue ----------------
+    const int pw = wave - 4;
+    const char* Ab = (const char*)p.A + m0 * lda_kb * ROW_KB;
+    const long long last_row = p.M - 1 + 7;
+    unsigned aoff[NAP];
+#pragma unroll
+    for (int i = 0; i < NAP; ++i) {
+      const int P = min(pw + 4 * i, G::PIECES - 1), g = P >> 1, pl = P & 1;
+      const int r = 16 * g + (lane >> 2);
+      const long long m = min(m0 + r, last_row);
+      const int c = (lane & 3) ^ swz(r);
+      aoff[i] = (unsigned)((m - m0) * lda_kb * ROW_KB + pl * 64 + 16 * c);
+    }
+    const char* Bb = (const char*)p.Bp + (long long)n0 * kb_total * ROW_KB;
+    unsigned boff[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int g = pw + 4 * j;
+      const int pl = g / 10, r = 16 * (g % 10) + (lane >> 2);
+      const int c = (lane & 3) ^ swz(r);
+      boff[j] = (unsigned)((long long)r * kb_total * ROW_KB + pl * 64 + 16 * c);
+    }
+    const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, 0x7fffffff, 0x00020000);
+    auto issue_a = [&](int chunk, int i0, int ni) {
+      char* base = aslab + (chunk & 1) * G::ASLAB;
+      const int src_chunk = (TM & 8) ? 0 : chunk;
+      for (int i = i0; i < i0 + ni; ++i) {
+        const int P = min(pw + 4 * i, G::PIECES - 1);
+        char* dst = base + (P & 1) * G::APLANE + (P >> 1) * 1024;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (lds_void*)dst, 16, aoff[i], (unsigned)(src_chunk * ROW_KB), 0, 0);
+      }
+    };
+    auto issue_b = [&](int s, int slot) {
+      if constexpr ((TM & 8) != 0) s = 0;
+      char* base = bring + slot * H3C_BSTAGE;
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + (pw + 4 * j) * 1024), 16, boff[j],
+                                                 (unsigned)(s * ROW_KB), 0, 0);
+    };
+    issue_a(0, 0, NAP);
+    issue_b(0, 0);
+    issue_b(min(1, nk - 1), 1);
+    if constexpr (NSB == 4) {
+      issue_b(min(2, nk - 1), 2);
+      if constexpr (PF)
+        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");    // stages 0 and 1 landed
+      else
+        asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    int slot = 0;
+    for (int c = 0; c < nchunk; ++c) {
+      const bool more_a = (c + 1 < nchunk) && !(TM & 2);
+      for (int t = 0; t < 8; ++t) {
+        const int s = c * 8 + t;
+        const int lslot = slot == 0 ? NSB - 1 : slot - 1;   // stage s+NSB-1's slot (read at s-1)
+        if constexpr (NSB == 3) {     // slab pieces 2,1,1,1,1,1,1,1
+          if (more_a) issue_a(c + 1, t == 0 ? 0 : t + 1, t == 0 ? 2 : (t + 1 < NAP ? 1 : 0));
+        } else {                      // 2,2,2,1,1,1,0,0
+          if (more_a && t < 6) issue_a(c + 1, t < 3 ? 2 * t : t + 3, t < 3 ? 2 : 1);
+        }
+        if (!(TM & 2)) issue_b(min(s + NSB - 1, nk - 1), lslot);
+        // everything but the B pieces of the last NSB-2 stages: B(s+1), and slab c+1 by tap 7
+        // (PF: all but this stage's pieces, so B(s+2) has landed at barrier s and the
+        // consumers read stage s+1's first fragments before that barrier)
+        if constexpr (NSB == 4 && !PF)
+          asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        slot = slot + 1 == NSB ? 0 : slot + 1;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (EPI == EPI_RELU || EPI == EPI_RELU_POOL4) {
+      __builtin_amdgcn_s_barrier();                    // consumers' epilogue reuses the LDS
+    }
+    return;
+  }
+
+  // ---------------- consumer: LDS reads and MFMAs ----------------
+  floatx16v acc32[2][5];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < 5; ++cb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc32[rb][cb][r] = 0.f;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int brow = fr * 64 + 16 * (fq ^ swz(fr));
+  auto read_a = [&](const char* slab, int t, bf16x8 (&a)[4][3]) {
+    const int rr2 = fr + t;
+    const int off = (wave * 64 + rr2) * 64 + 16 * (fq ^ swz(rr2));
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      a[mb][0] = *(const bf16x8*)(slab + off + mb * 1024);
+      a[mb][1] = *(const bf16x8*)(slab + off + mb * 1024 + G::APLANE);
+    }
+  };
+  auto read_b = [&](const char* base, int nb, bf16x8 (&b)[3]) {
+    const char* br = base + brow + nb * 1024;
+    b[0] = *(const bf16x8*)(br);
+    b[1] = *(const bf16x8*)(br + X6P_B_PLANE);
+  };
+  auto pin = [&]() {   // 6 MFMAs of 32 cycles per unit
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+    }
+  };
+  __builtin_amdgcn_s_barrier();                       // slab 0 and B stage 0 landed
+  asm volatile("" ::: "memory");
+  bf16x8 as[4][3];
+  bf16x8 b0[3], b1[3];
+  read_a(aslab, 0, as);
+  if constexpr (PF) read_b(bring, 0, b0);
+  int slot = 0;
+  for (int c = 0; c < nchunk; ++c) {
+    const char* slab = aslab + (c & 1) * G::ASLAB;
+    for (int t = 0; t < 8; ++t) {
+      const char* base = bring + slot * H3C_BSTAGE;
+      const int nslot = slot + 1 == NSB ? 0 : slot + 1;
+      if constexpr (!PF) read_b(base, 0, b0);
+#pragma unroll
+      for (int nb = 0; nb < 10; ++nb) {
+        if (nb + 1 < 10) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {   // unit nb = 2 cb + h: k-half h of column block cb
+          const bf16x8(&b)[3] = (nb & 1) ? b1 : b0;
+          const bf16x8(&a)[3] = as[2 * rb + (nb & 1)];
+          floatx16v& c = acc32[rb][nb >> 1];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(halfx8, a[1]), __builtin_bit_cast(halfx8, b[0]), c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(halfx8, a[0]), __builtin_bit_cast(halfx8, b[1]), c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(halfx8, a[0]), __builtin_bit_cast(halfx8, b[0]), c, 0, 0, 0);
+        }
+        pin();
+      }
+      if (t < 7)
+        read_a(slab, t + 1, as);   // slab reads stay in flight across the barrier
+      else if (PF && c + 1 < nchunk)
+        read_a(aslab + ((c + 1) & 1) * G::ASLAB, 0, as);   // next slab landed by tap 6's barrier
+      if constexpr (PF) {
+        if (c * 8 + t + 1 < nk) read_b(bring + nslot * H3C_BSTAGE, 0, b0);   // stage s+1 landed at barrier s-1
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      slot = nslot;
+    }
+    if (!PF && c + 1 < nchunk) read_a(aslab + ((c + 1) & 1) * G::ASLAB, 0, as);
+  }
+  floatx4v acc[4][10];
+  __builtin_memcpy(acc, acc32, sizeof(acc));
+  if constexpr ((TM & 2048) != 0) {   // timing probe (wrong results): no epilogue, one store per lane
+    __builtin_amdgcn_s_barrier();
+    float t = 0.f;
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 10; ++nb) t += acc[mb][nb][0] + acc[mb][nb][1] + acc[mb][nb][2] + acc[mb][nb][3];
+    p.C[(m0 + wave * 64 + lane) % p.M] = t;
+    return;
+  }
+  if constexpr (EPI == EPI_RELU || EPI == EPI_RELU_POOL4) {
+    __builtin_amdgcn_s_barrier();                     // producers drained their tail pieces
+    if constexpr (EPI == EPI_RELU)
+      epilogue_relu_h2_lds<4, (TM & 8192) == 0>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
+    else
+      epilogue_pool_h2_lds<4, LAYER == 4, (TM & 8192) == 0>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
+  } else {
+    gemm_epilogue16<EPI, 2, 10, 4>(p, acc, m0 + wave * 64, n0, 0, lane);
+  }
+}
+
+
+template <int LAYER, int EPI, int TM = 0, int NSB = 4>
+__global__ __launch_bounds__(512, 1) void beluga_conv_h3p32(GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[h3c_lds<NSB>()];
+  gemm_conv_h3p32_body<LAYER, EPI, TM, NSB>(p, smem);
+}
+
 }  // namespace expecto
