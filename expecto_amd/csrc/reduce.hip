@@ -374,6 +374,60 @@ __global__ void variant_reduce2_kernel(const float* __restrict__ eff, const long
   for (int k = 0; k < 10; ++k) store_nt2(o + (long long)k * nfeat, a0[k], a1[k]);
 }
 
+// The same sums with line-aligned stores.  An output row is 2002 f64 = 16,016 B, not a whole
+// number of 128-B lines, so the per-thread stores above start every 1-KB wave store inside a
+// line: 2 of its 9 lines are partial, each a read-modify-write at the memory, and the stores run
+// at 0.55-0.60 of 8 TB/s where a fill of the same bytes runs at 0.83-0.85
+// (tools/reduce_probe).  Here a 256-pair workgroup keeps its 10 x 2 sums in registers and puts
+// each decay row's 4-KB piece through a double-buffered LDS slot, from which its wave stores
+// start on 128-B lines: only the piece's first and last line are partial.  Same products and
+// sums per output: bitwise equal (probe: 0.63-0.67 vs 0.61-0.64 of 8 TB/s for the kernel above).
+constexpr int kRowsPairs = 256;
+__global__ __launch_bounds__(kRowsPairs) void variant_reduce_rows_kernel(
+    const float* __restrict__ eff, const long long* __restrict__ dist, const uint8_t* __restrict__ strand_plus,
+    const int* __restrict__ shifts, int n_shift, int n, int nfeat, const double* __restrict__ lut, int lut_len,
+    double* __restrict__ out) {
+#pragma clang fp contract(off)   // products rounded before the sum, as numpy
+  extern __shared__ __attribute__((aligned(16))) double rows_lds[];   // [2][256] f64 pairs, then [n_shift][10]
+  double* const wsh = rows_lds + 2 * 2 * kRowsPairs;
+  const long long v = blockIdx.y;
+  const int t = threadIdx.x, pb = blockIdx.x * kRowsPairs;
+  const int np = min(kRowsPairs, nfeat / 2 - pb);
+  variant_weights_lds(dist, strand_plus, shifts, n_shift, v, lut, lut_len, wsh);
+  __syncthreads();
+  double a0[10], a1[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) a0[k] = a1[k] = 0.0;
+  if (t < np) {
+    const int f = 2 * (pb + t);
+    for (int j = 0; j < n_shift; ++j) {
+      const float2 e2 = *reinterpret_cast<const float2*>(eff + ((long long)j * n + v) * nfeat + f);
+      const double e0 = (double)e2.x, e1 = (double)e2.y;
+#pragma unroll
+      for (int k = 0; k < 10; ++k) {
+        a0[k] += e0 * wsh[j * 10 + k];
+        a1[k] += e1 * wsh[j * 10 + k];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    // slot k & 1: the barrier of row k+1 orders every thread's reads of row k-1 before its reuse
+    double* const sb = rows_lds + (k & 1) * 2 * kRowsPairs;
+    if (t < np) *reinterpret_cast<f64x2*>(sb + 2 * t) = f64x2{a0[k], a1[k]};
+    __syncthreads();
+    double* const row = out + (v * 10 + k) * (long long)nfeat + 2 * pb;
+    const int lead = (int)(((unsigned long long)(size_t)row & 127) >> 4);   // 16-B slots before its line
+    for (int s = t; s < lead + np; s += kRowsPairs) {
+      const int piece = s - lead;
+      if (piece >= 0) {
+        const f64x2 x = *reinterpret_cast<const f64x2*>(sb + 2 * piece);
+        store_nt2(row + 2 * piece, x.x, x.y);
+      }
+    }
+  }
+}
+
 }  // namespace expecto
 
 using namespace expecto;
@@ -530,7 +584,14 @@ int expecto_variant_reduce_lut(const float* effects, const long long* dist, cons
   EXPECTO_REQUIRE(effects && dist && strand_plus && shifts && out, "null argument");
   EXPECTO_REQUIRE(!exp_lut || lut_len > 0, "empty exp table");
   const size_t shm = 10 * (size_t)n_shift * sizeof(double);
-  if (nfeat % 2 == 0 && (reinterpret_cast<uintptr_t>(effects) & 7) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+  const bool v2 =
+      nfeat % 2 == 0 && (reinterpret_cast<uintptr_t>(effects) & 7) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+  const size_t shm_rows = shm + 2 * 2 * kRowsPairs * sizeof(double);
+  if (v2 && shm_rows <= 65536) {   // <= 716 shifts (the reference sweeps 9)
+    dim3 grid((nfeat / 2 + kRowsPairs - 1) / kRowsPairs, n);
+    variant_reduce_rows_kernel<<<grid, dim3(kRowsPairs), shm_rows, as_stream(stream)>>>(
+        effects, dist, strand_plus, shifts, n_shift, n, nfeat, exp_lut, lut_len, out);
+  } else if (v2) {
     dim3 grid((nfeat / 2 + 255) / 256, n);
     variant_reduce2_kernel<<<grid, dim3(256), shm, as_stream(stream)>>>(effects, dist, strand_plus, shifts, n_shift, n,
                                                                       nfeat, exp_lut, lut_len, out);

@@ -35,8 +35,10 @@ def test_tss_reduce_matches_oracle_and_scalar_kernel(nfeat, S):
         np.testing.assert_array_equal(out[g], tss_ref(f[g], r[g], wn))
 
 
-@pytest.mark.parametrize("nfeat", [2002, 37])
+@pytest.mark.parametrize("nfeat", [2002, 37, 8, 1000])
 def test_variant_features_match_oracle_and_scalar_kernel(nfeat):
+    """2002 / 8 / 1000: the row-staged kernel (one or two 256-pair workgroups per variant, ragged
+    last workgroup, pieces shorter than a line); 37: the scalar kernel."""
     from expecto_amd.features import variant_features
     from oracle.reduce_np import variant_reduce, variant_weights
     rng = np.random.default_rng(4)
@@ -62,6 +64,21 @@ def test_variant_features_beyond_32_shifts():
     rng = np.random.default_rng(5)
     shifts = shift_order(5000)                      # 51 shifts
     n, nfeat = 40, 2002
+    eff = rng.standard_normal((len(shifts), n, nfeat)).astype(np.float32)
+    dist = rng.integers(-30000, 30000, n)
+    strand = rng.random(n) < 0.5
+    out = variant_features(torch.from_numpy(eff).cuda(), dist, strand, shifts).cpu().numpy()
+    np.testing.assert_array_equal(out, variant_reduce(list(eff), variant_weights(dist, strand, shifts), nfeat))
+
+
+def test_variant_features_past_the_row_kernels_lds():
+    """720 shifts: the weight table and the row slots exceed 64 KB of LDS, so the 2-feature
+    kernel without row staging runs; the same bits as the oracle."""
+    from expecto_amd.features import variant_features
+    from oracle.reduce_np import variant_reduce, variant_weights
+    rng = np.random.default_rng(7)
+    shifts = [200 * (i // 2) * (1 if i % 2 else -1) for i in range(720)]
+    n, nfeat = 3, 2002
     eff = rng.standard_normal((len(shifts), n, nfeat)).astype(np.float32)
     dist = rng.integers(-30000, 30000, n)
     strand = rng.random(n) < 0.5

@@ -495,6 +495,58 @@ __global__ __launch_bounds__(256) void variant_rowstage(const float* __restrict_
     }
   }
 }
+
+// variant, one 1024-thread workgroup per variant (thread = feature pair): the 10 sums per thread
+// stay in registers; row k goes through a triple-buffered 16-KB LDS slot and is written by a
+// sweep over the 128-B lines between row k's first line and row k+1's first line, the line that
+// straddles rows k-1 and k taking row k-1's tail from its slot: a variant's 160,160 contiguous
+// output bytes are written in whole lines except the two at its ends.  One barrier per row.
+__global__ __launch_bounds__(1024) void variant_vrow(const float* __restrict__ eff, const long long* __restrict__ dist,
+                                                     const uint8_t* __restrict__ strand_plus,
+                                                     const int* __restrict__ shifts, int n_shift, int n, int nfeat,
+                                                     const double* __restrict__ lut, int lut_len,
+                                                     double* __restrict__ out) {
+#pragma clang fp contract(off)
+  __shared__ __attribute__((aligned(16))) double stage[3][2 * 1024];
+  extern __shared__ double wsh[];
+  const long long v = blockIdx.x;
+  const int t = threadIdx.x, pairs = nfeat / 2;
+  variant_weights_lds(dist, strand_plus, shifts, n_shift, v, lut, lut_len, wsh);
+  __syncthreads();
+  double a0[10], a1[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) a0[k] = a1[k] = 0.0;
+  if (t < pairs) {
+    const int f = 2 * t;
+    for (int j = 0; j < n_shift; ++j) {
+      const float2 e2 = *reinterpret_cast<const float2*>(eff + ((long long)j * n + v) * nfeat + f);
+      const double e0 = (double)e2.x, e1 = (double)e2.y;
+#pragma unroll
+      for (int k = 0; k < 10; ++k) {
+        a0[k] += e0 * wsh[j * 10 + k];
+        a1[k] += e1 * wsh[j * 10 + k];
+      }
+    }
+  }
+  double* const vbase = out + v * 10LL * nfeat;            // 16-B aligned; rows of `pairs` pieces
+  const long long lead0 = ((long long)(size_t)vbase & 127) >> 4;   // pieces before the first line
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    if (t < pairs) *reinterpret_cast<f64x2*>(stage[k % 3] + 2 * t) = f64x2{a0[k], a1[k]};
+    __syncthreads();
+    // this sweep: variant pieces [q0, q1) with q the piece index from the variant's start;
+    // line-aligned except q0 = 0 (k = 0) and q1 = 10 * pairs (k = 9)
+    const long long rk = (long long)k * pairs;
+    const long long q0 = k == 0 ? 0 : ((rk + lead0) & ~7LL) - lead0;
+    const long long q1 = k == 9 ? 10LL * pairs : ((rk + pairs + lead0) & ~7LL) - lead0;
+    for (long long q = q0 + t; q < q1; q += 1024) {
+      const long long r = q - rk;                            // < 0: row k-1's tail
+      const double* src = r < 0 ? stage[(k + 2) % 3] + 2 * (r + pairs) : stage[k % 3] + 2 * r;
+      const f64x2 x = *reinterpret_cast<const f64x2*>(src);
+      store_nt2(vbase + 2 * q, x.x, x.y);
+    }
+  }
+}
 }  // namespace probe
 
 __global__ void hash_fill(float* d, long long n, unsigned seed) {
@@ -623,6 +675,8 @@ int main(int argc, char** argv) {
        [&] { probe::write_rows_stride<<<dim3(4, NV * 1001 / 1536), 256>>>(vout_b, 1536); }},
       {"variant rowstage", var_bytes, vout_b, vout_a, (size_t)NV * 10 * F,
        [&] { probe::variant_rowstage<<<dim3(4, NV), 256, S9 * 10 * 8>>>(eff, dist, plus, shifts, S9, NV, F, lut, lut_len, vout_b); }},
+      {"variant vrow", var_bytes, vout_b, vout_a, (size_t)NV * 10 * F,
+       [&] { probe::variant_vrow<<<NV, 1024, S9 * 10 * 8>>>(eff, dist, plus, shifts, S9, NV, F, lut, lut_len, vout_b); }},
       {"variant lds aligned", var_bytes, vout_b, vout_a, (size_t)NV * 10 * F,
        [&] { probe::variant_lds<true><<<dim3(2, NV), 512>>>(eff, dist, plus, shifts, S9, NV, F, lut, lut_len, vout_b); }},
       {"variant lds aligned (no math)", var_bytes, vout_b, nullptr, 0,
