@@ -547,6 +547,51 @@ __global__ __launch_bounds__(1024) void variant_vrow(const float* __restrict__ e
     }
   }
 }
+
+// sed reduction (shift_reduce_kernel<true, true>) with the 10 decay rows split over KS threads:
+// KS x the waves of the 96 x 2002-thread grid (3 waves per SIMD), each loading every shift (the
+// repeats hit L2) and summing its 10 / KS rows in the same shift order: bitwise equal
+template <int KS>
+__global__ void shift_reduce_ks(const float* __restrict__ fwd, const float* __restrict__ rc,
+                                const double* __restrict__ weights, int n_shift, int nfeat, double* __restrict__ out) {
+#pragma clang fp contract(off)
+  extern __shared__ double wsx[];
+  for (int i = threadIdx.x; i < 10 * n_shift; i += blockDim.x) wsx[i] = weights[i];
+  __syncthreads();
+  constexpr int KN = 10 / KS;
+  const int ks = blockIdx.z;
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  const long long g = blockIdx.y;
+  double* o = out + g * 10LL * (nfeat + 1);
+  if (f < KN && ks == 0) {
+    for (int k = 0; k < 10; ++k) if (k % KN == f) o[(long long)k * (nfeat + 1)] = 0.0;
+  }
+  if (f >= nfeat) return;
+  double acc[KN];
+#pragma unroll
+  for (int k = 0; k < KN; ++k) acc[k] = 0.0;
+  const float* pf = fwd + g * n_shift * nfeat + f;
+  const float* pr = rc + g * n_shift * nfeat + f;
+  constexpr int CH = 8;
+  for (int s0 = 0; s0 < n_shift; s0 += CH) {
+    float a[CH], b[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u)
+      if (s0 + u < n_shift) {
+        a[u] = pf[(long long)(s0 + u) * nfeat];
+        b[u] = pr[(long long)(s0 + u) * nfeat];
+      }
+#pragma unroll
+    for (int u = 0; u < CH; ++u)
+      if (s0 + u < n_shift) {
+        const double pd = ((double)a[u] + (double)b[u]) / 2.0;
+#pragma unroll
+        for (int k = 0; k < KN; ++k) acc[k] += wsx[(ks * KN + k) * n_shift + s0 + u] * pd;
+      }
+  }
+#pragma unroll
+  for (int k = 0; k < KN; ++k) o[(long long)(ks * KN + k) * (nfeat + 1) + 1 + f] = acc[k];
+}
 }  // namespace probe
 
 __global__ void hash_fill(float* d, long long n, unsigned seed) {
@@ -641,6 +686,8 @@ int main(int argc, char** argv) {
        [&] { probe::tss_bs<1024><<<dim3(1, G), 1024, 10 * S * 8>>>(fwd, rc, w, S, F, out_b); }},
       {"tss bs128", tss_bytes, out_b, out_a, (size_t)G * 10 * F,
        [&] { probe::tss_bs<128><<<dim3((F / 2 + 127) / 128, G), 128, 10 * S * 8>>>(fwd, rc, w, S, F, out_b); }},
+      {"variant per-thread stores (r02)", var_bytes, vout_b, vout_a, (size_t)NV * 10 * F,
+       [&] { probe::variant_bs<256><<<dim3((F / 2 + 255) / 256, NV), 256, S9 * 10 * 8>>>(eff, dist, plus, shifts, S9, NV, F, lut, lut_len, vout_b); }},
       {"variant bs512", var_bytes, vout_b, vout_a, (size_t)NV * 10 * F,
        [&] { probe::variant_bs<512><<<dim3((F / 2 + 511) / 512, NV), 512, S9 * 10 * 8>>>(eff, dist, plus, shifts, S9, NV, F, lut, lut_len, vout_b); }},
       {"variant bs1024", var_bytes, vout_b, vout_a, (size_t)NV * 10 * F,
@@ -683,6 +730,10 @@ int main(int argc, char** argv) {
        [&] { probe::variant_lds<false><<<dim3(2, NV), 512>>>(eff, dist, plus, shifts, S9, NV, F, lut, lut_len, vout_b); }},
       {"sed library (96)", sed_bytes, out_a, nullptr, 0,
        [&] { expecto_shift_reduce(fwd, rc, w, NSED, S, F, 3, out_a, nullptr); }},
+      {"sed k-split 2", sed_bytes, out_b, out_a, (size_t)NSED * 10 * (F + 1),
+       [&] { probe::shift_reduce_ks<2><<<dim3((F + 255) / 256, NSED, 2), 256, 10 * S * 8>>>(fwd, rc, w, S, F, out_b); }},
+      {"sed k-split 5", sed_bytes, out_b, out_a, (size_t)NSED * 10 * (F + 1),
+       [&] { probe::shift_reduce_ks<5><<<dim3((F + 255) / 256, NSED, 5), 256, 10 * S * 8>>>(fwd, rc, w, S, F, out_b); }},
   };
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
