@@ -285,7 +285,7 @@ int main(int argc, char** argv) {
     vs.push_back(mks3<2, EPI_RELU_POOL4, 4, 0>("h3s4"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4>("h3p"));
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 256, 4>("h3p4_pf"));
-    vs.push_back(mkp32<2, EPI_RELU_POOL4, 256, 4>("h3p4_pf_32"));
+
     vs.push_back(mkp3<2, EPI_RELU_POOL4, 256 | 8192, 4>("h3p4_pf_oldepi"));
     vs.push_back(mkr3<2, EPI_RELU_POOL4, 8192>("h3r_oldepi"));
     vs.push_back(mkpp<2, EPI_RELU_POOL4>("h3pp"));
@@ -308,7 +308,6 @@ int main(int argc, char** argv) {
     vs.push_back(mks3<3, EPI_RELU, 4, 0>("h3s4"));
     vs.push_back(mkp3<3, EPI_RELU>("h3p"));
     vs.push_back(mkp3<3, EPI_RELU, 256, 4>("h3p4_pf"));
-    vs.push_back(mkp32<3, EPI_RELU, 256, 4>("h3p4_pf_32"));
     vs.push_back(mkp3<3, EPI_RELU, 256 | 8192, 4>("h3p4_pf_oldepi"));
     vs.push_back(mkr3<3, EPI_RELU, 8192>("h3r_oldepi"));
     vs.push_back(mkpp<3, EPI_RELU>("h3pp"));
