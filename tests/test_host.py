@@ -137,3 +137,26 @@ def test_inputsize_other_than_2000_is_rejected(tmp_path):
     from expecto_amd import tss
     with pytest.raises(ValueError):
         tss.replicate_main([str(tmp_path / "a.csv"), "--windowsize", "1000"])
+
+
+def test_variant_tables_and_decay_table_follow_predict_py():
+    """features.variant_tables (the per-batch inputs the variant reduction keeps resident; the
+    bench times the kernel on them) on the CPU: dtypes the C-ABI binds and the exp table equal
+    to numpy's exp of predict.py:88-107's arguments for every floor(|d|/200) of the batch."""
+    import torch
+    from expecto_amd.features import DECAY, decay_table, variant_tables
+    from expecto_amd.pipeline import shift_order
+    rng = np.random.default_rng(8)
+    dist = rng.integers(-40000, 40000, 50)
+    plus = rng.random(50) < 0.5
+    shifts = shift_order(800)
+    d, sp, sh, lut = variant_tables(dist, plus, shifts, torch.device("cpu"))
+    assert (d.dtype, sp.dtype, sh.dtype, lut.dtype) == (torch.int64, torch.uint8, torch.int32, torch.float64)
+    assert d.tolist() == dist.tolist() and sp.tolist() == plus.astype(np.uint8).tolist() and sh.tolist() == shifts
+    tab = decay_table(dist, plus, shifts)
+    assert np.array_equal(lut.numpy(), tab)
+    sgn = np.where(plus, 1, -1)
+    fl = np.floor(np.abs(dist[:, None] * sgn[:, None] + np.asarray(shifts)[None] * sgn[:, None]) / 200.0)
+    assert tab.shape[1] == int(fl.max()) + 1
+    for k, c in enumerate(DECAY):
+        np.testing.assert_array_equal(tab[k][fl.astype(int)], np.exp(-c * fl))
