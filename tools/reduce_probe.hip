@@ -592,6 +592,38 @@ __global__ void shift_reduce_ks(const float* __restrict__ fwd, const float* __re
 #pragma unroll
   for (int k = 0; k < KN; ++k) o[(long long)(ks * KN + k) * (nfeat + 1) + 1 + f] = acc[k];
 }
+
+// TSS read pattern with a row stride of `ld` floats (ld = nfeat: the real [G][200][2002] layout,
+// rows 8,008 B apart, starting inside 128-B lines; ld = 2048: every row line-aligned)
+__global__ void tss_pattern_ld(const float* __restrict__ fwd, const float* __restrict__ rc, int n_shift, int nfeat,
+                               int ld, double* __restrict__ out) {
+  const int f = 2 * (blockIdx.x * blockDim.x + threadIdx.x);
+  const long long g = blockIdx.y;
+  if (f >= nfeat) return;
+  const long long h2 = ld / 2;
+  const float2* pf = reinterpret_cast<const float2*>(fwd + g * n_shift * (long long)ld + f);
+  const float2* pr = reinterpret_cast<const float2*>(rc + g * n_shift * (long long)ld + f);
+  float sx = 0.f, sy = 0.f;
+  constexpr int CH = 8;
+  for (int s0 = 0; s0 < n_shift; s0 += CH) {
+    float2 x[CH], y[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u)
+      if (s0 + u < n_shift) {
+        x[u] = pf[(s0 + u) * h2];
+        y[u] = pr[(s0 + u) * h2];
+      }
+#pragma unroll
+    for (int u = 0; u < CH; ++u)
+      if (s0 + u < n_shift) {
+        sx += x[u].x + y[u].x;
+        sy += x[u].y + y[u].y;
+      }
+  }
+  double* o = out + g * 10LL * nfeat + f;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) store_nt2(o + (long long)k * nfeat, sx + k, sy + k);
+}
 }  // namespace probe
 
 __global__ void hash_fill(float* d, long long n, unsigned seed) {
@@ -665,6 +697,10 @@ int main(int argc, char** argv) {
        [&] { probe::tss_pattern<8><<<tgrid, 256>>>(fwd, rc, S, F, out_b); }},
       {"tss pattern ch16 (no math)", tss_bytes, out_b, nullptr, 0,
        [&] { probe::tss_pattern<16><<<tgrid, 256>>>(fwd, rc, S, F, out_b); }},
+      {"tss pattern ld 2002 (real)", tss_bytes, out_b, nullptr, 0,
+       [&] { probe::tss_pattern_ld<<<dim3((F / 2 + 1023) / 1024, G), 1024>>>(fwd, rc, S, F, F, out_b); }},
+      {"tss pattern ld 2048 (lines)", tss_bytes * 977.0 / 1000.0, out_b, nullptr, 0,
+       [&] { probe::tss_pattern_ld<<<dim3((F / 2 + 1023) / 1024, 977), 1024>>>(fwd, rc, S, F, 2048, out_b); }},
       {"tss pipe ch8", tss_bytes, out_b, out_a, (size_t)G * 10 * F,
        [&] { probe::tss_pipe<8><<<tgrid, 256, 10 * S * 8>>>(fwd, rc, w, S, F, out_b); }},
       {"tss pipe ch4", tss_bytes, out_b, out_a, (size_t)G * 10 * F,
@@ -684,6 +720,8 @@ int main(int argc, char** argv) {
        [&] { probe::tss_bs<512><<<dim3((F / 2 + 511) / 512, G), 512, 10 * S * 8>>>(fwd, rc, w, S, F, out_b); }},
       {"tss bs1024", tss_bytes, out_b, out_a, (size_t)G * 10 * F,
        [&] { probe::tss_bs<1024><<<dim3(1, G), 1024, 10 * S * 8>>>(fwd, rc, w, S, F, out_b); }},
+      {"tss library (late in the round)", tss_bytes, out_b, nullptr, 0,
+       [&] { expecto_tss_reduce(fwd, rc, w, G, S, F, out_b, nullptr); }},
       {"tss bs128", tss_bytes, out_b, out_a, (size_t)G * 10 * F,
        [&] { probe::tss_bs<128><<<dim3((F / 2 + 127) / 128, G), 128, 10 * S * 8>>>(fwd, rc, w, S, F, out_b); }},
       {"variant per-thread stores (r02)", var_bytes, vout_b, vout_a, (size_t)NV * 10 * F,
