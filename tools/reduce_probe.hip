@@ -451,17 +451,18 @@ __global__ __launch_bounds__(512) void variant_lds(const float* __restrict__ eff
 // sums in registers, and for each decay row k puts its 4-KB piece of the row through an 8-KB
 // double-buffered LDS slot and writes it with wave stores that start on 128-B lines (only the
 // piece's first and last line partial, instead of 2 of every wave store's 9 lines)
-__global__ __launch_bounds__(256) void variant_rowstage(const float* __restrict__ eff, const long long* __restrict__ dist,
+template <int PB = 256>
+__global__ __launch_bounds__(PB) void variant_rowstage(const float* __restrict__ eff, const long long* __restrict__ dist,
                                                         const uint8_t* __restrict__ strand_plus,
                                                         const int* __restrict__ shifts, int n_shift, int n, int nfeat,
                                                         const double* __restrict__ lut, int lut_len,
                                                         double* __restrict__ out) {
 #pragma clang fp contract(off)
-  __shared__ __attribute__((aligned(16))) double stage[2][2 * 256];
+  __shared__ __attribute__((aligned(16))) double stage[2][2 * PB];
   extern __shared__ double wsh[];
   const long long v = blockIdx.y;
-  const int t = threadIdx.x, pb = blockIdx.x * 256;
-  const int pairs = nfeat / 2, np = min(256, pairs - pb);
+  const int t = threadIdx.x, pb = blockIdx.x * PB;
+  const int pairs = nfeat / 2, np = min(PB, pairs - pb);
   variant_weights_lds(dist, strand_plus, shifts, n_shift, v, lut, lut_len, wsh);
   __syncthreads();
   double a0[10], a1[10];
@@ -486,7 +487,7 @@ __global__ __launch_bounds__(256) void variant_rowstage(const float* __restrict_
     __syncthreads();
     double* row = out + (v * 10 + k) * (long long)nfeat + 2 * pb;
     const int lead = (int)(((long long)(size_t)row & 127) >> 4);
-    for (int s = t; s < lead + np; s += 256) {
+    for (int s = t; s < lead + np; s += PB) {
       const int piece = s - lead;
       if (piece >= 0) {
         const f64x2 x = *reinterpret_cast<const f64x2*>(sb + 2 * piece);
@@ -759,7 +760,11 @@ int main(int argc, char** argv) {
       {"rows stride 1536", (double)(NV * 1001LL / 1536) * 10 * F * 8, vout_b, nullptr, 0,
        [&] { probe::write_rows_stride<<<dim3(4, NV * 1001 / 1536), 256>>>(vout_b, 1536); }},
       {"variant rowstage", var_bytes, vout_b, vout_a, (size_t)NV * 10 * F,
-       [&] { probe::variant_rowstage<<<dim3(4, NV), 256, S9 * 10 * 8>>>(eff, dist, plus, shifts, S9, NV, F, lut, lut_len, vout_b); }},
+       [&] { probe::variant_rowstage<256><<<dim3(4, NV), 256, S9 * 10 * 8>>>(eff, dist, plus, shifts, S9, NV, F, lut, lut_len, vout_b); }},
+      {"variant rowstage 512", var_bytes, vout_b, vout_a, (size_t)NV * 10 * F,
+       [&] { probe::variant_rowstage<512><<<dim3(2, NV), 512, S9 * 10 * 8>>>(eff, dist, plus, shifts, S9, NV, F, lut, lut_len, vout_b); }},
+      {"variant rowstage 128", var_bytes, vout_b, vout_a, (size_t)NV * 10 * F,
+       [&] { probe::variant_rowstage<128><<<dim3(8, NV), 128, S9 * 10 * 8>>>(eff, dist, plus, shifts, S9, NV, F, lut, lut_len, vout_b); }},
       {"variant vrow", var_bytes, vout_b, vout_a, (size_t)NV * 10 * F,
        [&] { probe::variant_vrow<<<NV, 1024, S9 * 10 * 8>>>(eff, dist, plus, shifts, S9, NV, F, lut, lut_len, vout_b); }},
       {"variant lds aligned", var_bytes, vout_b, vout_a, (size_t)NV * 10 * F,
