@@ -1178,8 +1178,12 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
         beluga_conv_h3p<LAYER, EPI, 256, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
     } else if constexpr (EPI == EPI_PARTIAL) {
       // FC split-K partials: 336-column tiles on 8 MFMA waves when the caller tiled N that way
-      // (fc_wide_tiles), else 160-column producer / consumer tiles (same bits either way)
-      if ((long long)a.n_tiles * FCW_BN >= a.n_store && (long long)(a.n_tiles - 1) * FCW_BN < a.n_store)
+      // (n_tile_cols, set from fc_wide_tiles), else 160-column producer / consumer tiles (same
+      // bits either way)
+      EXPECTO_REQUIRE(a.n_tile_cols == 0 || a.n_tile_cols == FCW_BN, "FC tile width: 0 (160) or 336 columns");
+      EXPECTO_REQUIRE((long long)a.n_tiles * (a.n_tile_cols ? a.n_tile_cols : GBN) >= a.n_store,
+                      "FC N tiles do not cover the stored columns");
+      if (a.n_tile_cols == FCW_BN)
         beluga_fc_h3w<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
       else
         beluga_fc_h3p<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
@@ -1308,6 +1312,7 @@ int run_fc1(expecto_beluga* h, const float* act, const long long* a_rows, int nb
     if (wide) {   // 336-column tiles: N fastest per XCD (orders measured equal within 1 %)
       a.m_fastest = 0;
       a.linear_order = 0;
+      a.n_tile_cols = FCW_BN;
     }
     a.C = h->part;
     a.ldc = kHidLd;
@@ -1356,7 +1361,10 @@ int run_fc2(expecto_beluga* h, const float* h1, int nb, float* y, hipStream_t st
     // the 13 N tiles of its A tiles back to back) for the large unsplit launches of the segment
     // path, whose h1 rows (up to fc2_rows x 8 KB) would otherwise be streamed once per N tile
     a.m_fastest = (double)m_tiles * gemm_bm() * (kHidLd / h->fc2_splits) * 4.0 <= h->fc1_m_order_mb * (1 << 20) ? 1 : 0;
-    if (wide) a.m_fastest = 0;
+    if (wide) {
+      a.m_fastest = 0;
+      a.n_tile_cols = FCW_BN;
+    }
     a.C = h->part2;
     a.ldc = kHidLd;
     a.n_store = kNFeat;

@@ -51,6 +51,8 @@ struct GemmArgs {
   const unsigned* ks_mask;  // split-K planes GEMM: bit ks of ks_mask[m_tile] = compute that slab
                             // (others keep the partials already in C: alt FC1 of SNV pairs)
   int m_group;              // FC m_fastest 3: M tiles per dispatch group (see gemm_fc_h3p_body)
+  int n_tile_cols;          // f16x3 split-K FC: columns per N tile the caller tiled for (FCW_BN:
+                            // beluga_fc_h3w; 0 = the 160-column kernels)
 };
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));

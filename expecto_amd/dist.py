@@ -17,6 +17,21 @@ def env_rank():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
 
 
+def local_device(local: int) -> int:
+    """The GPU of local rank ``local``: one rank per GPU.  A local rank beyond the visible devices
+    (HIP_VISIBLE_DEVICES narrower than --nproc-per-node) is a launch error and raises, instead of
+    silently putting two ranks on one GPU (RCCL also rejects duplicate GPUs in a communicator).
+    EXPECTO_SHARE_GPUS=1 opts into sharing (local % visible): the multi-rank rehearsals over gloo
+    on a one-GPU box."""
+    n = torch.cuda.device_count()
+    if 0 <= local < n:
+        return local
+    if n > 0 and os.environ.get("EXPECTO_SHARE_GPUS") == "1":
+        return local % n
+    raise RuntimeError(f"local rank {local} has no GPU of its own ({n} visible); launch one rank per GPU "
+                       f"(or set EXPECTO_SHARE_GPUS=1 to rehearse several ranks on one GPU)")
+
+
 def init(backend: str | None = None):
     """Initialise the process group when launched with WORLD_SIZE > 1; returns (rank, world, local).
     Backend: the argument, else $EXPECTO_DIST_BACKEND, else "nccl" (RCCL) on a GPU, "gloo" on CPU."""
@@ -27,7 +42,7 @@ def init(backend: str | None = None):
         if backend is None:
             backend = os.environ.get("EXPECTO_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
-            torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+            torch.cuda.set_device(local_device(local))
         dist.init_process_group(backend=backend)
     return rank, world, local
 

@@ -184,6 +184,11 @@ class RowWriter:
         while done < len(mv):
             done += os.pwrite(self.fd, mv[done:], off + done)
 
+    def sync(self) -> None:
+        """fsync: the header and size reach the file system before other processes attach."""
+        import os
+        os.fsync(self.fd)
+
     def close(self) -> None:
         import os
         if self.fd is not None:

@@ -66,7 +66,7 @@ def match_counts(fasta, vs: VariantSet):
     """(ref_matched, alt_matched) booleans of chromatin.py:207-208 (window-independent)."""
     rm, am = [], []
     for c, p, r, a in zip(vs.chrom, vs.pos, vs.ref, vs.alt):
-        g = fasta.raw(c)[int(p) - 1:int(p) - 1 + len(r)].decode("latin-1").upper()
+        g = bytes(fasta.raw(c)[int(p) - 1:int(p) - 1 + len(r)]).decode("latin-1").upper()
         rm.append(g == r.upper())
         am.append(g == a.upper())
     return np.array(rm, bool), np.array(am, bool)
@@ -334,8 +334,9 @@ class VariantPipeline:
         rerun it in f16x3 as `parts` variant slices with one flag each -- an output row depends
         only on its own window, so the rerun reproduces the batch's bits and only locates the
         overflow -- then recompute just the flagged slices in bf16x6 into `out`.  Cost 1 + 2f
-        batch-times for a flagged fraction f, against 2 for the whole batch.  Returns the number
-        of slices recomputed (each counted by the engine's fallback counter)."""
+        batch-times for a flagged fraction f, against 2 for the whole batch.  If no slice flags
+        again, the whole batch is recomputed in bf16x6 (counted once).  Returns the number of
+        slices recomputed (each flagged slice counted by the engine's fallback counter)."""
         eng = self.engine
         n = len(vs)
         if n == 0:
@@ -360,6 +361,14 @@ class VariantPipeline:
             out.narrow(dim, int(bounds[i]), int(bounds[i + 1] - bounds[i])).copy_(y)
             eng.count_fallback()
             redone += 1
+        if redone == 0:
+            # the batch flagged but no slice rerun did: the rerun did not reproduce the batch's
+            # launches (a launch-size dependence of some kernel), so the overflowed rows are not
+            # located -- recompute the whole batch in bf16x6 rather than release them
+            with eng.precision_override("bf16x6"):
+                self.predict(self.prepare(vs, shifts, rows), out=out)
+            eng.count_fallback()
+            redone = k
         return redone
 
     def sed_features(self, y: torch.Tensor, weights: torch.Tensor, out: torch.Tensor | None = None,

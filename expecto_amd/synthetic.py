@@ -78,6 +78,65 @@ def write_fasta(path: str, genome: dict, width: int = 60) -> None:
                 f.write(seq[i:i + width] + b"\n")
 
 
+HG19_LENGTHS = {   # hg19 chr1..chr22, chrX, chrY (3,095,677,412 bp): the size of the real genome
+    "chr1": 249250621, "chr2": 243199373, "chr3": 198022430, "chr4": 191154276, "chr5": 180915260,
+    "chr6": 171115067, "chr7": 159138663, "chr8": 146364022, "chr9": 141213431, "chr10": 135534747,
+    "chr11": 135006516, "chr12": 133851895, "chr13": 115169878, "chr14": 107349540, "chr15": 102531392,
+    "chr16": 90354753, "chr17": 81195210, "chr18": 78077248, "chr19": 59128983, "chr20": 63025520,
+    "chr21": 48129895, "chr22": 51304566, "chrX": 155270560, "chrY": 59373566}
+
+
+class TiledGenome:
+    """A genome of hg19's size written fast: every contig is a line-aligned rotation of one
+    seeded ``block`` of bases (i.i.d. A/C/G/T, 10 % lowercase, 1 % N), so a multi-GB FASTA
+    costs one block of random numbers and the file write.  ``base(chrom, pos1)`` gives the
+    base at a 1-based position (for SNVs whose ref matches the genome)."""
+
+    def __init__(self, lengths: dict | None = None, block_lines: int = 1 << 18, width: int = 60, seed: int = 0):
+        rng = np.random.default_rng(seed)
+        nb = block_lines * width
+        s = _BASES[rng.integers(0, 4, nb)]
+        s = np.where(rng.random(nb) < 0.10, s + 32, s).astype(np.uint8)
+        s = np.where(rng.random(nb) < 0.01, np.uint8(ord("N")), s).astype(np.uint8)
+        self.block, self.width, self.block_lines = s, width, block_lines
+        self.lengths = dict(HG19_LENGTHS if lengths is None else lengths)
+        # contig k starts at line (k * 7919) % block_lines of the block
+        self.start = {c: (k * 7919) % block_lines for k, c in enumerate(self.lengths)}
+
+    def base(self, chrom: str, pos1: int) -> int:
+        return int(self.block[(self.start[chrom] * self.width + pos1 - 1) % self.block.size])
+
+    def write_fasta(self, path: str, lines_per_write: int = 1 << 20) -> int:
+        """Write the FASTA; returns its size in bytes."""
+        w, nl = self.width, self.block_lines
+        lines = np.concatenate([self.block.reshape(nl, w), np.full((nl, 1), ord("\n"), np.uint8)], 1)
+        with open(path, "wb") as f:
+            for c, ln in self.lengths.items():
+                f.write(b">" + c.encode() + b"\n")
+                full, tail = divmod(ln, w)
+                for a in range(0, full, lines_per_write):
+                    idx = (self.start[c] + np.arange(a, min(full, a + lines_per_write))) % nl
+                    f.write(lines[idx].tobytes())
+                if tail:
+                    row = lines[(self.start[c] + full) % nl]
+                    f.write(row[:tail].tobytes() + b"\n")
+            return f.tell()
+
+    def snvs(self, n: int, seed: int = 1, margin: int = 5000):
+        """(chrom, pos, ref, alt) SNVs with ref = the genome base (upper case), as ``snvs``."""
+        rng = np.random.default_rng(seed)
+        names = list(self.lengths)
+        out = []
+        while len(out) < n:
+            chrom = names[int(rng.integers(0, len(names)))]
+            pos = int(rng.integers(margin, self.lengths[chrom] - margin))
+            ref = chr(self.base(chrom, pos)).upper()
+            if ref not in "ACGT":
+                continue
+            out.append((chrom, pos, ref, "ACGT".replace(ref, "")[int(rng.integers(0, 3))]))
+        return out
+
+
 def snvs(genome: dict, n: int, seed: int = 1, margin: int = 5000):
     """List of (chrom, pos(1-based), ref, alt) biallelic SNVs."""
     rng = np.random.default_rng(seed)

@@ -110,14 +110,15 @@ def _load_model(args) -> Beluga:
     return m.cuda()
 
 
-def _common_args(p):
+def _common_args(p, gene_batch: int = 16, max_batch: int = 2048):
     p.add_argument('--windowsize', action="store", dest="windowsize", type=int, default=2000)
     p.add_argument('--cuda', action='store_true')
     p.add_argument('--genome', default='./resources/hg19.fa')
     p.add_argument('--weights', default='./resources/deepsea.beluga.pth')
     p.add_argument('--synthetic-weights', type=int, default=None, dest='synthetic_weights')
-    p.add_argument('--max-batch', type=int, default=2048, dest='max_batch')
-    p.add_argument('--gene-batch', type=int, default=16, dest='gene_batch')
+    p.add_argument('--max-batch', type=int, default=max_batch, dest='max_batch',
+                   help="windows per device chunk / FC slice (handle workspace: ~5 MB per window)")
+    p.add_argument('--gene-batch', type=int, default=gene_batch, dest='gene_batch')
 
 
 def _anno_genes(path):
@@ -154,7 +155,7 @@ def compute_main(argv=None):
         raise ValueError("--windowsize must be 2000 (Beluga.py:43)")
     rank, world, local = edist.init()
     if world > 1:
-        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        torch.cuda.set_device(edist.local_device(local))
     os.makedirs(args.out_dir, exist_ok=True)
     fasta = Fasta(args.genome)
     model = _load_model(args)
@@ -205,27 +206,124 @@ def compute_main(argv=None):
     return arr
 
 
+REPLICATE_LAST = {}   # timing of the last replicate run (bench.py's replicate_rank extra reads it)
+
+
+def replicate_batch_genes(args, n_shifts: int) -> int:
+    """Genes per streamed replicate batch: --gene-batch, capped so that one batch's host slot
+    (n_shifts x 2002 fp32 per gene, two pinned slots) stays within --batch-gb."""
+    per_gene = n_shifts * 2002 * 4
+    cap = max(1, int(float(args.batch_gb) * (1 << 30)) // per_gene)
+    return max(1, min(int(args.gene_batch), cap))
+
+
 def replicate_main(argv=None):
     """replicate_expecto_features.py main() (:16-86): one (200,2002) float32 .npy per gene."""
     p = argparse.ArgumentParser(description='Replicate ExPecto chromatin features')
     p.add_argument('annoFile')
     p.add_argument('-o', dest="out_dir", type=str, default='temp_replicate_expecto_features')
-    _common_args(p)
-    args = p.parse_args(argv)
+    _common_args(p, gene_batch=96, max_batch=8192)
+    p.add_argument('--batch-gb', type=float, default=2.0, dest='batch_gb',
+                   help="cap on one batch's pinned host slot in GiB (two slots are kept)")
+    p.add_argument('--write-threads', type=int, default=4, dest='write_threads',
+                   help="threads writing a batch's per-gene .npy files")
+    return replicate_run(p.parse_args(argv))
+
+
+def replicate_run(args):
+    """Streamed replicate (replicate_expecto_features.py:65-86): this rank's genes go through
+    the device in batches of --gene-batch (default 96, the bench's step); batch k+1's windows,
+    forward and fwd/rc mean are enqueued, with its D2H copy into one of two pinned slots, while
+    batch k's per-gene .npy files are written from the other slot.  The f16x3 overflow check is
+    deferred to each batch's release point (a flagged batch is recomputed in bf16x6 before its
+    files are written), so no forward call waits on the host.
+
+    Genes shard by contiguous rank ranges with no collective (per-gene files).  A gene id that
+    appears more than once is computed once, at its LAST row: the reference writes every row in
+    order, so the last one's file is what remains (replicate_expecto_features.py:86)."""
+    from concurrent.futures import ThreadPoolExecutor
+    import time
+    t_start = time.perf_counter()
     if args.windowsize != 2000:
         raise ValueError("--windowsize must be 2000 (Beluga.py:43)")
     rank, world, local = edist.init()
+    if world > 1:
+        torch.cuda.set_device(edist.local_device(local))
     os.makedirs(args.out_dir, exist_ok=True)
+    setup = {}
+    t1 = time.perf_counter()
     fasta = Fasta(args.genome)
+    setup["fasta_s"] = time.perf_counter() - t1
+    t1 = time.perf_counter()
     model = _load_model(args)
-    genes = _anno_genes(args.annoFile)
-    lo, hi = edist.shard_range(len(genes), rank, world)   # per-gene files: no collective
+    torch.cuda.synchronize()
+    setup["model_s"] = time.perf_counter() - t1
+    rows = _anno_genes(args.annoFile)
+    last = {g[0]: i for i, g in enumerate(rows)}
+    genes = [g for i, g in enumerate(rows) if last[g[0]] == i]
+    lo, hi = edist.shard_range(len(genes), rank, world)
+    mine = genes[lo:hi]
+    t1 = time.perf_counter()
     dg = DeviceGenome(fasta)
-    pipe = TSSPipeline(model.engine(), dg)
-    for b in _batches(genes[lo:hi], args.gene_batch):
-        pred = pipe.pred_fwd_rc([g[1] for g in b], [g[2] for g in b], [g[3] for g in b]).cpu().numpy()
-        for g, pr in zip(b, pred):
-            np.save(f'{args.out_dir}/{g[0]}', pr)
+    setup["device_genome_s"] = time.perf_counter() - t1
+    eng = model.engine()
+    pipe = TSSPipeline(eng, dg)
+    S = len(pipe.shifts)
+    B = replicate_batch_genes(args, S)
+    nb = -(-len(mine) // B)
+    slots = [torch.empty((min(B, len(mine)), S, 2002), dtype=torch.float32, pin_memory=True)
+             for _ in range(min(2, nb))]
+    tm = {"launch_s": 0.0, "wait_s": 0.0, "write_s": 0.0, "recomputed_batches": 0}
+
+    def launch(k):
+        b = mine[k * B:(k + 1) * B]
+        job = {"genes": b, "flag": torch.zeros(1, dtype=torch.int32).pin_memory(), "event": torch.cuda.Event()}
+        job["pred"] = pipe.pred_fwd_rc([g[1] for g in b], [g[2] for g in b], [g[3] for g in b])
+        eng.overflow_take(job["flag"])
+        job["host"] = slots[k % 2][:len(b)]
+        job["host"].copy_(job["pred"], non_blocking=True)
+        job["event"].record()
+        return job
+
+    def complete(job, pool):
+        t1 = time.perf_counter()
+        job["event"].synchronize()
+        tm["wait_s"] += time.perf_counter() - t1
+        b = job["genes"]
+        if int(job["flag"][0]):
+            # f16x3 overflow in this batch: recompute it in bf16x6 before its files are written
+            with eng.precision_override("bf16x6"):
+                pred = pipe.pred_fwd_rc([g[1] for g in b], [g[2] for g in b], [g[3] for g in b])
+            eng.count_fallback()
+            job["host"].copy_(pred)
+            tm["recomputed_batches"] += 1
+        t1 = time.perf_counter()
+        arr = job["host"].numpy()
+        list(pool.map(lambda i: np.save(f'{args.out_dir}/{b[i][0]}', arr[i]), range(len(b))))
+        tm["write_s"] += time.perf_counter() - t1
+
+    eng.set_overflow_check(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    try:
+        with ThreadPoolExecutor(max(1, args.write_threads)) as pool:
+            pending = None
+            for k in range(nb):
+                t1 = time.perf_counter()
+                job = launch(k)                 # batch k computes while batch k-1 is written
+                tm["launch_s"] += time.perf_counter() - t1
+                if pending is not None:
+                    complete(pending, pool)
+                pending = job
+            if pending is not None:
+                complete(pending, pool)
+    finally:
+        eng.set_overflow_check(False)
+    loop_s = time.perf_counter() - t0
+    REPLICATE_LAST.clear()
+    REPLICATE_LAST.update(loop_s=loop_s, setup_s=t0 - t_start, total_s=time.perf_counter() - t_start, setup=setup,
+                          genes=len(mine), batches=nb, gene_batch=B, rank=rank, world=world, **tm)
+    return dict(REPLICATE_LAST)
 
 
 def atac_peak_bins(chrom, tss, strand, peaks: dict) -> np.ndarray:

@@ -34,7 +34,7 @@ def test_committed_traffic_matches_the_default_workload_key():
     import bench
     key = bench.profile_key()
     traffic, src = bench.pmc_traffic(key, bench.kernel_name("conv2", "f16x3"))
-    assert traffic is not None and traffic > 0, "re-take profiles: tools/profile_round.sh + collect_profiles.py"
+    assert traffic is not None and traffic > 0, "re-take profiles: STEPS=prof,pmc tools/gpu_session.sh + collect_profiles.py"
     assert src.startswith("profiles/")
 
 
@@ -42,7 +42,7 @@ def test_committed_sq_counters_give_the_held_clock():
     import bench
     key = bench.profile_key()
     held = bench.pmc_held_clock(key, bench.kernel_name("conv2", "f16x3"))
-    assert held is not None, "re-take profiles: tools/profile_round.sh + collect_profiles.py"
+    assert held is not None, "re-take profiles: STEPS=prof,pmc tools/gpu_session.sh + collect_profiles.py"
     assert 0.3 < held["mfma_busy"] <= 1.0 and 1.0 < held["held_clock_ghz"] < 2.6
 
 

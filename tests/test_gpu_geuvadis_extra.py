@@ -81,19 +81,32 @@ def test_top_eqtls_and_merge_match_reference(inputs, capsys):
     assert capsys.readouterr().out == gold["top_stdout"].item().decode()
     m = GBLinear.load(p["model"])
     w = tss_pos_weights()
+    ours, bounds = {}, {}
     for gi, g in enumerate(mg.TOP_GENES):
         gene = g.lower()
-        pbar = _check_windows(cap["y"][gi][:, 0], gold, "top", gi)
+        _check_windows(cap["y"][gi][:, 0], gold, "top", gi)
         x = cap["x"][gi]
         assert_close(x[0, ::4], gold[f"top_feat_{gi}"], what=f"top {gene} features")
         r = h5.read(str(out / gene / f"{gene}.h5"))
         assert list(r["record_ids"]) == list(gold[f"top_ids_{gi}"])
         assert [hashlib.sha1(bytes(s)).hexdigest().encode() for s in r["seqs"]] == list(gold[f"top_seq_sha1_{gi}"])
         assert r["preds"].dtype == np.float32 and r["preds"].shape == gold[f"top_preds_{gi}"].shape
-        assert abs(float(r["preds"][0]) - float(gold[f"top_preds_{gi}"][0])) <= _score_bound(m, x[0], pbar, w), gene
+        # every record's score within the bound its own window predictions give (_score_bound)
+        yk = cap["y"][gi]
+        bounds[gene] = np.array([_score_bound(m, x[k], (yk[0, k].astype(np.float64) + yk[1, k]) / 2, w)
+                                 for k in range(x.shape[0])])
+        ours[gene] = r["preds"]
+        err = np.abs(r["preds"].astype(np.float64) - gold[f"top_preds_{gi}"])
+        assert (err <= bounds[gene]).all(), (gene, err.max(), bounds[gene].min())
     merged = d / "merged"
     consensus.merge_main(["--batch_dir", str(out), "--n_genes", str(len(mg.TOP_GENES)), "-o", str(merged)])
     r = h5.read(str(merged / "expecto_preds.h5"))
     assert list(r["record_ids"]) == list(gold["merge_record_ids"]) and list(r["genes"]) == list(gold["merge_genes"])
     assert r["preds"].shape == gold["merge_preds"].shape
-    np.testing.assert_allclose(r["preds"], gold["merge_preds"], rtol=0, atol=2e-3)
+    # the merge stacks our per-gene scores unchanged; against the reference's merge each row stays
+    # within its gene's derived bound (replaces round 3's atol=2e-3)
+    for gi, stem in enumerate(r["genes"]):
+        gene = bytes(stem).decode()
+        assert np.array_equal(r["preds"][gi], ours[gene]), gene
+        err = np.abs(r["preds"][gi].astype(np.float64) - gold["merge_preds"][gi])
+        assert (err <= bounds[gene]).all(), (gene, err.max())

@@ -303,7 +303,7 @@ def test_chromatin_cli_two_ranks_equals_one(workdir):
         port = s.getsockname()[1]
         s.close()
         two = workdir / f"out_2rank_{mode}"
-        env = dict(os.environ, EXPECTO_DIST_BACKEND="gloo")
+        env = dict(os.environ, EXPECTO_DIST_BACKEND="gloo", EXPECTO_SHARE_GPUS="1")
         r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                             "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "expecto_amd.chromatin",
                             str(vcf), "--output_dir", str(two), "--variant-batch", "2", "--output-mode", mode] + common,
@@ -382,6 +382,41 @@ def test_chromatin_cli_overflowed_batches_are_recomputed(workdir, monkeypatch):
         assert open(out / name, "rb").read() == open(ref / name, "rb").read(), name
 
 
+def test_recompute_overflowed_without_relocated_slice_redoes_the_batch(monkeypatch):
+    """a batch whose deferred flag fired but whose slice reruns all report no
+    overflow (forced here by routing the reruns' flag copies to a scratch tensor) is recomputed
+    whole in bf16x6 instead of keeping its f16x3 rows."""
+    import torch
+    from expecto_amd import synthetic
+    from expecto_amd.genome import DeviceGenome, Fasta
+    from expecto_amd.pipeline import VariantPipeline, VariantSet, shift_order
+    g = synthetic.genome_bytes(**GENOME_ARGS)
+    fa = Fasta.from_dict(g)
+    snv = synthetic.snvs(g, 10, seed=9)
+    vs = VariantSet([s[0] for s in snv], np.array([s[1] for s in snv]), [s[2] for s in snv], [s[3] for s in snv])
+    shifts = shift_order(200)
+    eng = _engine("f16x3")
+    eng.set_overflow_check(deferred=True)
+    eng.set_f16_target(20)
+    pipe = VariantPipeline(eng, fa, DeviceGenome(fa))
+    y = pipe.predict(vs, shifts)
+    flag = torch.zeros(1, dtype=torch.int32).pin_memory()
+    eng.overflow_take(flag)
+    torch.cuda.synchronize()
+    assert int(flag[0]) == 1
+    real, scratch = eng.overflow_take, torch.zeros(1, dtype=torch.int32).pin_memory()
+    monkeypatch.setattr(eng, "overflow_take", lambda dst, stream=None: real(scratch, stream))
+    fb0 = eng.f16_state()[0]
+    redone = pipe.recompute_overflowed(vs, shifts, y)
+    torch.cuda.synchronize()
+    assert redone == 8 and eng.f16_state()[0] - fb0 == 1
+    with eng.precision_override("bf16x6"):
+        want = pipe.predict(vs, shifts)
+    assert torch.equal(y, want)
+    eng.set_f16_target(10)
+    eng.set_overflow_check(deferred=False)
+
+
 def test_chromatin_cli_batch_gb_caps_the_batch():
     """--batch-gb lowers --variant-batch so one batch's y + diff of every shift fits the cap
     (a 201-shift sweep at the default 4096 variants would pin ~79 GB)."""
@@ -393,6 +428,53 @@ def test_chromatin_cli_batch_gb_caps_the_batch():
     assert b * per_variant <= 4 * (1 << 30) < (b + 1) * per_variant
     a = chromatin.build_parser().parse_args(["x.vcf", "--batch-gb", "0"])
     assert chromatin.batch_variants(a, 9) == 1
+
+
+def test_replicate_streamed_equals_one_batch(workdir, monkeypatch):
+    """The streamed replicate CLI (two pinned slots, batch k's .npy files
+    written while batch k+1 computes, deferred overflow check) writes the same bytes in batches
+    of 2 genes as in one batch; a duplicated gene id keeps its last row's file, as the
+    reference's sequential writes leave it; with every activation forced past fp16's range each
+    batch is recomputed in bf16x6 and the files equal a bf16x6 run byte for byte."""
+    from expecto_amd import tss
+    rows = [("ENSGT0001", "chr1", 30000, "+"), ("ENSGT0002", "chr2", 29123, "-"), ("ENSGT0003", "chr3", 25000, "+"),
+            ("ENSGT0004", "chr1", 34000, "-"), ("ENSGT0002", "chr3", 33000, "+"), ("ENSGT0005", "chr2", 23000, "+"),
+            ("ENSGT0006", "chr3", 37000, "-")]
+    anno = workdir / "anno_rep.csv"
+    anno.write_text("id,symbol,seqnames,strand,TSS,CAGE_representative_TSS,type\n" +
+                    "".join(f"{g},S{k},{c},{s},{t},{t},protein_coding\n" for k, (g, c, t, s) in enumerate(rows)))
+    last = workdir / "anno_rep_last.csv"
+    last.write_text("id,symbol,seqnames,strand,TSS,CAGE_representative_TSS,type\n"
+                    "ENSGT0002,S4,chr3,+,33000,33000,protein_coding\n")
+    common = ["--genome", str(workdir / "hg19.fa"), "--synthetic-weights", "0", "--max-batch", "400"]
+    outs = {}
+    for name, extra in (("b2", ["--gene-batch", "2"]), ("b16", ["--gene-batch", "16"])):
+        outs[name] = workdir / f"rep_{name}"
+        r = tss.replicate_main([str(anno), "-o", str(outs[name])] + common + extra)
+        assert r["genes"] == 6 and r["batches"] == (3 if name == "b2" else 1), r
+    names = sorted(os.listdir(outs["b16"]))
+    assert names == sorted({f"{g}.npy" for g, _, _, _ in rows})
+    for n in names:
+        assert open(outs["b2"] / n, "rb").read() == open(outs["b16"] / n, "rb").read(), n
+    one = workdir / "rep_last"
+    tss.replicate_main([str(last), "-o", str(one)] + common)
+    assert open(one / "ENSGT0002.npy", "rb").read() == open(outs["b2"] / "ENSGT0002.npy", "rb").read()
+    monkeypatch.setenv("EXPECTO_PRECISION", "bf16x6")
+    ref = workdir / "rep_bf16x6"
+    tss.replicate_main([str(anno), "-o", str(ref), "--gene-batch", "2"] + common)
+    monkeypatch.setenv("EXPECTO_PRECISION", "f16x3")
+    real = tss._load_model
+
+    def forced(args):
+        m = real(args)
+        m.engine().set_f16_target(20)
+        return m
+    monkeypatch.setattr(tss, "_load_model", forced)
+    ovf = workdir / "rep_forced"
+    r = tss.replicate_main([str(anno), "-o", str(ovf), "--gene-batch", "2"] + common)
+    assert r["recomputed_batches"] == r["batches"] == 3, r
+    for n in names:
+        assert open(ovf / n, "rb").read() == open(ref / n, "rb").read(), n
 
 
 def test_tss_compute_two_ranks_equals_one(workdir):
@@ -419,7 +501,7 @@ def test_tss_compute_two_ranks_equals_one(workdir):
     port = s.getsockname()[1]
     s.close()
     two = workdir / "tss_2rank"
-    env = dict(os.environ, EXPECTO_DIST_BACKEND="gloo")
+    env = dict(os.environ, EXPECTO_DIST_BACKEND="gloo", EXPECTO_SHARE_GPUS="1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "expecto_amd.tss",
                         "compute"] + common + ["-o", str(two)],

@@ -24,7 +24,7 @@ def test_fasta_roundtrip_and_one_based_slices(tmp_path, genome):
     fa = Fasta(p)
     assert list(fa.keys()) == ["chr1", "chr2", "chr3"]
     for c in fa.keys():
-        assert fa.raw(c) == genome[c]
+        assert bytes(fa.raw(c)) == genome[c]
     s = fa.sequence({"chr": "chr2", "start": 101, "stop": 110})
     assert s == genome["chr2"][100:110].decode() and len(s) == 10
 

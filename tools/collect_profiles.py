@@ -1,4 +1,4 @@
-"""Turn one tools/profile_round.sh run (gpurun_out/) into the committed profiles/<tag>/ summaries.
+"""Turn one tools/gpu_session.sh prof,pmc run (gpurun_out/) into the committed profiles/<tag>/ summaries.
 
     python tools/collect_profiles.py r01 [--bench-log gpurun_out/bench.log]
 

@@ -1,4 +1,4 @@
-"""Summarise gemm_bench SQ counter passes (tools/gpu_pmc_gb.sh) for one variant's kernel.
+"""Summarise gemm_bench SQ counter passes (tools/gpu_session.sh step gbpmc) for one variant's kernel.
     python tools/sq_summary.py <variant> [kernel-substring]"""
 import csv
 import glob
