@@ -120,14 +120,8 @@ __global__ __launch_bounds__(320) void beluga_conv1(const float* __restrict__ x,
 // canonical split, staged per wave through LDS so each row's two 128-B plane groups leave as
 // 16-B stores (the VALU kernel's 2-byte stores and 32 FMAs per output were its limit).
 // 5 waves; 256 output rows per workgroup in 32-row steps.
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int C1H_ROWS = 256, C1H_STEP = 32;
 constexpr int C1H_WROW = 2 * 128 + 16;   // staged bytes per row and wave (2 plane groups + pad)
-
-__device__ __forceinline__ unsigned onehot_h2(unsigned c, unsigned hi_pair) {
-  // fp16 1.0 (0x3C00) in the half of channel c within the channel pair (0,1) or (2,3)
-  return (c >> 1) == hi_pair ? (0x3C00u << ((c & 1u) * 16u)) : 0u;
-}
 
 __global__ __launch_bounds__(320) void beluga_conv1_h3(const float* __restrict__ x, const uint8_t* __restrict__ codes,
                                                        long long code_stride, int n_src, int mode, long long row0,
@@ -660,6 +654,47 @@ __global__ void seg_delta_codes(const uint8_t* __restrict__ codes, long long str
   out[(long long)m * 16 + i] = c;
 }
 
+// conv1 fused into conv2 (f16x3): the ref conv1 planes are never stored, so the alt conv2 patch
+// (kDA[2] conv1 rows from 4*r2) is conv1 of the alt codes [4*r2, 4*r2 + kDA[2] + 7) -- every row
+// computed from the alt sequence, which is the ref row where the SNV is outside its 8 taps, bit
+// for bit (conv1 is row-local).  kC1Pat codes per block at a kC1PatStride stride, code 4 (N) past
+// the segment end; seg_delta_codes2 for segments (strand orientation, as seg_delta_codes),
+// delta_codes2 for the pair path's alt windows (as delta_codes).
+constexpr int kC1Pat = kDA[2] + 7, kC1PatStride = 48;
+__global__ void seg_delta_codes2(const uint8_t* __restrict__ codes, long long stride, const uint8_t* __restrict__ alt_code,
+                                 int s0, int ns, int rc, int L, const int* __restrict__ tab, uint8_t* __restrict__ out) {
+  const int i = threadIdx.x % kC1PatStride;
+  const int m = blockIdx.x * (blockDim.x / kC1PatStride) + threadIdx.x / kC1PatStride;
+  if (m >= ns) return;
+  const int q = tab[m * kSegTab], x = 4 * tab[m * kSegTab + 2] + i;
+  uint8_t c = 4;
+  if (i < kC1Pat && x < L) {
+    c = x == q ? alt_code[s0 + m] : codes[(long long)(s0 + m) * stride + (rc ? L - 1 - x : x)];
+    if (rc && c < 4) c = (uint8_t)(3 - c);
+  }
+  out[(long long)m * kC1PatStride + i] = c;
+}
+
+__global__ void delta_codes2(const uint8_t* __restrict__ alt, long long stride, int nv, int v0,
+                             const int* __restrict__ var_pos, uint8_t* __restrict__ out, int R) {
+  const int i = threadIdx.x % kC1PatStride;
+  const int m = blockIdx.x * (blockDim.x / kC1PatStride) + threadIdx.x / kC1PatStride;
+  if (m >= R) return;
+  const int s = m / nv, v = v0 + m % nv;
+  const int pos = 4 * delta_rows(pair_pos(var_pos, m, nv, v0)).r[2] + i;
+  const uint8_t* a = alt + (long long)v * stride;
+  uint8_t c = 4;
+  if (i < kC1Pat && pos < kLen) {
+    if (s) {
+      const uint8_t f = a[kLen - 1 - pos];
+      c = f < 4 ? (uint8_t)(3 - f) : f;
+    } else {
+      c = a[pos];
+    }
+  }
+  out[(long long)m * kC1PatStride + i] = c;
+}
+
 // Input patch of one alt run: rows base + i (i < arows) of ref block m (ref_rows rows per
 // block), except rows inside [rp, rp + wprev), taken from the previous alt run.  Blocks are
 // segments (nb = 1) or (segment, phase) pairs (nb = n_ph, per-phase table entries).
@@ -987,6 +1022,7 @@ struct expecto_beluga {
   int seg_chunk_windows = 0;          // segment path: windows per chunk cap (0 = none; tuning knob)
   int cus = 0;                        // compute units of the device (workgroups per round)
   bool pool_one_pass = true;          // segment path: pool2 of all phases in one pass (same bits)
+  bool fuse_conv1 = true;             // f16x3 codes input: conv1 inside the conv2 launch (EXPECTO_FUSE_CONV1; same bits)
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, int>> pending;  // (layer, event index of start)
@@ -1172,7 +1208,14 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
       // all bitwise equal (same products and k order per output); per-layer choice from
       // tools/gemm_bench: 256-row tiles on the producer/consumer kernel (MFMA waves never issue
       // LDS-DMA), 384-row tiles (conv2) on the 4-wave 96-row kernel
-      if (bm == 384)
+      if (a.c1_codes) {   // conv2 with conv1 fused into the producers (A slabs from base codes)
+        if constexpr (LAYER == 2 && EPI == EPI_RELU_POOL4) {
+          EXPECTO_REQUIRE(bm == 256 && a.c1_w && a.c1_cs && a.c1_b, "fused conv1: 256-row tiles, conv1 planes");
+          beluga_conv_h3p<LAYER, EPI, 256 | H3P_FUSE_CONV1, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
+        } else {
+          EXPECTO_REQUIRE(false, "fused conv1: conv2 + pool1 only");
+        }
+      } else if (bm == 384)
         beluga_conv_h3r<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
       else   // 4-deep B ring, next-stage fragments read before the stage barrier (TM 256)
         beluga_conv_h3p<LAYER, EPI, 256, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
@@ -1212,9 +1255,27 @@ int run_conv1(expecto_beluga* h, const float* x, const uint8_t* codes, long long
   return check_launch("beluga_conv1");
 }
 
-// conv layer l (0 = conv2 .. 4 = conv6) over `groups` row groups of s_in rows each.
+// Base codes of a conv1 input, as run_conv1 takes them (window w = code row row0 + w; mode
+// EXPECTO_STRAND_*, rows >= n_src of a BOTH call are the rc of row - n_src; len bases).
+struct C1Src {
+  const uint8_t* codes;
+  long long stride;
+  int n_src, mode;
+  long long row0;
+  int len;
+};
+
+// conv1 fused into conv2 (f16x3, codes input): no conv1 launch, no conv1 planes in HBM; the conv2
+// producers compute the A slabs from the codes (gemm_kernel.h conv12_producer; same bits).
+// EXPECTO_FUSE_CONV1=0 keeps the separate beluga_conv1_h3 launch.
+bool fuse_conv1(const expecto_beluga* h, const float* x) {
+  return h->fuse_conv1 && !x && g_precision == EXPECTO_PRECISION_F16X3 && h->w1h;
+}
+
+// conv layer l (0 = conv2 .. 4 = conv6) over `groups` row groups of s_in rows each.  f1 (conv2
+// only): compute conv1 from these codes inside the conv2 launch instead of reading src.
 int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long groups, int s_in, int t_valid,
-             int s_out, bool pool, hipStream_t st) {
+             int s_out, bool pool, hipStream_t st, const C1Src* f1 = nullptr) {
   const ConvGeo& g = kConv[l];
   GemmArgs a{};
   a.A = src;
@@ -1229,7 +1290,7 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
   a.kper = 8 * g.cin;
   a.taps = 8;
   a.n_tiles = npad_of(g.cout) / GBN;
-  const int bm = conv_tile_rows(h, l, pool, a.M, (int)a.n_tiles);
+  const int bm = f1 ? 256 : conv_tile_rows(h, l, pool, a.M, (int)a.n_tiles);
   a.m_tiles = (a.M + bm - 1) / bm;
   a.m_fastest = 0;
   a.bias = h->bt[l];
@@ -1239,6 +1300,24 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
   a.s_in = s_in;
   a.t_valid = t_valid;
   a.s_out = s_out;
+  if (f1) {
+    EXPECTO_REQUIRE(l == 0 && pool && g_precision == EXPECTO_PRECISION_F16X3 && h->w1h && f1->len >= 8,
+                    "fused conv1: f16x3 conv2 + pool1 from codes");
+    a.A = nullptr;
+    a.c1_codes = f1->codes;
+    a.c1_stride = f1->stride;
+    a.c1_row0 = f1->row0;
+    a.c1_n_src = f1->n_src;
+    a.c1_mode = f1->mode;
+    a.c1_len = f1->len;
+    a.c1_n_win = (int)groups;
+    a.c1_w = reinterpret_cast<const _Float16*>(h->w1h);
+    a.c1_cs = h->cs1;
+    a.c1_b = h->b1;
+    a.c1_osc = exp2i(h->sx[0]);
+    // conv1's algorithmic MACs stay in conv1's slot (its time is inside this launch)
+    if (h->profiling) h->macs[h->timer_base + 0] += (double)groups * (f1->len - 7) * 320 * 32;
+  }
   LayerTimer lt(h, l + 1, st);
   if (h->profiling) h->macs[h->timer_base + l + 1] += (double)a.M * g.cout * a.kper;
   if (pool) {
@@ -1421,12 +1500,16 @@ int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long 
                   int mode, long long row0, int nb, float* y, hipStream_t st) {
   int rc;
   g_precision = h->precision;
-  if ((rc = run_conv1(h, x, codes, code_stride, n_src, mode, row0, nb, kLen, kS1, st))) return rc;
+  const bool fuse = fuse_conv1(h, x);
+  const C1Src f1{codes, code_stride, n_src, mode, row0, kLen};
+  if (!fuse && (rc = run_conv1(h, x, codes, code_stride, n_src, mode, row0, nb, kLen, kS1, st))) return rc;
   float* src = h->P;
   float* dst = h->Q;
   for (int l = 0; l < 5; ++l) {
     const ConvGeo& g = kConv[l];
-    if ((rc = run_conv(h, l, src, dst, nb, g.s_in, g.t_valid, g.s_out, g.pool != 0, st))) return rc;
+    if ((rc = run_conv(h, l, src, dst, nb, g.s_in, g.t_valid, g.s_out, g.pool != 0, st,
+                       l == 0 && fuse ? &f1 : nullptr)))
+      return rc;
     std::swap(src, dst);
   }
   return run_fc(h, src, nullptr, nb, y, st);  // src = act5 (buffer Q), 106 x 640 rows per window
@@ -1441,7 +1524,7 @@ int ensure_delta(expecto_beluga* h) {
   float *pc = nullptr, *tb = nullptr;
   int rc;
   if ((rc = dalloc(h, &h->DA, act_alloc(da))) || (rc = dalloc(h, &h->D0, act_alloc(dd))) ||
-      (rc = dalloc(h, &h->D1, act_alloc(dd))) || (rc = dalloc(h, &pc, (size_t)h->max_batch * 4)) ||
+      (rc = dalloc(h, &h->D1, act_alloc(dd))) || (rc = dalloc(h, &pc, (size_t)h->max_batch * kC1PatStride / 4)) ||
       (rc = dalloc(h, &tb, (size_t)h->max_batch * kSegTab)) ||
       (rc = dalloc(h, &h->slab_mask, (size_t)h->max_batch / 64 + 64)))
     return rc;
@@ -1656,26 +1739,39 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
         EXPECTO_HIP_CHECK(hipEventRecord(h->pev[0], st));
         EXPECTO_HIP_CHECK(hipStreamWaitEvent(sa, h->pev[0], 0));
       }
-      // conv1 from codes: virtual rows = segments; rc mode mirrors inside the kernel
-      if ((rc = run_conv1(h, nullptr, codes + (long long)s0 * code_stride, code_stride, ns,
-                          is_rc ? EXPECTO_STRAND_RC : EXPECTO_STRAND_FWD, 0, ns, L, g.S1, st)))
-        return rc;
+      // conv1 from codes: virtual rows = segments; rc mode mirrors inside the kernel (fused: inside
+      // the conv2 launch)
+      const bool fuse = fuse_conv1(h, nullptr);
+      const C1Src f1{codes + (long long)s0 * code_stride, code_stride, ns, is_rc ? EXPECTO_STRAND_RC : EXPECTO_STRAND_FWD,
+                     0, L};
+      if (!fuse && (rc = run_conv1(h, nullptr, f1.codes, code_stride, ns, f1.mode, 0, ns, L, g.S1, st))) return rc;
       if (pr) {
         seg_delta_table<<<dim3((ns + 255) / 256), dim3(256), 0, sa>>>(h->seg_var_d, s0, ns, is_rc ? 1 : 0, gd, n_ph,
                                                                      ph4, h->seg_tab);
         if ((rc = check_launch("seg_delta_table"))) return rc;
-        seg_delta_codes<<<dim3((ns + 15) / 16), dim3(256), 0, sa>>>(codes, code_stride, pr->alt_code, s0, ns,
-                                                                   is_rc ? 1 : 0, L, h->seg_tab, h->delta_codes);
-        if ((rc = check_launch("seg_delta_codes"))) return rc;
-        DeltaScope ds(h);
-        if ((rc = run_conv1(h, nullptr, h->delta_codes, 16, ns, EXPECTO_STRAND_FWD, 0, ns, kDA[1], kDW[1], sa,
-                            h->D0)))
-          return rc;
+        if (fuse) {   // the alt conv2 patch straight from the alt codes (conv1 of kC1Pat codes -> DA)
+          seg_delta_codes2<<<dim3((ns + 4) / 5), dim3(5 * kC1PatStride), 0, sa>>>(
+              codes, code_stride, pr->alt_code, s0, ns, is_rc ? 1 : 0, L, h->seg_tab, h->delta_codes);
+          if ((rc = check_launch("seg_delta_codes2"))) return rc;
+          DeltaScope ds(h);
+          if ((rc = run_conv1(h, nullptr, h->delta_codes, kC1PatStride, ns, EXPECTO_STRAND_FWD, 0, ns, kC1Pat, kDA[2],
+                              sa, h->DA)))
+            return rc;
+        } else {
+          seg_delta_codes<<<dim3((ns + 15) / 16), dim3(256), 0, sa>>>(codes, code_stride, pr->alt_code, s0, ns,
+                                                                     is_rc ? 1 : 0, L, h->seg_tab, h->delta_codes);
+          if ((rc = check_launch("seg_delta_codes"))) return rc;
+          DeltaScope ds(h);
+          if ((rc = run_conv1(h, nullptr, h->delta_codes, 16, ns, EXPECTO_STRAND_FWD, 0, ns, kDA[1], kDW[1], sa,
+                              h->D0)))
+            return rc;
+        }
       }
       // conv2 + pool1 (P -> Q), conv3 (Q -> P), conv4 unpooled (P -> Q); alt runs D0 <-> D1
-      if (pr && (rc = alt_asm(0, h->P, g.S1, h->D0, kDW[1], 1, 2, 4, 1, kDA[2], h->pev[1], h->pev[2]))) return rc;
-      if ((rc = run_conv(h, 0, h->P, h->Q, ns, g.S1, g.P1, g.P1, true, st))) return rc;
-      if (pr && ((rc = st_wait(h->pev[2])) || (rc = alt_gemm(0, 1, kDA[2], kDW[2], true, h->D1)))) return rc;
+      if (pr && !fuse && (rc = alt_asm(0, h->P, g.S1, h->D0, kDW[1], 1, 2, 4, 1, kDA[2], h->pev[1], h->pev[2])))
+        return rc;
+      if ((rc = run_conv(h, 0, h->P, h->Q, ns, g.S1, g.P1, g.P1, true, st, fuse ? &f1 : nullptr))) return rc;
+      if (pr && ((!fuse && (rc = st_wait(h->pev[2]))) || (rc = alt_gemm(0, 1, kDA[2], kDW[2], true, h->D1)))) return rc;
       if (pr && (rc = alt_asm(1, h->Q, g.P1, h->D1, kDW[2], 1, 3, 1, 2, kDA[3], h->pev[3], h->pev[4]))) return rc;
       if ((rc = run_conv(h, 1, h->Q, h->P, ns, g.P1, g.T3, g.T3, false, st))) return rc;
       if (pr && ((rc = st_wait(h->pev[4])) || (rc = alt_gemm(1, 1, kDA[3], kDW[3], false, h->D0)))) return rc;
@@ -1832,11 +1928,21 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
   for (int v0 = 0; v0 < n; v0 += nv_max) {
     const int nv = std::min(nv_max, n - v0), R = strands * nv;
     if ((rc = order(st, sa, h->pev[0]))) return rc;   // caller's inputs (and the previous chunk)
-    // conv1: ref windows (full) and the alt runs (15 codes -> 8 rows)
-    if ((rc = run_conv1(h, nullptr, ref + (long long)v0 * stride, stride, nv, mode, 0, R, kLen, kS1, st))) return rc;
-    delta_codes<<<dim3((R + 15) / 16), dim3(256), 0, sa>>>(alt, stride, nv, v0, var_pos, h->delta_codes, R);
-    if ((rc = check_launch("delta_codes"))) return rc;
-    {
+    // conv1: ref windows (full; fused: inside the conv2 launch) and the alt runs (15 codes -> 8
+    // rows; fused: the whole alt conv2 patch, kC1Pat codes -> kDA[2] rows)
+    const bool fuse = fuse_conv1(h, nullptr);
+    const C1Src f1{ref + (long long)v0 * stride, stride, nv, mode, 0, kLen};
+    if (!fuse && (rc = run_conv1(h, nullptr, f1.codes, stride, nv, mode, 0, R, kLen, kS1, st))) return rc;
+    if (fuse) {
+      delta_codes2<<<dim3((R + 4) / 5), dim3(5 * kC1PatStride), 0, sa>>>(alt, stride, nv, v0, var_pos, h->delta_codes, R);
+      if ((rc = check_launch("delta_codes2"))) return rc;
+      DeltaScope ds(h);
+      if ((rc = run_conv1(h, nullptr, h->delta_codes, kC1PatStride, R, EXPECTO_STRAND_FWD, 0, R, kC1Pat, kDA[2], sa,
+                          h->DA)))
+        return rc;
+    } else {
+      delta_codes<<<dim3((R + 15) / 16), dim3(256), 0, sa>>>(alt, stride, nv, v0, var_pos, h->delta_codes, R);
+      if ((rc = check_launch("delta_codes"))) return rc;
       DeltaScope ds(h);
       if ((rc = run_conv1(h, nullptr, h->delta_codes, 16, R, EXPECTO_STRAND_FWD, 0, R, kDA[1], kDW[1], sa, h->D0)))
         return rc;
@@ -1849,10 +1955,14 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
       const ConvGeo& g = kConv[l];
       const int L = l + 2;
       if ((rc = order(st, sa, h->pev[1 + 2 * l]))) return rc;   // src (ref layer l-1) written
-      if ((rc = run_conv(h, l, src, dst, R, g.s_in, g.t_valid, g.s_out, g.pool != 0, st))) return rc;
+      const bool fused = l == 0 && fuse;   // the alt conv2 patch is already in DA
+      if ((rc = run_conv(h, l, src, dst, R, g.s_in, g.t_valid, g.s_out, g.pool != 0, st, fused ? &f1 : nullptr)))
+        return rc;
       const int row16 = g.cin * eb / 16;
-      delta_assemble<<<dim3(R), dim3(256), 0, sa>>>(src, g.s_in, dprev, L, row16, nv, v0, var_pos, h->DA);
-      if ((rc = check_launch("delta_assemble"))) return rc;
+      if (!fused) {
+        delta_assemble<<<dim3(R), dim3(256), 0, sa>>>(src, g.s_in, dprev, L, row16, nv, v0, var_pos, h->DA);
+        if ((rc = check_launch("delta_assemble"))) return rc;
+      }
       if ((rc = order(sa, st, h->pev[2 + 2 * l]))) return rc;   // src read: ref l+1 may overwrite it
       DeltaScope ds(h);
       if ((rc = run_conv(h, l, h->DA, dnext, R, kDA[L], kDW[L], kDW[L], g.pool != 0, sa))) return rc;
@@ -2090,6 +2200,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   if (const char* e = getenv("EXPECTO_FC_WIDE")) h->fc_wide = atoi(e) != 0;                   // same bits
   if (const char* e = getenv("EXPECTO_OVERLAP")) h->overlap = atoi(e) != 0;   // same bits either way
   if (const char* e = getenv("EXPECTO_POOL_ONE_PASS")) h->pool_one_pass = atoi(e) != 0;   // same bits either way
+  if (const char* e = getenv("EXPECTO_FUSE_CONV1")) h->fuse_conv1 = atoi(e) != 0;         // same bits either way
   if (const char* e = getenv("EXPECTO_SEG_CHUNK_WINDOWS")) h->seg_chunk_windows = atoi(e);   // same bits either way
   if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)
     const int v = atoi(e);

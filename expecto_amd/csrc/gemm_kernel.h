@@ -53,7 +53,21 @@ struct GemmArgs {
   int m_group;              // FC m_fastest 3: M tiles per dispatch group (see gemm_fc_h3p_body)
   int n_tile_cols;          // f16x3 split-K FC: columns per N tile the caller tiled for (FCW_BN:
                             // beluga_fc_h3w; 0 = the 160-column kernels)
+  // conv2 with conv1 fused (f16x3, beluga_conv_h3p with TM & H3P_FUSE_CONV1): A is not read; the
+  // producer waves compute each 32-channel chunk's slab of conv1 rows from base codes.  Conv1 row
+  // m = (window w, position t) with w = m / s_in; window w is code row c1_row0 + w of c1_codes
+  // (c1_mode: 0 fwd, 1 rc, 2 both = rows >= c1_n_src are the rc of row - c1_n_src, as
+  // EXPECTO_STRAND_*), c1_len bases; c1_n_win windows, c1_len - 7 valid conv1 rows each.
+  const unsigned char* c1_codes;
+  long long c1_stride;
+  long long c1_row0;
+  int c1_n_src, c1_mode, c1_len, c1_n_win;
+  const _Float16* c1_w;     // conv1 weight planes [320][hi 32 | lo 32] (k = tap*4 + ci)
+  const float* c1_cs;       // conv1 per-channel unscale
+  const float* c1_b;        // conv1 bias
+  float c1_osc;             // conv2 input scale 2^sx[0]
 };
+constexpr int H3P_FUSE_CONV1 = 16384;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -91,6 +105,13 @@ __device__ __forceinline__ void split3(const floatx4 x, bf16x4& h, bf16x4& m, bf
 //      on the bf16x6 path.
 typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 typedef _Float16 halfx4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// fp16 1.0 (0x3C00) in the half of channel c within the channel pair (0,1) or (2,3): one dword of
+// a one-hot conv1 operand fragment (codes 0..3 = A,G,C,T; 4 = N, all zero)
+__device__ __forceinline__ unsigned onehot_h2(unsigned c, unsigned hi_pair) {
+  return (c >> 1) == hi_pair ? (0x3C00u << ((c & 1u) * 16u)) : 0u;
+}
 
 template <int PL>
 __device__ __forceinline__ long long act_index(long long row, long long ld, int n) {
@@ -1597,6 +1618,172 @@ __global__ __launch_bounds__(256, 1) void beluga_conv_h3r(GemmArgs p) {
 // kernel: bitwise equal.
 // NSB: B ring depth; 4 gives the producers' pieces two stages to land (slab pieces then go out
 // at taps 0-5 only, so the vmcnt that leaves the last two stages' B pieces in flight covers them).
+// Producer waves of conv2 with conv1 FUSED (TM & H3P_FUSE_CONV1; f16x3).  Instead of LDS-DMA
+// copies of conv1's stored planes, the producers compute each 32-channel chunk's A slab (288 conv1
+// rows x 32 channels, hi and lo planes) from base codes -- conv1's 2 x 5 GB of plane writes and
+// re-reads per 200-window step never reach HBM.  Conv1 is the K = 32 one-hot GEMM of
+// beluga_conv1_h3 (k = tap*4 + channel) issued TRANSPOSED: A = the chunk's weight planes (rows =
+// channels), B = the one-hot fragment of 16 slab rows (a lane's positions t+2fq, t+2fq+1), so the
+// 16x16 result gives a lane 4 consecutive CHANNELS of one row = one 8-byte piece of the slab row
+// per plane.  The dot products are those of beluga_conv1_h3 over the same k (products x*w_lo
+// into 0, then x*w_hi), followed by its epilogue (fmaf(acc, cs*osc, b*osc), ReLU, plain split):
+// bitwise the planes beluga_conv1_h3 stores, so conv2's output is bitwise the unfused one
+// (tests/test_gpu_forward.py).  Work per chunk and workgroup: 18 groups of 16 rows x 2 channel
+// blocks x 2 MFMAs (72 MFMAs beside the consumers' 3,840, +1.9 %) and 36 values per producer lane.
+// Schedule: the one-hot fragments of the producer's <= 5 groups (groups pw + 4i) are built once
+// per tile from codes (global byte loads); chunk c+1's weights are loaded at tap 0 of chunk c and
+// its slab groups computed at taps 1..5, written with ds_write_b64 and drained (lgkmcnt(0)) before
+// those taps' barriers -- slab c+1 is complete at barrier 5, before the consumers read it (tap 7's
+// PF read, after barrier 6).  The B ring is issued exactly as in the unfused producer.
+template <int NSB, bool PF>
+__device__ __forceinline__ void conv12_producer(const GemmArgs& p, char* smem, long long m0, int n0, int pw,
+                                                int lane) {
+  using G = SlabGeo<4>;
+  constexpr int ROW_KB = 128;
+  constexpr int NG = 5;                               // slab groups per producer wave (18 over 4 waves)
+  const int kb_total = (int)(p.ldb / GBK);
+  const int nchunk = (int)(p.lda / GBK);
+  const int nk = nchunk * 8;
+  char* const aslab = smem;
+  char* const bring = smem + 2 * G::ASLAB;
+  auto swz = [](int r) { return conv_swz<0>(r); };
+  // B ring pieces: as gemm_conv_h3p_body's producers
+  const char* Bb = (const char*)p.Bp + (long long)n0 * kb_total * ROW_KB;
+  unsigned boff[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int g = pw + 4 * j;
+    const int pl = g / 10, r = 16 * (g % 10) + (lane >> 2);
+    const int c = (lane & 3) ^ swz(r);
+    boff[j] = (unsigned)((long long)r * kb_total * ROW_KB + pl * 64 + 16 * c);
+  }
+  const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, 0x7fffffff, 0x00020000);
+  auto issue_b = [&](int s, int slot) {
+    char* base = bring + slot * H3C_BSTAGE;
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + (pw + 4 * j) * 1024), 16, boff[j],
+                                               (unsigned)(s * ROW_KB), 0, 0);
+  };
+  // one-hot B fragments of the wave's slab rows (built once per tile)
+  const int fr = lane & 15, fq = lane >> 4;
+  halfx8 oh[NG];
+  bool rvalid[NG];
+#pragma unroll
+  for (int i = 0; i < NG; ++i) {
+    const int g = pw + 4 * i;
+    unsigned c0 = 4, c1 = 4;
+    rvalid[i] = false;
+    if (g < G::GROUPS) {
+      const long long m = m0 + 16 * g + fr;
+      const long long w = m / p.s_in;
+      const int t = (int)(m - w * p.s_in);
+      if (w < p.c1_n_win) {
+        long long src = p.c1_row0 + w;
+        bool rc = p.c1_mode == 1;
+        if (p.c1_mode == 2 && src >= p.c1_n_src) {
+          src -= p.c1_n_src;
+          rc = true;
+        }
+        const unsigned char* row = p.c1_codes + src * p.c1_stride;
+        const int pos = t + 2 * fq;
+        if (pos < p.c1_len) c0 = row[rc ? p.c1_len - 1 - pos : pos];
+        if (pos + 1 < p.c1_len) c1 = row[rc ? p.c1_len - 2 - pos : pos + 1];
+        if (rc) {
+          c0 = c0 < 4 ? 3 - c0 : c0;
+          c1 = c1 < 4 ? 3 - c1 : c1;
+        }
+        rvalid[i] = t < p.c1_len - 7;
+      }
+    }
+    const u32x4 u = {onehot_h2(c0, 0), onehot_h2(c0, 1), onehot_h2(c1, 0), onehot_h2(c1, 1)};
+    oh[i] = __builtin_bit_cast(halfx8, u);
+  }
+  // chunk weights: A fragments of channels 32c + 16cb + fr, factors of channels 32c + 16cb + 4fq + j
+  halfx8 wh[2], wl[2];
+  floatx4 sc[2], bb[2];
+  auto load_w = [&](int c) {
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const _Float16* w = p.c1_w + (32 * c + 16 * cb + fr) * 64 + 8 * fq;
+      wh[cb] = *(const halfx8*)w;
+      wl[cb] = *(const halfx8*)(w + 32);
+      sc[cb] = *(const floatx4*)(p.c1_cs + 32 * c + 16 * cb + 4 * fq);
+      bb[cb] = *(const floatx4*)(p.c1_b + 32 * c + 16 * cb + 4 * fq);
+    }
+  };
+  auto scale_w = [&]() {   // cs * osc and b * osc, as beluga_conv1_h3 forms them (once per chunk)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      sc[cb] *= p.c1_osc;
+      bb[cb] *= p.c1_osc;
+    }
+  };
+  float vmax = 0.f;
+  auto slab_group = [&](char* base, int i) {
+    const int g = pw + 4 * i;
+    if (g >= G::GROUPS) return;
+    const int r = 16 * g + fr;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      floatx4v c = {0.f, 0.f, 0.f, 0.f};
+      c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[cb], oh[i], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cb], oh[i], c, 0, 0, 0);
+      floatx4 v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = fmaxf(fmaf(c[j], sc[cb][j], bb[cb][j]), 0.f);
+      const float vm = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+      vmax = fmaxf(vmax, rvalid[i] ? vm : 0.f);
+      // split_h2p of the 4 values, converted in pairs (v_cvt_pk_f16_f32: the same RNE conversion)
+      const halfx4 hv = __builtin_convertvector(v, halfx4);
+      const halfx4 lv = __builtin_convertvector(v - __builtin_convertvector(hv, floatx4), halfx4);
+      const int off = r * 64 + 16 * ((2 * cb + (fq >> 1)) ^ swz(r)) + 8 * (fq & 1);
+      *(halfx4*)(base + off) = hv;
+      *(halfx4*)(base + G::APLANE + off) = lv;
+    }
+  };
+  load_w(0);
+  scale_w();
+  issue_b(0, 0);
+  issue_b(min(1, nk - 1), 1);
+  if constexpr (NSB == 4) issue_b(min(2, nk - 1), 2);
+#pragma unroll
+  for (int i = 0; i < NG; ++i) slab_group(aslab, i);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if constexpr (NSB == 4) {
+    if constexpr (PF)
+      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");    // stages 0 and 1 landed
+    else
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  int slot = 0;
+  for (int c = 0; c < nchunk; ++c) {
+    const bool more = c + 1 < nchunk;
+    char* const nslab = aslab + ((c + 1) & 1) * G::ASLAB;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int s = c * 8 + t;
+      const int lslot = slot == 0 ? NSB - 1 : slot - 1;
+      if (t == 0 && more) load_w(c + 1);
+      if (t == 1 && more) scale_w();
+      if (t >= 1 && t <= NG && more) slab_group(nslab, t - 1);
+      issue_b(min(s + NSB - 1, nk - 1), lslot);
+      if constexpr (NSB == 4 && !PF)
+        asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      if (t >= 1 && t <= NG) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      slot = slot + 1 == NSB ? 0 : slot + 1;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (!(vmax < 65504.f)) *p.ovf = 1;   // conv1 value out of fp16 range: recomputed (bf16x6)
+}
+
 template <int LAYER, int EPI, int TM, int NSB>
 __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem) {
   static_assert(NSB == 3 || NSB == 4, "B ring depth");
@@ -1625,6 +1812,11 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
   char* const bring = smem + 2 * G::ASLAB;
 
   if (wave >= 4) {
+    if constexpr ((TM & H3P_FUSE_CONV1) != 0) {   // conv2 with conv1 fused: slabs from base codes
+      conv12_producer<NSB, PF>(p, smem, m0, n0, wave - 4, lane);
+      if constexpr (EPI == EPI_RELU || EPI == EPI_RELU_POOL4) __builtin_amdgcn_s_barrier();
+      return;
+    }
     // ---------------- producer: all LDS-DMA issue ----------------
     const int pw = wave - 4;
     const char* Ab = (const char*)p.A + m0 * lda_kb * ROW_KB;
