@@ -90,6 +90,8 @@ def kernel_name(layer: str, precision: str, segments: bool = True) -> str:
     if precision == "f16x3":
         if l in (7, 8):   # split-K FC GEMMs on 336-column tiles (beluga_fc_h3w)
             return f"beluga_fc_h3w<{l}, {e}, 0>"
+        if layer == "conv2" and os.environ.get("EXPECTO_FUSE_CONV1", "1") != "0":
+            return f"beluga_conv_h3p<{l}, {e}, 16640, 4>"   # conv1 fused into the producers (256 | 16384)
         return f"beluga_conv_h3p<{l}, {e}, 256, 4>"   # producer / consumer 256-row tiles (every conv layer)
     return f"beluga_gemm<{l}, {e}, 4, 2, 32, 1>"
 

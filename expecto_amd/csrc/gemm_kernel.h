@@ -68,7 +68,6 @@ struct GemmArgs {
   float c1_osc;             // conv2 input scale 2^sx[0]
 };
 constexpr int H3P_FUSE_CONV1 = 16384;
-
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
