@@ -20,8 +20,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -918,6 +920,160 @@ __global__ void calib_codes(uint8_t* __restrict__ codes, long long n, unsigned s
 
 using namespace expecto;
 
+
+// ---- conv1 + ReLU + conv2 as a k-mer table (f16x3 path, base-code inputs) ----------------
+// Conv1 (k = 8) sees 8 bases, so relu(conv1) at position p is a function of the 8-mer at p, and
+// conv2 (k = 8) at p is  sum_{j<8} W2_j relu(conv1(p + j)) = sum_{i<4} T_i(9-mer at p + 2i)  with
+//   T_i(x_0..x_8) = W2_{2i} relu(conv1(x_0..x_7)) + W2_{2i+1} relu(conv1(x_1..x_8))
+// (Beluga.py:23-26 regrouped: a tap pair shares 9 bases).  Over the code alphabet A,G,C,T,N (N =
+// the zero one-hot column, chromatin.py:155-160) T has 4 x 5^9 rows of 320 values (10 GB fp32),
+// built once per weight set in fp64 -- the conv1 sums, the 320-deep conv2 products and the pair
+// sum -- and rounded to fp32 once.  The conv2 + pool1 layer of every f16x3 forward from codes then
+// is a gather (conv2_kmer_pool): a pooled row reads 16 table rows (4 conv2 rows x 4 tap pairs,
+// 20 KB) and adds them, in place of 4 x 819,200 multiply-adds x 3 f16x3 products on the MFMAs.
+// The table is MORE accurate than the MFMA path (one fp32 rounding per entry and three fp32 adds
+// per conv2 value, against 22-bit operands and a 2,560-long fp32 accumulation); every path (per
+// window, segments, pairs, the alt-delta patches) computes a conv2 row by this one formula from
+// its codes, so the paths stay bitwise equal to each other.
+constexpr int kMer8 = 390625;           // 5^8
+constexpr long long kMer9 = 1953125LL;  // 5^9
+
+// F[m8][c] = relu(conv1) of 8-mer m8 (digit k = code at tap k, base 5), fp64
+__global__ __launch_bounds__(320) void kmer_conv1(const float* __restrict__ w1, const float* __restrict__ b1,
+                                                  double* __restrict__ F) {
+  const int m8 = blockIdx.x, co = threadIdx.x;
+  double s = b1[co];
+  int v = m8;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int d = v % 5;
+    v /= 5;
+    if (d < 4) s += (double)w1[co * 32 + d * 8 + k];   // reference layout [320][4][1][8]
+  }
+  F[(long long)m8 * 320 + co] = s > 0.0 ? s : 0.0;
+}
+
+// G[m8][co] = sum_ci W2[co][ci][tap] F[m8][ci] in fp64 (wt0: the repacked conv2 weights,
+// [co][ci/32][tap][ci%32]); 64 x 64 tiles, 4 x 4 outputs per thread
+__global__ __launch_bounds__(256) void kmer_conv2(const double* __restrict__ F, const float* __restrict__ wt0, int tap,
+                                                  double* __restrict__ G) {
+  __shared__ double fs[16][65], ws[16][65];
+  const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  double acc[4][4] = {};
+  for (int k0 = 0; k0 < 320; k0 += 16) {
+    for (int e = threadIdx.x; e < 16 * 64; e += 256) {
+      const int r = e >> 4, c = e & 15, ci = k0 + c;
+      const int m = m0 + r;
+      fs[c][r] = m < kMer8 ? F[(long long)m * 320 + ci] : 0.0;
+      ws[c][r] = (double)wt0[(long long)(n0 + r) * 2560 + (ci >> 5) * 256 + tap * 32 + (ci & 31)];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      double a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a[i] = fs[c][ty + 16 * i];
+        b[i] = ws[c][tx + 16 * i];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fma(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + ty + 16 * i;
+    if (m >= kMer8) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) G[(long long)m * 320 + n0 + tx + 16 * j] = acc[i][j];
+  }
+}
+
+// T[m9][co] = fp32(Ga[first 8-mer of m9][co] + Gb[last 8-mer][co]); the digits of m9 are the
+// codes x_0..x_8 (base 5, x_0 lowest), so the first 8-mer is m9 % 5^8 and the last m9 / 5
+__global__ void kmer_pair(const double* __restrict__ Ga, const double* __restrict__ Gb, float* __restrict__ T) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= kMer9 * 320) return;
+  const long long m9 = e / 320;
+  const int co = (int)(e - m9 * 320);
+  T[e] = (float)(Ga[(m9 % kMer8) * 320 + co] + Gb[(m9 / 5) * 320 + co]);
+}
+
+// conv2 + bias + ReLU + maxpool4 of `rows` pooled rows per window from base codes (window w =
+// code row row0 + w, strand mode as beluga_conv1_h3, code 4 past len), gathered from the k-mer
+// table; output: the f16x3 planes of the pooled rows (scaled by osc = 2^sx[1], plain split, as
+// the MFMA conv2's epilogue stores them), row w * s_out + g.  640 threads = 8 pooled rows x 80
+// channel quads; a quad's 16 table reads are 16-B loads of one 1,280-B table row each.
+constexpr int KP_ROWS = 8;
+__global__ __launch_bounds__(640) void conv2_kmer_pool(const uint8_t* __restrict__ codes, long long stride, int n_src,
+                                                       int mode, long long row0, int len, int rows, int row_blocks,
+                                                       int s_out, const float* __restrict__ T,
+                                                       const float* __restrict__ b2, float osc,
+                                                       float* __restrict__ out, int* __restrict__ ovf) {
+  __shared__ unsigned char cl[4 * KP_ROWS + 16];
+  __shared__ int ix[4 * KP_ROWS + 8];
+  const long long win = blockIdx.x / row_blocks;
+  const int g0 = (int)(blockIdx.x - win * row_blocks) * KP_ROWS;
+  const int tid = threadIdx.x;
+  long long src = row0 + win;
+  bool rc = mode == EXPECTO_STRAND_RC;
+  if (mode == EXPECTO_STRAND_BOTH && src >= n_src) {
+    src -= n_src;
+    rc = true;
+  }
+  const int p0 = 4 * g0;
+  if (tid < 4 * KP_ROWS + 15) {   // bases p0 .. p0 + 4*KP_ROWS + 14: the block's 9-mers at p0 + o, o < 4*KP_ROWS + 6
+    const int pos = p0 + tid;
+    unsigned c = 4;
+    if (pos < len) {
+      c = codes[src * stride + (rc ? len - 1 - pos : pos)];
+      if (rc && c < 4) c = 3 - c;
+    }
+    cl[tid] = (unsigned char)c;
+  }
+  __syncthreads();
+  if (tid < 4 * KP_ROWS + 6) {
+    int v = 0;
+#pragma unroll
+    for (int k = 8; k >= 0; --k) v = v * 5 + cl[tid + k];
+    ix[tid] = v;
+  }
+  __syncthreads();
+  const int lr = tid / 80, q = tid - lr * 80, g = g0 + lr;
+  if (g >= rows) return;
+  floatx4 t[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      t[r][i] = *reinterpret_cast<const floatx4*>(T + ((long long)i * kMer9 + ix[4 * lr + r + 2 * i]) * 320 + 4 * q);
+  const floatx4 bb = *reinterpret_cast<const floatx4*>(b2 + 4 * q);
+  floatx4 m;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const floatx4 s = ((t[r][0] + t[r][1]) + t[r][2]) + t[r][3];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) m[c] = r == 0 ? s[c] : fmaxf(m[c], s[c]);
+  }
+  floatx4 v;
+  float vmax = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    v[c] = fmaxf(fmaf(m[c], osc, bb[c] * osc), 0.f);   // maxpool(relu(x + b)) = relu(max(x) + b), scaled
+    vmax = fmaxf(vmax, v[c]);
+  }
+  const halfx4 hv = __builtin_convertvector(v, halfx4);
+  const halfx4 lv = __builtin_convertvector(v - __builtin_convertvector(hv, floatx4), halfx4);
+  char* d = reinterpret_cast<char*>(out) + ((win * s_out + g) * 10 + (q >> 3)) * 128 + (q & 7) * 8;
+  *reinterpret_cast<halfx4*>(d) = hv;
+  *reinterpret_cast<halfx4*>(d + 64) = lv;
+  if (!(vmax < 65504.f)) *ovf = 1;   // out of fp16 range: the call is recomputed (bf16x6)
+}
+
 // ---- handle -----------------------------------------------------------------------------
 namespace {
 constexpr int kNumLayers = 9;
@@ -1023,6 +1179,9 @@ struct expecto_beluga {
   int cus = 0;                        // compute units of the device (workgroups per round)
   bool pool_one_pass = true;          // segment path: pool2 of all phases in one pass (same bits)
   bool fuse_conv1 = true;             // f16x3 codes input: conv1 inside the conv2 launch (EXPECTO_FUSE_CONV1; same bits)
+  bool kmer_on = true;                // f16x3 codes input: conv1 + conv2 + pool1 from the k-mer table (EXPECTO_CONV2_TABLE)
+  float* kmer = nullptr;              //   the table (shared by handles with the same conv1 / conv2 weights)
+  uint64_t kmer_key = 0;
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, int>> pending;  // (layer, event index of start)
@@ -1050,6 +1209,90 @@ int dalloc(expecto_beluga* h, float** p, size_t nfloat) {
 }
 
 int npad_of(int n) { return (n + GBN - 1) / GBN * GBN; }
+
+// Process-wide k-mer tables: handles of one device with the same conv1 / conv2 weights share one
+// (tests and benches create many handles of one seeded model); refcounted, freed with the last.
+struct KmerEntry {
+  int device;
+  uint64_t key;
+  float* T;
+  int refs;
+};
+std::mutex g_kmer_mu;
+std::vector<KmerEntry> g_kmer;
+
+uint64_t fnv1a(const void* p, size_t n, uint64_t hsh = 1469598103934665603ULL) {
+  const unsigned char* b = static_cast<const unsigned char*>(p);
+  for (size_t i = 0; i < n; ++i) hsh = (hsh ^ b[i]) * 1099511628211ULL;
+  return hsh;
+}
+
+// Build (or share) the handle's k-mer table from its conv1 weights (w1, b1) and repacked conv2
+// weights.  If its 10 GB do not fit, the handle runs conv2 on the MFMAs instead (kmer stays null).
+int kmer_acquire(expecto_beluga* h, const float* const* params, hipStream_t st) {
+  std::vector<float> hw(320 * 32 + 320 + 320 * 320 * 8);
+  EXPECTO_HIP_CHECK(hipMemcpyAsync(hw.data(), params[0], 320 * 32 * sizeof(float), hipMemcpyDeviceToHost, st));
+  EXPECTO_HIP_CHECK(hipMemcpyAsync(hw.data() + 320 * 32, params[1], 320 * sizeof(float), hipMemcpyDeviceToHost, st));
+  EXPECTO_HIP_CHECK(hipMemcpyAsync(hw.data() + 320 * 33, params[2], 320 * 320 * 8 * sizeof(float),
+                                   hipMemcpyDeviceToHost, st));
+  EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
+  const uint64_t key = fnv1a(hw.data(), hw.size() * sizeof(float));
+  std::lock_guard<std::mutex> lock(g_kmer_mu);
+  for (KmerEntry& e : g_kmer)
+    if (e.device == h->device && e.key == key) {
+      ++e.refs;
+      h->kmer = e.T;
+      h->kmer_key = key;
+      return EXPECTO_OK;
+    }
+  void *t = nullptr, *f = nullptr, *gg = nullptr;
+  const size_t tb = 4 * (size_t)kMer9 * 320 * sizeof(float), fb = (size_t)kMer8 * 320 * sizeof(double);
+  if (hipMalloc(&t, tb) != hipSuccess || hipMalloc(&f, fb) != hipSuccess || hipMalloc(&gg, 2 * fb) != hipSuccess) {
+    (void)hipGetLastError();
+    for (void* x : {t, f, gg})
+      if (x) (void)hipFree(x);
+    return EXPECTO_OK;   // no table: conv2 on the MFMAs
+  }
+  float* T = static_cast<float*>(t);
+  double* F = static_cast<double*>(f);
+  double* G = static_cast<double*>(gg);
+  kmer_conv1<<<dim3(kMer8), dim3(320), 0, st>>>(h->w1, h->b1, F);
+  int rc = check_launch("kmer_conv1");
+  for (int i = 0; i < 4 && !rc; ++i) {
+    const dim3 grid((kMer8 + 63) / 64, 5);
+    kmer_conv2<<<grid, dim3(256), 0, st>>>(F, h->wt[0], 2 * i, G);
+    kmer_conv2<<<grid, dim3(256), 0, st>>>(F, h->wt[0], 2 * i + 1, G + (size_t)kMer8 * 320);
+    kmer_pair<<<dim3((unsigned)((kMer9 * 320 + 255) / 256)), dim3(256), 0, st>>>(G, G + (size_t)kMer8 * 320,
+                                                                                T + (size_t)i * kMer9 * 320);
+    rc = check_launch("kmer table");
+  }
+  if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = check_launch("kmer table sync");
+  (void)hipFree(f);
+  (void)hipFree(gg);
+  if (rc) {
+    (void)hipFree(t);
+    return rc;
+  }
+  g_kmer.push_back({h->device, key, T, 1});
+  h->kmer = T;
+  h->kmer_key = key;
+  return EXPECTO_OK;
+}
+
+void kmer_release(expecto_beluga* h) {
+  if (!h->kmer) return;
+  std::lock_guard<std::mutex> lock(g_kmer_mu);
+  for (size_t i = 0; i < g_kmer.size(); ++i)
+    if (g_kmer[i].T == h->kmer) {
+      if (--g_kmer[i].refs == 0) {
+        (void)hipFree(g_kmer[i].T);
+        g_kmer.erase(g_kmer.begin() + (long)i);
+      }
+      break;
+    }
+  h->kmer = nullptr;
+}
+
 
 // Host -> device copies of one call's tables through a pinned staging slot.  The slot was last
 // filled two calls ago; its event fires once those copies ran (they precede that call's kernels
@@ -1270,6 +1513,23 @@ struct C1Src {
 // EXPECTO_FUSE_CONV1=0 keeps the separate beluga_conv1_h3 launch.
 bool fuse_conv1(const expecto_beluga* h, const float* x) {
   return h->fuse_conv1 && !x && g_precision == EXPECTO_PRECISION_F16X3 && h->w1h;
+}
+
+// conv1 + conv2 + pool1 from the k-mer table (f16x3, codes input; EXPECTO_CONV2_TABLE=0 runs them
+// on the MFMAs): `rows` pooled rows per window into dst rows w * s_out + g
+bool use_kmer(const expecto_beluga* h, const float* x) {
+  return h->kmer && !x && g_precision == EXPECTO_PRECISION_F16X3;
+}
+
+int run_conv2_kmer(expecto_beluga* h, const C1Src& f, long long n_win, int rows, int s_out, float* dst, hipStream_t st) {
+  LayerTimer lt(h, 1, st);
+  const int rb = (rows + KP_ROWS - 1) / KP_ROWS;
+  const long long nblk = n_win * rb;
+  EXPECTO_REQUIRE(nblk > 0 && nblk < (1LL << 31) && f.len >= 18, "conv2 k-mer grid / window length");
+  conv2_kmer_pool<<<dim3((unsigned)nblk), dim3(640), 0, st>>>(f.codes, f.stride, f.n_src, f.mode, f.row0, f.len, rows,
+                                                              rb, s_out, h->kmer, h->bt[0], exp2i(h->sx[1]), dst,
+                                                              h->ovf);
+  return check_launch("conv2_kmer_pool");
 }
 
 // conv layer l (0 = conv2 .. 4 = conv6) over `groups` row groups of s_in rows each.  f1 (conv2
@@ -1500,16 +1760,19 @@ int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long 
                   int mode, long long row0, int nb, float* y, hipStream_t st) {
   int rc;
   g_precision = h->precision;
-  const bool fuse = fuse_conv1(h, x);
+  const bool kmer = use_kmer(h, x);
+  const bool fuse = !kmer && fuse_conv1(h, x);
   const C1Src f1{codes, code_stride, n_src, mode, row0, kLen};
-  if (!fuse && (rc = run_conv1(h, x, codes, code_stride, n_src, mode, row0, nb, kLen, kS1, st))) return rc;
+  if (!kmer && !fuse && (rc = run_conv1(h, x, codes, code_stride, n_src, mode, row0, nb, kLen, kS1, st))) return rc;
   float* src = h->P;
   float* dst = h->Q;
   for (int l = 0; l < 5; ++l) {
     const ConvGeo& g = kConv[l];
-    if ((rc = run_conv(h, l, src, dst, nb, g.s_in, g.t_valid, g.s_out, g.pool != 0, st,
-                       l == 0 && fuse ? &f1 : nullptr)))
-      return rc;
+    if (l == 0 && kmer)
+      rc = run_conv2_kmer(h, f1, nb, g.t_valid, g.s_out, dst, st);
+    else
+      rc = run_conv(h, l, src, dst, nb, g.s_in, g.t_valid, g.s_out, g.pool != 0, st, l == 0 && fuse ? &f1 : nullptr);
+    if (rc) return rc;
     std::swap(src, dst);
   }
   return run_fc(h, src, nullptr, nb, y, st);  // src = act5 (buffer Q), 106 x 640 rows per window
@@ -1741,21 +2004,23 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
       }
       // conv1 from codes: virtual rows = segments; rc mode mirrors inside the kernel (fused: inside
       // the conv2 launch)
-      const bool fuse = fuse_conv1(h, nullptr);
+      const bool kmer = use_kmer(h, nullptr);
+      const bool fuse = !kmer && fuse_conv1(h, nullptr);
       const C1Src f1{codes + (long long)s0 * code_stride, code_stride, ns, is_rc ? EXPECTO_STRAND_RC : EXPECTO_STRAND_FWD,
                      0, L};
-      if (!fuse && (rc = run_conv1(h, nullptr, f1.codes, code_stride, ns, f1.mode, 0, ns, L, g.S1, st))) return rc;
+      if (!kmer && !fuse && (rc = run_conv1(h, nullptr, f1.codes, code_stride, ns, f1.mode, 0, ns, L, g.S1, st)))
+        return rc;
       if (pr) {
         seg_delta_table<<<dim3((ns + 255) / 256), dim3(256), 0, sa>>>(h->seg_var_d, s0, ns, is_rc ? 1 : 0, gd, n_ph,
                                                                      ph4, h->seg_tab);
         if ((rc = check_launch("seg_delta_table"))) return rc;
-        if (fuse) {   // the alt conv2 patch straight from the alt codes (conv1 of kC1Pat codes -> DA)
+        if (kmer || fuse) {   // the alt conv2 patch straight from the alt codes (k-mer table, or conv1 -> DA)
           seg_delta_codes2<<<dim3((ns + 4) / 5), dim3(5 * kC1PatStride), 0, sa>>>(
               codes, code_stride, pr->alt_code, s0, ns, is_rc ? 1 : 0, L, h->seg_tab, h->delta_codes);
           if ((rc = check_launch("seg_delta_codes2"))) return rc;
           DeltaScope ds(h);
-          if ((rc = run_conv1(h, nullptr, h->delta_codes, kC1PatStride, ns, EXPECTO_STRAND_FWD, 0, ns, kC1Pat, kDA[2],
-                              sa, h->DA)))
+          if (fuse && (rc = run_conv1(h, nullptr, h->delta_codes, kC1PatStride, ns, EXPECTO_STRAND_FWD, 0, ns, kC1Pat,
+                                      kDA[2], sa, h->DA)))
             return rc;
         } else {
           seg_delta_codes<<<dim3((ns + 15) / 16), dim3(256), 0, sa>>>(codes, code_stride, pr->alt_code, s0, ns,
@@ -1768,10 +2033,20 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
         }
       }
       // conv2 + pool1 (P -> Q), conv3 (Q -> P), conv4 unpooled (P -> Q); alt runs D0 <-> D1
-      if (pr && !fuse && (rc = alt_asm(0, h->P, g.S1, h->D0, kDW[1], 1, 2, 4, 1, kDA[2], h->pev[1], h->pev[2])))
+      if (pr && !kmer && !fuse && (rc = alt_asm(0, h->P, g.S1, h->D0, kDW[1], 1, 2, 4, 1, kDA[2], h->pev[1], h->pev[2])))
         return rc;
-      if ((rc = run_conv(h, 0, h->P, h->Q, ns, g.S1, g.P1, g.P1, true, st, fuse ? &f1 : nullptr))) return rc;
-      if (pr && ((!fuse && (rc = st_wait(h->pev[2]))) || (rc = alt_gemm(0, 1, kDA[2], kDW[2], true, h->D1)))) return rc;
+      if (kmer)
+        rc = run_conv2_kmer(h, f1, ns, g.P1, g.P1, h->Q, st);
+      else
+        rc = run_conv(h, 0, h->P, h->Q, ns, g.S1, g.P1, g.P1, true, st, fuse ? &f1 : nullptr);
+      if (rc) return rc;
+      if (pr && kmer) {   // alt pooled conv2 rows [r2, r2 + kDW[2]) of each segment into D1
+        DeltaScope ds(h);
+        const C1Src fa{h->delta_codes, kC1PatStride, ns, EXPECTO_STRAND_FWD, 0, kC1Pat};
+        if ((rc = run_conv2_kmer(h, fa, ns, kDW[2], kDW[2], h->D1, sa))) return rc;
+      } else if (pr && ((!fuse && (rc = st_wait(h->pev[2]))) || (rc = alt_gemm(0, 1, kDA[2], kDW[2], true, h->D1)))) {
+        return rc;
+      }
       if (pr && (rc = alt_asm(1, h->Q, g.P1, h->D1, kDW[2], 1, 3, 1, 2, kDA[3], h->pev[3], h->pev[4]))) return rc;
       if ((rc = run_conv(h, 1, h->Q, h->P, ns, g.P1, g.T3, g.T3, false, st))) return rc;
       if (pr && ((rc = st_wait(h->pev[4])) || (rc = alt_gemm(1, 1, kDA[3], kDW[3], false, h->D0)))) return rc;
@@ -1930,15 +2205,16 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
     if ((rc = order(st, sa, h->pev[0]))) return rc;   // caller's inputs (and the previous chunk)
     // conv1: ref windows (full; fused: inside the conv2 launch) and the alt runs (15 codes -> 8
     // rows; fused: the whole alt conv2 patch, kC1Pat codes -> kDA[2] rows)
-    const bool fuse = fuse_conv1(h, nullptr);
+    const bool kmer = use_kmer(h, nullptr);
+    const bool fuse = !kmer && fuse_conv1(h, nullptr);
     const C1Src f1{ref + (long long)v0 * stride, stride, nv, mode, 0, kLen};
-    if (!fuse && (rc = run_conv1(h, nullptr, f1.codes, stride, nv, mode, 0, R, kLen, kS1, st))) return rc;
-    if (fuse) {
+    if (!kmer && !fuse && (rc = run_conv1(h, nullptr, f1.codes, stride, nv, mode, 0, R, kLen, kS1, st))) return rc;
+    if (kmer || fuse) {
       delta_codes2<<<dim3((R + 4) / 5), dim3(5 * kC1PatStride), 0, sa>>>(alt, stride, nv, v0, var_pos, h->delta_codes, R);
       if ((rc = check_launch("delta_codes2"))) return rc;
       DeltaScope ds(h);
-      if ((rc = run_conv1(h, nullptr, h->delta_codes, kC1PatStride, R, EXPECTO_STRAND_FWD, 0, R, kC1Pat, kDA[2], sa,
-                          h->DA)))
+      if (fuse && (rc = run_conv1(h, nullptr, h->delta_codes, kC1PatStride, R, EXPECTO_STRAND_FWD, 0, R, kC1Pat, kDA[2],
+                                  sa, h->DA)))
         return rc;
     } else {
       delta_codes<<<dim3((R + 15) / 16), dim3(256), 0, sa>>>(alt, stride, nv, v0, var_pos, h->delta_codes, R);
@@ -1956,16 +2232,25 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
       const int L = l + 2;
       if ((rc = order(st, sa, h->pev[1 + 2 * l]))) return rc;   // src (ref layer l-1) written
       const bool fused = l == 0 && fuse;   // the alt conv2 patch is already in DA
-      if ((rc = run_conv(h, l, src, dst, R, g.s_in, g.t_valid, g.s_out, g.pool != 0, st, fused ? &f1 : nullptr)))
-        return rc;
+      const bool tab = l == 0 && kmer;     // conv2 from the k-mer table (ref windows and alt patches)
+      if (tab)
+        rc = run_conv2_kmer(h, f1, R, g.t_valid, g.s_out, dst, st);
+      else
+        rc = run_conv(h, l, src, dst, R, g.s_in, g.t_valid, g.s_out, g.pool != 0, st, fused ? &f1 : nullptr);
+      if (rc) return rc;
       const int row16 = g.cin * eb / 16;
-      if (!fused) {
+      if (!fused && !tab) {
         delta_assemble<<<dim3(R), dim3(256), 0, sa>>>(src, g.s_in, dprev, L, row16, nv, v0, var_pos, h->DA);
         if ((rc = check_launch("delta_assemble"))) return rc;
       }
       if ((rc = order(sa, st, h->pev[2 + 2 * l]))) return rc;   // src read: ref l+1 may overwrite it
       DeltaScope ds(h);
-      if ((rc = run_conv(h, l, h->DA, dnext, R, kDA[L], kDW[L], kDW[L], g.pool != 0, sa))) return rc;
+      if (tab) {
+        const C1Src fa{h->delta_codes, kC1PatStride, R, EXPECTO_STRAND_FWD, 0, kC1Pat};
+        if ((rc = run_conv2_kmer(h, fa, R, kDW[L], kDW[L], dnext, sa))) return rc;
+      } else if ((rc = run_conv(h, l, h->DA, dnext, R, kDA[L], kDW[L], kDW[L], g.pool != 0, sa))) {
+        return rc;
+      }
       std::swap(src, dst);
       std::swap(dprev, dnext);
     }
@@ -2201,6 +2486,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   if (const char* e = getenv("EXPECTO_OVERLAP")) h->overlap = atoi(e) != 0;   // same bits either way
   if (const char* e = getenv("EXPECTO_POOL_ONE_PASS")) h->pool_one_pass = atoi(e) != 0;   // same bits either way
   if (const char* e = getenv("EXPECTO_FUSE_CONV1")) h->fuse_conv1 = atoi(e) != 0;         // same bits either way
+  if (const char* e = getenv("EXPECTO_CONV2_TABLE")) h->kmer_on = atoi(e) != 0;   // conv2 on the MFMAs (parity, not bits)
   if (const char* e = getenv("EXPECTO_SEG_CHUNK_WINDOWS")) h->seg_chunk_windows = atoi(e);   // same bits either way
   if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)
     const int v = atoi(e);
@@ -2229,6 +2515,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   EXPECTO_HIP_CHECK(hipMemsetAsync(h->Q, 0, act_alloc(qf) * sizeof(float), st));
   // default arithmetic: f16x3 (fp16 weight planes + activation-scale calibration now)
   if ((rc = f16_prepare(h, st))) return fail(rc);
+  if (h->kmer_on && (rc = kmer_acquire(h, params, st))) return fail(rc);
   h->precision = EXPECTO_PRECISION_F16X3;
   EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
   *out = h;
@@ -2237,6 +2524,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
 
 void expecto_beluga_destroy(expecto_beluga_t h) {
   if (!h) return;
+  kmer_release(h);
   if (h->win_seg_d) (void)hipFree(h->win_seg_d);
   if (h->alt_w_d) (void)hipFree(h->alt_w_d);
   if (h->copy_w_d) (void)hipFree(h->copy_w_d);

@@ -42,7 +42,6 @@ def _run(monkeypatch, env, fa, dg, vs, shifts, max_batch=2048, use_segments=True
 
 @pytest.mark.parametrize("env", [{"EXPECTO_SEG_CHUNK_WINDOWS": "1000"}, {"EXPECTO_OVERLAP": "0"},
                                  {"EXPECTO_CONV_TILE": "256"}, {"EXPECTO_POOL_ONE_PASS": "0"},
-                                 {"EXPECTO_FUSE_CONV1": "0"},
                                  {"EXPECTO_FC_WIDE": "0"}, {"EXPECTO_FC_WIDE": "0", "EXPECTO_FC1_ORDER": "2"},
                                  {"EXPECTO_FC_WIDE": "0", "EXPECTO_FC1_ORDER": "0", "EXPECTO_FC1_M_ORDER_MB": "0"},
                                  {"EXPECTO_FC_WIDE": "0", "EXPECTO_FC1_M_GROUP": "3"}])
@@ -63,14 +62,61 @@ def test_fc2_without_split_k(monkeypatch):
     assert_close(seg.cpu().numpy(), base.cpu().numpy(), what="FC2 split 1 vs split 7")
 
 
-@pytest.mark.parametrize("use_pairs", [True, False])
-def test_fused_conv1_bitwise_on_window_paths(monkeypatch, use_pairs):
-    """conv1 inside the conv2 launch (default) vs the separate conv1 launch: the per-window path
-    (forward_codes, fwd + rc) and the pair path (forward_pairs: ref conv2 fused, the alt conv2
-    patch computed from the alt codes) give the same bits."""
+@pytest.mark.parametrize("use_segments,use_pairs", [(True, True), (False, True), (False, False)])
+def test_fused_conv1_bitwise(monkeypatch, use_segments, use_pairs):
+    """conv2 on the MFMAs (EXPECTO_CONV2_TABLE=0): conv1 inside the conv2 launch vs the separate
+    conv1 launch give the same bits on the segment-pair path, the per-window path (forward_codes,
+    fwd + rc) and the pair path (forward_pairs: ref conv2 fused, the alt conv2 patch computed from
+    the alt codes)."""
     fa, dg, vs, _ = _setup(n=40)
-    shifts = [-400, 0, 400]
-    fused = _run(monkeypatch, {}, fa, dg, vs, shifts, use_segments=False, use_pairs=use_pairs)
-    sep = _run(monkeypatch, {"EXPECTO_FUSE_CONV1": "0"}, fa, dg, vs, shifts, use_segments=False,
+    shifts = list(range(-20000, 20000, 200)) if use_segments else [-400, 0, 400]
+    base = {"EXPECTO_CONV2_TABLE": "0"}
+    fused = _run(monkeypatch, base, fa, dg, vs, shifts, use_segments=use_segments, use_pairs=use_pairs)
+    sep = _run(monkeypatch, dict(base, EXPECTO_FUSE_CONV1="0"), fa, dg, vs, shifts, use_segments=use_segments,
                use_pairs=use_pairs)
     assert torch.equal(fused, sep), f"max|diff| {float((fused - sep).abs().max())}"
+
+
+@pytest.mark.parametrize("use_segments,use_pairs", [(True, True), (False, True), (False, False)])
+def test_conv2_table_paths_bitwise_and_parity(monkeypatch, use_segments, use_pairs):
+    """conv1 + conv2 + pool1 from the k-mer table (default): the segment-pair, pair and per-window
+    paths agree bit for bit with each other (every conv2 row is the same gather of its codes) and
+    with conv2 on the MFMAs (EXPECTO_CONV2_TABLE=0) to the parity bar."""
+    fa, dg, vs, _ = _setup(n=24)
+    shifts = [-800, -400, 0, 400, 800]
+    tab = _run(monkeypatch, {}, fa, dg, vs, shifts, use_segments=use_segments, use_pairs=use_pairs)
+    ref = _run(monkeypatch, {}, fa, dg, vs, shifts, use_segments=False, use_pairs=False)
+    assert torch.equal(tab, ref), f"max|diff| {float((tab - ref).abs().max())}"
+    mfma = _run(monkeypatch, {"EXPECTO_CONV2_TABLE": "0"}, fa, dg, vs, shifts, use_segments=use_segments,
+                use_pairs=use_pairs)
+    assert_close(tab.cpu().numpy(), mfma.cpu().numpy(), what="conv2 k-mer table vs MFMA")
+
+
+def test_conv2_table_accuracy_against_float64(monkeypatch):
+    """Against a float64 forward, the k-mer table's outputs are at least as accurate as conv2 on
+    the MFMAs (the table is built in fp64 and rounded once; the MFMA path multiplies 22-bit
+    operand splits), and inside the parity bound; N bases (code 4) included."""
+    import os
+    from expecto_amd import beluga
+    from expecto_amd.encode import codes_to_onehot
+    from oracle.beluga_np import forward_torch_cpu
+    rng = np.random.default_rng(21)
+    codes_np = rng.integers(0, 4, (16, 2000)).astype(np.uint8)
+    codes_np[3, 500:900] = 4
+    codes_np[7, ::37] = 4
+    codes = torch.from_numpy(codes_np).cuda()
+    m = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=64)
+    sd64 = {k: v.detach().double() for k, v in m.state_dict().items()}
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    y64 = forward_torch_cpu(sd64, torch.from_numpy(codes_to_onehot(codes_np).astype(np.float64)).unsqueeze(2)).numpy()
+    err = {}
+    for on in ("1", "0"):
+        monkeypatch.setenv("EXPECTO_CONV2_TABLE", on)
+        mm = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=64).cuda()
+        y = mm.forward_codes(codes, 2).cpu().numpy().astype(np.float64)
+        assert mm.engine().f16_state()[0] == 0
+        err[on] = float((np.abs(y - y64) / (1e-4 * np.abs(y64) + 1e-5)).max())
+        del mm
+    monkeypatch.delenv("EXPECTO_CONV2_TABLE")
+    assert err["1"] < 0.5, err
+    assert err["1"] <= 1.25 * err["0"], err
