@@ -77,6 +77,32 @@ DTYPES = {
 }
 
 
+def conv2_table_on() -> bool:
+    """f16x3 conv1 + conv2 + pool1 from the k-mer table (the library default; EXPECTO_CONV2_TABLE=0
+    runs them on the MFMAs)."""
+    return os.environ.get("EXPECTO_CONV2_TABLE", "1") != "0"
+
+
+# 200-window segment (41,800 bp): pooled conv2 rows per segment, and the k-mer gather's algorithmic
+# bytes per pooled row (16 table rows of 320 fp32 read, 320 fp16 hi + lo planes written)
+SEG200_POOL1_ROWS = ((2000 + 199 * 200 - 7) - 7) // 4
+KMER_BYTES_PER_POOLED_ROW = 16 * 320 * 4 + 320 * 4
+
+
+def conv2_table_roofline(layers, n):
+    """HBM roofline of the k-mer gather (conv2_kmer_pool) of the headline: algorithmic bytes per
+    strand launch over its average launch time (HIP events on the launch stream)."""
+    ms, calls, _ = layers["conv2"]
+    if not calls:
+        return None
+    b = n * SEG200_POOL1_ROWS * KMER_BYTES_PER_POOLED_ROW
+    gbs = b / (ms / calls * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": "conv2_kmer_pool", "achieved": gbs, "peak": 8000.0, "unit": "GB/s",
+            "frac": gbs / 8000.0, "bytes_per_launch": b, "avg_launch_ms": ms / calls, "launches": calls,
+            "what": f"{n} segments x {SEG200_POOL1_ROWS} pooled rows x (16 table rows x 1,280 B read + 1,280 B "
+                    f"written); table hits in L2 / Infinity Cache (repeated 9-mers) count as HBM bytes here"}
+
+
 def kernel_name(layer: str, precision: str, segments: bool = True) -> str:
     """rocprofv3 kernel name of a layer's launch.  On the segment path (the headline, configs[2]
     and [4]) conv4 runs unpooled (its pool2 is a separate per-phase kernel)."""
@@ -90,6 +116,8 @@ def kernel_name(layer: str, precision: str, segments: bool = True) -> str:
     if precision == "f16x3":
         if l in (7, 8):   # split-K FC GEMMs on 336-column tiles (beluga_fc_h3w)
             return f"beluga_fc_h3w<{l}, {e}, 0>"
+        if layer == "conv2" and conv2_table_on():
+            return "conv2_kmer_pool"                       # conv1 + conv2 + pool1 gathered from the k-mer table
         if layer == "conv2" and os.environ.get("EXPECTO_FUSE_CONV1", "1") != "0":
             return f"beluga_conv_h3p<{l}, {e}, 16640, 4>"   # conv1 fused into the producers (256 | 16384)
         return f"beluga_conv_h3p<{l}, {e}, 256, 4>"   # producer / consumer 256-row tiles (every conv layer)
@@ -359,7 +387,8 @@ def products_and_peak(precision):
 def roofline(layers, precision, segments=True):
     """MFMA roofline of the dominant GEMM kernel from executed work per launch (library counts)
     and its average launch duration (HIP events on the launch stream)."""
-    dom = max((k for k in GEMM_LAYER_EPI), key=lambda k: layers[k][0])
+    gemm = [k for k in GEMM_LAYER_EPI if not (k == "conv2" and precision == "f16x3" and conv2_table_on())]
+    dom = max(gemm, key=lambda k: layers[k][0])   # (the f16x3 conv2 is a gather: conv2_table_roofline)
     ms, calls, macs = layers[dom]
     fp32_flops_launch = 2.0 * macs / calls
     fp32_tflops = fp32_flops_launch / (ms / calls / 1e3) / 1e12
@@ -744,6 +773,8 @@ def main():
         "executed_fp32_tflops": 2.0 * m["exec_macs_step"] * world / step_s / 1e12,
         "step_mfma_frac": mult * 2.0 * m["exec_macs_step"] / step_s / 1e12 / peak,
         "roofline": roof,
+        "conv2_table_gather": (conv2_table_roofline(m["layers"], n)
+                               if eng.precision == "f16x3" and conv2_table_on() else None),
         "layer_ms_per_step": ms_l,
         "layer_tflops": tf_l,
         "layer_timing": f"separate profiled pass of {m['prof_steps']} steps (HIP events per launch); the "

@@ -33,15 +33,16 @@ def test_reported_kernel_names_exist_in_the_committed_kernel_trace():
 def test_committed_traffic_matches_the_default_workload_key():
     import bench
     key = bench.profile_key()
-    traffic, src = bench.pmc_traffic(key, bench.kernel_name("conv2", "f16x3"))
-    assert traffic is not None and traffic > 0, "re-take profiles: STEPS=prof,pmc tools/gpu_session.sh + collect_profiles.py"
-    assert src.startswith("profiles/")
+    for layer in ("fc1", "conv2"):   # the MFMA roofline's kernel (FC1) and the k-mer gather
+        traffic, src = bench.pmc_traffic(key, bench.kernel_name(layer, "f16x3"))
+        assert traffic is not None and traffic > 0, "re-take profiles: STEPS=prof,pmc tools/gpu_session.sh + collect_profiles.py"
+        assert src.startswith("profiles/")
 
 
 def test_committed_sq_counters_give_the_held_clock():
     import bench
     key = bench.profile_key()
-    held = bench.pmc_held_clock(key, bench.kernel_name("conv2", "f16x3"))
+    held = bench.pmc_held_clock(key, bench.kernel_name("fc1", "f16x3"))   # the dominant MFMA kernel
     assert held is not None, "re-take profiles: STEPS=prof,pmc tools/gpu_session.sh + collect_profiles.py"
     assert 0.3 < held["mfma_busy"] <= 1.0 and 1.0 < held["held_clock_ghz"] < 2.6
 
