@@ -937,6 +937,8 @@ using namespace expecto;
 // its codes, so the paths stay bitwise equal to each other.
 constexpr int kMer8 = 390625;           // 5^8
 constexpr long long kMer9 = 1953125LL;  // 5^9
+constexpr long long kMer11 = 4194304LL; // 4^11: the quad tables cover A, G, C, T only
+constexpr size_t kKmerFloats = (4 * (size_t)kMer9 + 2 * (size_t)kMer11) * 320;   // pair + quad tables, 20.7 GB
 
 // F[m8][c] = relu(conv1) of 8-mer m8 (digit k = code at tap k, base 5), fp64
 __global__ __launch_bounds__(320) void kmer_conv1(const float* __restrict__ w1, const float* __restrict__ b1,
@@ -1003,19 +1005,45 @@ __global__ void kmer_pair(const double* __restrict__ Ga, const double* __restric
   T[e] = (float)(Ga[(m9 % kMer8) * 320 + co] + Gb[(m9 / 5) * 320 + co]);
 }
 
+// Quad tables (round 4): Q_h(y_0..y_10) = sum_{t<4} W2_{4h+t} F(y_t..y_{t+7}), h = 0, 1 -- taps 0-3
+// and 4-7 of conv2, so a conv2 row is Q_0(11-mer at p) + Q_1(11-mer at p + 4): 2 table rows
+// instead of 4.  Over A, G, C, T only (4^11 rows each; 5^11 would be 62.5 GB a table): a
+// conv2 half whose 11-mer holds an N takes the two pair tables instead.  The fp64 sum over the
+// four taps (tap order) is rounded to fp32 once.  G: all 8 taps, [tap][5^8][320].
+__global__ void kmer_quad(const double* __restrict__ G, int h, float* __restrict__ Q) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= kMer11 * 320) return;
+  const long long m11 = e / 320;
+  const int co = (int)(e - m11 * 320);
+  int d[11];
+#pragma unroll
+  for (int k = 0; k < 11; ++k) d[k] = (int)((m11 >> (2 * k)) & 3);
+  double sum = 0.0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    int i5 = 0;
+#pragma unroll
+    for (int k = 7; k >= 0; --k) i5 = i5 * 5 + d[t + k];
+    sum += G[((long long)(4 * h + t) * kMer8 + i5) * 320 + co];
+  }
+  Q[e] = (float)sum;
+}
+
 // conv2 + bias + ReLU + maxpool4 of `rows` pooled rows per window from base codes (window w =
 // code row row0 + w, strand mode as beluga_conv1_h3, code 4 past len), gathered from the k-mer
 // table; output: the f16x3 planes of the pooled rows (scaled by osc = 2^sx[1], plain split, as
 // the MFMA conv2's epilogue stores them), row w * s_out + g.  640 threads = 8 pooled rows x 80
-// channel quads; a quad's 16 table reads are 16-B loads of one 1,280-B table row each.
+// channel quads; a conv2 row is Q_0 + Q_1 (2 16-B loads per quad, each from one 1,280-B table
+// row), a half whose 11-mer holds an N (T_0 + T_1) or (T_2 + T_3).
 constexpr int KP_ROWS = 8;
 __global__ __launch_bounds__(640) void conv2_kmer_pool(const uint8_t* __restrict__ codes, long long stride, int n_src,
                                                        int mode, long long row0, int len, int rows, int row_blocks,
                                                        int s_out, const float* __restrict__ T,
-                                                       const float* __restrict__ b2, float osc,
+                                                       const float* __restrict__ b2, float osc, int quad,
                                                        float* __restrict__ out, int* __restrict__ ovf) {
   __shared__ unsigned char cl[4 * KP_ROWS + 16];
-  __shared__ int ix[4 * KP_ROWS + 8];
+  __shared__ int ix[4 * KP_ROWS + 8];    // 9-mer (base 5) at offset o
+  __shared__ int iq[4 * KP_ROWS + 8];    // 11-mer (base 4) at offset o, -1 if it holds an N
   const long long win = blockIdx.x / row_blocks;
   const int g0 = (int)(blockIdx.x - win * row_blocks) * KP_ROWS;
   const int tid = threadIdx.x;
@@ -1041,21 +1069,38 @@ __global__ __launch_bounds__(640) void conv2_kmer_pool(const uint8_t* __restrict
 #pragma unroll
     for (int k = 8; k >= 0; --k) v = v * 5 + cl[tid + k];
     ix[tid] = v;
+  } else if (tid >= 64 && tid < 64 + 4 * KP_ROWS + 4) {
+    const int o = tid - 64;
+    int v = 0;
+    bool n = false;
+#pragma unroll
+    for (int k = 10; k >= 0; --k) {
+      n |= cl[o + k] > 3;
+      v = v * 4 + (cl[o + k] & 3);
+    }
+    iq[o] = n || !quad ? -1 : v;
   }
   __syncthreads();
   const int lr = tid / 80, q = tid - lr * 80, g = g0 + lr;
   if (g >= rows) return;
-  floatx4 t[4][4];
+  const float* Q = T + 4 * kMer9 * 320;
+  auto row = [&](const float* base, long long r) { return *reinterpret_cast<const floatx4*>(base + r * 320 + 4 * q); };
+  floatx4 hv2[4][2];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      t[r][i] = *reinterpret_cast<const floatx4*>(T + ((long long)i * kMer9 + ix[4 * lr + r + 2 * i]) * 320 + 4 * q);
+    for (int h = 0; h < 2; ++h) {
+      const int o = 4 * lr + r + 4 * h, k = iq[o];
+      if (k >= 0)
+        hv2[r][h] = row(Q + h * kMer11 * 320, k);
+      else
+        hv2[r][h] = row(T + 2 * h * kMer9 * 320, ix[o]) + row(T + (2 * h + 1) * kMer9 * 320, ix[o + 2]);
+    }
   const floatx4 bb = *reinterpret_cast<const floatx4*>(b2 + 4 * q);
   floatx4 m;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const floatx4 s = ((t[r][0] + t[r][1]) + t[r][2]) + t[r][3];
+    const floatx4 s = hv2[r][0] + hv2[r][1];
 #pragma unroll
     for (int c = 0; c < 4; ++c) m[c] = r == 0 ? s[c] : fmaxf(m[c], s[c]);
   }
@@ -1182,6 +1227,7 @@ struct expecto_beluga {
   bool kmer_on = true;                // f16x3 codes input: conv1 + conv2 + pool1 from the k-mer table (EXPECTO_CONV2_TABLE)
   float* kmer = nullptr;              //   the table (shared by handles with the same conv1 / conv2 weights)
   uint64_t kmer_key = 0;
+  bool kmer_quad = true;              //   conv2 rows from the quad tables (EXPECTO_KMER_QUAD=0: pair tables only)
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, int>> pending;  // (layer, event index of start)
@@ -1246,8 +1292,8 @@ int kmer_acquire(expecto_beluga* h, const float* const* params, hipStream_t st) 
       return EXPECTO_OK;
     }
   void *t = nullptr, *f = nullptr, *gg = nullptr;
-  const size_t tb = 4 * (size_t)kMer9 * 320 * sizeof(float), fb = (size_t)kMer8 * 320 * sizeof(double);
-  if (hipMalloc(&t, tb) != hipSuccess || hipMalloc(&f, fb) != hipSuccess || hipMalloc(&gg, 2 * fb) != hipSuccess) {
+  const size_t tb = kKmerFloats * sizeof(float), fb = (size_t)kMer8 * 320 * sizeof(double);
+  if (hipMalloc(&t, tb) != hipSuccess || hipMalloc(&f, fb) != hipSuccess || hipMalloc(&gg, 8 * fb) != hipSuccess) {
     (void)hipGetLastError();
     for (void* x : {t, f, gg})
       if (x) (void)hipFree(x);
@@ -1258,14 +1304,15 @@ int kmer_acquire(expecto_beluga* h, const float* const* params, hipStream_t st) 
   double* G = static_cast<double*>(gg);
   kmer_conv1<<<dim3(kMer8), dim3(320), 0, st>>>(h->w1, h->b1, F);
   int rc = check_launch("kmer_conv1");
-  for (int i = 0; i < 4 && !rc; ++i) {
-    const dim3 grid((kMer8 + 63) / 64, 5);
-    kmer_conv2<<<grid, dim3(256), 0, st>>>(F, h->wt[0], 2 * i, G);
-    kmer_conv2<<<grid, dim3(256), 0, st>>>(F, h->wt[0], 2 * i + 1, G + (size_t)kMer8 * 320);
-    kmer_pair<<<dim3((unsigned)((kMer9 * 320 + 255) / 256)), dim3(256), 0, st>>>(G, G + (size_t)kMer8 * 320,
-                                                                                T + (size_t)i * kMer9 * 320);
-    rc = check_launch("kmer table");
-  }
+  for (int j = 0; j < 8; ++j)   // G: the 8 taps' products, [tap][5^8][320] fp64
+    kmer_conv2<<<dim3((kMer8 + 63) / 64, 5), dim3(256), 0, st>>>(F, h->wt[0], j, G + (size_t)j * kMer8 * 320);
+  for (int i = 0; i < 4; ++i)
+    kmer_pair<<<dim3((unsigned)((kMer9 * 320 + 255) / 256)), dim3(256), 0, st>>>(
+        G + (size_t)(2 * i) * kMer8 * 320, G + (size_t)(2 * i + 1) * kMer8 * 320, T + (size_t)i * kMer9 * 320);
+  for (int hq = 0; hq < 2; ++hq)
+    kmer_quad<<<dim3((unsigned)((kMer11 * 320 + 255) / 256)), dim3(256), 0, st>>>(
+        G, hq, T + (4 * (size_t)kMer9 + hq * (size_t)kMer11) * 320);
+  rc = rc ? rc : check_launch("kmer table");
   if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = check_launch("kmer table sync");
   (void)hipFree(f);
   (void)hipFree(gg);
@@ -1527,8 +1574,8 @@ int run_conv2_kmer(expecto_beluga* h, const C1Src& f, long long n_win, int rows,
   const long long nblk = n_win * rb;
   EXPECTO_REQUIRE(nblk > 0 && nblk < (1LL << 31) && f.len >= 18, "conv2 k-mer grid / window length");
   conv2_kmer_pool<<<dim3((unsigned)nblk), dim3(640), 0, st>>>(f.codes, f.stride, f.n_src, f.mode, f.row0, f.len, rows,
-                                                              rb, s_out, h->kmer, h->bt[0], exp2i(h->sx[1]), dst,
-                                                              h->ovf);
+                                                              rb, s_out, h->kmer, h->bt[0], exp2i(h->sx[1]),
+                                                              h->kmer_quad ? 1 : 0, dst, h->ovf);
   return check_launch("conv2_kmer_pool");
 }
 
@@ -2487,6 +2534,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   if (const char* e = getenv("EXPECTO_POOL_ONE_PASS")) h->pool_one_pass = atoi(e) != 0;   // same bits either way
   if (const char* e = getenv("EXPECTO_FUSE_CONV1")) h->fuse_conv1 = atoi(e) != 0;         // same bits either way
   if (const char* e = getenv("EXPECTO_CONV2_TABLE")) h->kmer_on = atoi(e) != 0;   // conv2 on the MFMAs (parity, not bits)
+  if (const char* e = getenv("EXPECTO_KMER_QUAD")) h->kmer_quad = atoi(e) != 0;    // pair tables only (parity, not bits)
   if (const char* e = getenv("EXPECTO_SEG_CHUNK_WINDOWS")) h->seg_chunk_windows = atoi(e);   // same bits either way
   if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)
     const int v = atoi(e);

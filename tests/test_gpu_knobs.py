@@ -93,9 +93,10 @@ def test_conv2_table_paths_bitwise_and_parity(monkeypatch, use_segments, use_pai
 
 
 def test_conv2_table_accuracy_against_float64(monkeypatch):
-    """Against a float64 forward, the k-mer table's outputs are at least as accurate as conv2 on
-    the MFMAs (the table is built in fp64 and rounded once; the MFMA path multiplies 22-bit
-    operand splits), and inside the parity bound; N bases (code 4) included."""
+    """Against a float64 forward, the k-mer tables' outputs (quad tables with the pair-table N
+    fallback, and the pair tables alone) are at least as accurate as conv2 on the MFMAs (the
+    tables are built in fp64 and rounded once; the MFMA path multiplies 22-bit operand splits),
+    and inside the parity bound; N runs and scattered N bases (code 4) included."""
     import os
     from expecto_amd import beluga
     from expecto_amd.encode import codes_to_onehot
@@ -110,13 +111,16 @@ def test_conv2_table_accuracy_against_float64(monkeypatch):
     torch.set_num_threads(min(16, os.cpu_count() or 1))
     y64 = forward_torch_cpu(sd64, torch.from_numpy(codes_to_onehot(codes_np).astype(np.float64)).unsqueeze(2)).numpy()
     err = {}
-    for on in ("1", "0"):
-        monkeypatch.setenv("EXPECTO_CONV2_TABLE", on)
+    for name, env in (("quad", {}), ("pair", {"EXPECTO_KMER_QUAD": "0"}), ("mfma", {"EXPECTO_CONV2_TABLE": "0"})):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         mm = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=64).cuda()
+        for k in env:
+            monkeypatch.delenv(k)
         y = mm.forward_codes(codes, 2).cpu().numpy().astype(np.float64)
         assert mm.engine().f16_state()[0] == 0
-        err[on] = float((np.abs(y - y64) / (1e-4 * np.abs(y64) + 1e-5)).max())
+        err[name] = float((np.abs(y - y64) / (1e-4 * np.abs(y64) + 1e-5)).max())
         del mm
-    monkeypatch.delenv("EXPECTO_CONV2_TABLE")
-    assert err["1"] < 0.5, err
-    assert err["1"] <= 1.25 * err["0"], err
+    for name in ("quad", "pair"):   # quad tables, and the pair tables alone (the N fallback)
+        assert err[name] < 0.5, err
+        assert err[name] <= 1.25 * err["mfma"], err
