@@ -84,9 +84,10 @@ def conv2_table_on() -> bool:
 
 
 # 200-window segment (41,800 bp): pooled conv2 rows per segment, and the k-mer gather's algorithmic
-# bytes per pooled row (16 table rows of 320 fp32 read, 320 fp16 hi + lo planes written)
+# bytes per pooled row (4 conv2 rows x 2 quad-table rows of 320 fp32 read, 320 fp16 hi + lo planes
+# written; a conv2 half whose 11-mer holds an N reads 2 pair-table rows instead of 1)
 SEG200_POOL1_ROWS = ((2000 + 199 * 200 - 7) - 7) // 4
-KMER_BYTES_PER_POOLED_ROW = 16 * 320 * 4 + 320 * 4
+KMER_BYTES_PER_POOLED_ROW = 8 * 320 * 4 + 320 * 4
 
 
 def conv2_table_roofline(layers, n):
@@ -99,8 +100,8 @@ def conv2_table_roofline(layers, n):
     gbs = b / (ms / calls * 1e-3) / 1e9
     return {"bound": "hbm", "kernel": "conv2_kmer_pool", "achieved": gbs, "peak": 8000.0, "unit": "GB/s",
             "frac": gbs / 8000.0, "bytes_per_launch": b, "avg_launch_ms": ms / calls, "launches": calls,
-            "what": f"{n} segments x {SEG200_POOL1_ROWS} pooled rows x (16 table rows x 1,280 B read + 1,280 B "
-                    f"written); table hits in L2 / Infinity Cache (repeated 9-mers) count as HBM bytes here"}
+            "what": f"{n} segments x {SEG200_POOL1_ROWS} pooled rows x (8 quad-table rows x 1,280 B read + 1,280 B "
+                    f"written); table hits in L2 / Infinity Cache (repeated k-mers) count as HBM bytes here"}
 
 
 def kernel_name(layer: str, precision: str, segments: bool = True) -> str:
