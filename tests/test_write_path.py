@@ -10,10 +10,10 @@ import pytest
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
 
 
-@pytest.mark.parametrize("stagger", [False, True])
-def test_eight_writers_fill_the_files_exactly(tmp_path, stagger):
+@pytest.mark.parametrize("stagger,threads", [(False, 1), (True, 1), (True, 4)])
+def test_eight_writers_fill_the_files_exactly(tmp_path, stagger, threads):
     import write_probe
     shifts = [0, -200, -400, 200, 400]
-    r = write_probe.run(str(tmp_path), ranks=8, n=1001, shifts=shifts, batch=37, stagger=stagger)
+    r = write_probe.run(str(tmp_path), ranks=8, n=1001, shifts=shifts, batch=37, stagger=stagger, threads=threads)
     assert r["bytes"] == len(shifts) * 3 * 2 * 1001 * 2002 * 4
     write_probe.check(str(tmp_path), 1001, shifts)

@@ -46,7 +46,7 @@ def _files(d: str, shifts):
     return {s: os.path.join(d, f"snps.shift_{s}.diff.h5.part") for s in shifts}
 
 
-def _rank(rank, ranks, n, shifts, batch, d, stagger, barrier, q):
+def _rank(rank, ranks, n, shifts, batch, d, stagger, barrier, q, threads=1):
     specs = {k: ((2 * n, F), np.float32) for k in DATASETS}
     writers = {s: h5.RowWriter(p, specs, create=False) for s, p in _files(d, shifts).items()}
     lo, hi = shard_range(n, rank, ranks)
@@ -57,17 +57,31 @@ def _rank(rank, ranks, n, shifts, batch, d, stagger, barrier, q):
     t0 = time.perf_counter()
     nbytes = 0
     blk2 = np.empty_like(blk)
+    pool = None
+    if threads > 1:   # the CLI's --write-threads: one shift's 6 blocks written concurrently
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(max_workers=threads)
+        tagged = [np.empty_like(blk) for _ in range(2 * len(DATASETS))]
     for b0 in range(lo, hi, batch):
         b1 = min(hi, b0 + batch)
         xs = [row_block(np.arange(b0, b1) + strand * n, x[:b1 - b0]) for strand, x in ((0, blk), (1, blk2))]
         for j in order:
             w = writers[shifts[j]]
+            jobs = []
             for strand in (0, 1):
                 x = xs[strand]
                 for di, name in enumerate(DATASETS):
-                    x[:, 0] = j * 4 + di
-                    w.write_rows(name, b0 + strand * n, x)
+                    if pool is None:
+                        x[:, 0] = j * 4 + di
+                        w.write_rows(name, b0 + strand * n, x)
+                    else:
+                        t = tagged[strand * len(DATASETS) + di][:b1 - b0]
+                        t[:] = x
+                        t[:, 0] = j * 4 + di
+                        jobs.append(pool.submit(w.write_rows, name, b0 + strand * n, t))
                     nbytes += x.nbytes
+            for f in jobs:
+                f.result()
     el = time.perf_counter() - t0
     for w in writers.values():
         w.close()
@@ -75,7 +89,7 @@ def _rank(rank, ranks, n, shifts, batch, d, stagger, barrier, q):
 
 
 def run(d: str, ranks: int = 8, n: int = 100_000, shifts=(0, -200, -400, -600, -800, 200, 400, 600, 800),
-        batch: int = 4096, stagger: bool = False) -> dict:
+        batch: int = 4096, stagger: bool = False, threads: int = 1) -> dict:
     os.makedirs(d, exist_ok=True)
     shifts = list(shifts)
     specs = {k: ((2 * n, F), np.float32) for k in DATASETS}
@@ -85,7 +99,8 @@ def run(d: str, ranks: int = 8, n: int = 100_000, shifts=(0, -200, -400, -600, -
         w.close()
     ctx = mp.get_context("spawn")
     barrier, q = ctx.Barrier(ranks), ctx.Queue()
-    procs = [ctx.Process(target=_rank, args=(r, ranks, n, shifts, batch, d, stagger, barrier, q)) for r in range(ranks)]
+    procs = [ctx.Process(target=_rank, args=(r, ranks, n, shifts, batch, d, stagger, barrier, q, threads))
+             for r in range(ranks)]
     for p in procs:
         p.start()
     res = [q.get(timeout=3600) for _ in procs]
@@ -95,7 +110,7 @@ def run(d: str, ranks: int = 8, n: int = 100_000, shifts=(0, -200, -400, -600, -
             raise RuntimeError(f"a writer rank failed (exit {p.exitcode})")
     el = max(r[1] for r in res)
     total = sum(r[2] for r in res)
-    return {"ranks": ranks, "variants": n, "shifts": len(shifts), "batch": batch, "stagger": stagger,
+    return {"ranks": ranks, "variants": n, "shifts": len(shifts), "batch": batch, "stagger": stagger, "threads": threads,
             "bytes": total, "slowest_rank_s": el, "fastest_rank_s": min(r[1] for r in res),
             "aggregate_GB_per_s": total / el / 1e9}
 
@@ -120,12 +135,13 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--dir", required=True)
     ap.add_argument("--stagger", action="store_true")
+    ap.add_argument("--threads", type=int, default=1, help="write threads per rank (the CLI's --write-threads)")
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--keep", action="store_true")
     a = ap.parse_args()
     shifts = [0, -200, -400, -600, -800, 200, 400, 600, 800]
     try:
-        r = run(a.dir, a.ranks, a.variants, shifts, a.batch, a.stagger)
+        r = run(a.dir, a.ranks, a.variants, shifts, a.batch, a.stagger, a.threads)
         if a.check:
             check(a.dir, a.variants, shifts)
             r["checked"] = True
