@@ -921,7 +921,7 @@ __global__ void calib_codes(uint8_t* __restrict__ codes, long long n, unsigned s
 using namespace expecto;
 
 
-// ---- conv1 + ReLU + conv2 as a k-mer table (f16x3 path, base-code inputs) ----------------
+// ---- conv1 + ReLU + conv2 as a k-mer table (f16x3 and bf16x6, base-code inputs) ----------
 // Conv1 (k = 8) sees 8 bases, so relu(conv1) at position p is a function of the 8-mer at p, and
 // conv2 (k = 8) at p is  sum_{j<8} W2_j relu(conv1(p + j)) = sum_{i<4} T_i(9-mer at p + 2i)  with
 //   T_i(x_0..x_8) = W2_{2i} relu(conv1(x_0..x_7)) + W2_{2i+1} relu(conv1(x_1..x_8))
@@ -1032,14 +1032,14 @@ __global__ void kmer_quad(const double* __restrict__ G, int h, float* __restrict
 // conv2 + bias + ReLU + maxpool4 of `rows` pooled rows per window from base codes (window w =
 // code row row0 + w, strand mode as beluga_conv1_h3, code 4 past len), gathered from the k-mer
 // table; output: the f16x3 planes of the pooled rows (scaled by osc = 2^sx[1], plain split, as
-// the MFMA conv2's epilogue stores them), row w * s_out + g.  640 threads = 8 pooled rows x 80
+// the MFMA conv2's epilogue stores them; bf16x6: the exact 3-way bf16 split), row w * s_out + g.  640 threads = 8 pooled rows x 80
 // channel quads; a conv2 row is Q_0 + Q_1 (2 16-B loads per quad, each from one 1,280-B table
 // row), a half whose 11-mer holds an N (T_0 + T_1) or (T_2 + T_3).
 constexpr int KP_ROWS = 8;
 __global__ __launch_bounds__(640) void conv2_kmer_pool(const uint8_t* __restrict__ codes, long long stride, int n_src,
                                                        int mode, long long row0, int len, int rows, int row_blocks,
                                                        int s_out, const float* __restrict__ T,
-                                                       const float* __restrict__ b2, float osc, int quad,
+                                                       const float* __restrict__ b2, float osc, int quad, int fmt,
                                                        float* __restrict__ out, int* __restrict__ ovf) {
   __shared__ unsigned char cl[4 * KP_ROWS + 16];
   __shared__ int ix[4 * KP_ROWS + 8];    // 9-mer (base 5) at offset o
@@ -1110,6 +1110,15 @@ __global__ __launch_bounds__(640) void conv2_kmer_pool(const uint8_t* __restrict
   for (int c = 0; c < 4; ++c) {
     v[c] = fmaxf(fmaf(m[c], osc, bb[c] * osc), 0.f);   // maxpool(relu(x + b)) = relu(max(x) + b), scaled
     vmax = fmaxf(vmax, v[c]);
+  }
+  if (fmt == 1) {   // bf16x6 planes [row][C/32][3][32] (osc = 1): the exact 3-way split, as store_act<1>
+    bf16x4 x0, x1, x2;
+    split3(v, x0, x1, x2);
+    char* d = reinterpret_cast<char*>(out) + ((win * s_out + g) * 10 + (q >> 3)) * 192 + (q & 7) * 8;
+    *reinterpret_cast<bf16x4*>(d) = x0;
+    *reinterpret_cast<bf16x4*>(d + 64) = x1;
+    *reinterpret_cast<bf16x4*>(d + 128) = x2;
+    return;
   }
   const halfx4 hv = __builtin_convertvector(v, halfx4);
   const halfx4 lv = __builtin_convertvector(v - __builtin_convertvector(hv, floatx4), halfx4);
@@ -1562,10 +1571,10 @@ bool fuse_conv1(const expecto_beluga* h, const float* x) {
   return h->fuse_conv1 && !x && g_precision == EXPECTO_PRECISION_F16X3 && h->w1h;
 }
 
-// conv1 + conv2 + pool1 from the k-mer table (f16x3, codes input; EXPECTO_CONV2_TABLE=0 runs them
+// conv1 + conv2 + pool1 from the k-mer table (f16x3 and bf16x6, codes input; EXPECTO_CONV2_TABLE=0 runs them
 // on the MFMAs): `rows` pooled rows per window into dst rows w * s_out + g
 bool use_kmer(const expecto_beluga* h, const float* x) {
-  return h->kmer && !x && g_precision == EXPECTO_PRECISION_F16X3;
+  return h->kmer && !x && (g_precision == EXPECTO_PRECISION_F16X3 || g_precision == EXPECTO_PRECISION_BF16X6);
 }
 
 int run_conv2_kmer(expecto_beluga* h, const C1Src& f, long long n_win, int rows, int s_out, float* dst, hipStream_t st) {
@@ -1574,8 +1583,9 @@ int run_conv2_kmer(expecto_beluga* h, const C1Src& f, long long n_win, int rows,
   const long long nblk = n_win * rb;
   EXPECTO_REQUIRE(nblk > 0 && nblk < (1LL << 31) && f.len >= 18, "conv2 k-mer grid / window length");
   conv2_kmer_pool<<<dim3((unsigned)nblk), dim3(640), 0, st>>>(f.codes, f.stride, f.n_src, f.mode, f.row0, f.len, rows,
-                                                              rb, s_out, h->kmer, h->bt[0], exp2i(h->sx[1]),
-                                                              h->kmer_quad ? 1 : 0, dst, h->ovf);
+                                                              rb, s_out, h->kmer, h->bt[0],
+                                                              act_fmt() == 2 ? exp2i(h->sx[1]) : 1.f,
+                                                              h->kmer_quad ? 1 : 0, act_fmt(), dst, h->ovf);
   return check_launch("conv2_kmer_pool");
 }
 
