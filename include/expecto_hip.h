@@ -86,7 +86,11 @@ enum {
 /* Build a model handle on `device`.  `params` are 16 DEVICE pointers to fp32 tensors in
  * the reference layouts (conv weight [Cout,Cin,1,8], fc weight [out,in]); they are
  * repacked into the kernels' layouts, so the caller may free them afterwards.
- * `max_batch` bounds the windows processed per internal chunk (workspace size). */
+ * `max_batch` bounds the windows processed per internal chunk (workspace size).
+ * The handle also builds (or shares, with other handles of this device holding the same
+ * conv1 / conv2 weights) the k-mer tables its forwards from base codes gather conv1 + conv2
+ * + pool1 from: 20.7 GB, ~40 ms, freed with the last handle using them; if they do not fit,
+ * conv2 runs on the MFMAs.  EXPECTO_CONV2_TABLE=0 skips them. */
 int expecto_beluga_create(int device, const float* const* params, int max_batch, void* stream,
                           expecto_beluga_t* out);
 void expecto_beluga_destroy(expecto_beluga_t h);
