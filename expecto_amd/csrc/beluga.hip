@@ -1270,6 +1270,7 @@ int npad_of(int n) { return (n + GBN - 1) / GBN * GBN; }
 struct KmerEntry {
   int device;
   uint64_t key;
+  std::vector<float> w;   // the conv1 / conv2 weights the tables were built from (exact match, not just the hash)
   float* T;
   int refs;
 };
@@ -1294,7 +1295,7 @@ int kmer_acquire(expecto_beluga* h, const float* const* params, hipStream_t st) 
   const uint64_t key = fnv1a(hw.data(), hw.size() * sizeof(float));
   std::lock_guard<std::mutex> lock(g_kmer_mu);
   for (KmerEntry& e : g_kmer)
-    if (e.device == h->device && e.key == key) {
+    if (e.device == h->device && e.key == key && e.w == hw) {
       ++e.refs;
       h->kmer = e.T;
       h->kmer_key = key;
@@ -1329,7 +1330,7 @@ int kmer_acquire(expecto_beluga* h, const float* const* params, hipStream_t st) 
     (void)hipFree(t);
     return rc;
   }
-  g_kmer.push_back({h->device, key, T, 1});
+  g_kmer.push_back({h->device, key, std::move(hw), T, 1});
   h->kmer = T;
   h->kmer_key = key;
   return EXPECTO_OK;
