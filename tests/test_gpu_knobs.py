@@ -124,3 +124,29 @@ def test_conv2_table_accuracy_against_float64(monkeypatch):
     for name in ("quad", "pair"):   # quad tables, and the pair tables alone (the N fallback)
         assert err[name] < 0.5, err
         assert err[name] <= 1.25 * err["mfma"], err
+
+
+def test_kmer_tables_are_shared_and_freed():
+    """Handles with the same conv1 / conv2 weights share one set of k-mer tables (20.7 GB); the
+    last handle to go frees them, so creating and dropping engines does not leak device memory."""
+    import gc
+    from expecto_amd import beluga
+    table = (4 * 5 ** 9 + 2 * 4 ** 11) * 320 * 4
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free0 = torch.cuda.mem_get_info()[0]
+    a = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=64).cuda()
+    ea = a.engine()
+    free1 = torch.cuda.mem_get_info()[0]
+    assert free0 - free1 >= table, (free0 - free1) / 1e9
+    b = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=64).cuda()
+    eb = b.engine()
+    free2 = torch.cuda.mem_get_info()[0]
+    assert free1 - free2 < table / 2, (free1 - free2) / 1e9          # b shares a's tables
+    del ea, eb, a, b
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free3 = torch.cuda.mem_get_info()[0]
+    assert free0 - free3 < 1 << 30, (free0 - free3) / 1e9            # all of it back
