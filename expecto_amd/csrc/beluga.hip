@@ -926,13 +926,15 @@ using namespace expecto;
 // conv2 (k = 8) at p is  sum_{j<8} W2_j relu(conv1(p + j)) = sum_{i<4} T_i(9-mer at p + 2i)  with
 //   T_i(x_0..x_8) = W2_{2i} relu(conv1(x_0..x_7)) + W2_{2i+1} relu(conv1(x_1..x_8))
 // (Beluga.py:23-26 regrouped: a tap pair shares 9 bases).  Over the code alphabet A,G,C,T,N (N =
-// the zero one-hot column, chromatin.py:155-160) T has 4 x 5^9 rows of 320 values (10 GB fp32),
-// built once per weight set in fp64 -- the conv1 sums, the 320-deep conv2 products and the pair
-// sum -- and rounded to fp32 once.  The conv2 + pool1 layer of every f16x3 forward from codes then
-// is a gather (conv2_kmer_pool): a pooled row reads 16 table rows (4 conv2 rows x 4 tap pairs,
-// 20 KB) and adds them, in place of 4 x 819,200 multiply-adds x 3 f16x3 products on the MFMAs.
-// The table is MORE accurate than the MFMA path (one fp32 rounding per entry and three fp32 adds
-// per conv2 value, against 22-bit operands and a 2,560-long fp32 accumulation); every path (per
+// the zero one-hot column, chromatin.py:155-160) T has 4 x 5^9 rows of 320 values (10 GB fp32);
+// the quad tables Q_h (kmer_quad: taps 4h..4h+3 over 11-mers of A,G,C,T, 10.7 GB) halve the
+// gathers again.  Built once per weight set in fp64 -- the conv1 sums, the 320-deep conv2
+// products and the pair / quad sums -- and rounded to fp32 once.  The conv2 + pool1 layer of every
+// f16x3 / bf16x6 forward from codes then is a gather (conv2_kmer_pool): a pooled row reads 8 table
+// rows (4 conv2 rows x 2 tap quads, 10 KB) and adds them, in place of 4 x 819,200 multiply-adds x
+// 3 f16x3 products on the MFMAs.  The tables are MORE accurate than the MFMA path (one fp32
+// rounding per entry and one to three fp32 adds per conv2 value, against 22-bit operands and a
+// 2,560-long fp32 accumulation); every path (per
 // window, segments, pairs, the alt-delta patches) computes a conv2 row by this one formula from
 // its codes, so the paths stay bitwise equal to each other.
 constexpr int kMer8 = 390625;           // 5^8
