@@ -2606,7 +2606,9 @@ void expecto_beluga_destroy(expecto_beluga_t h) {
   delete h;
 }
 
-size_t expecto_beluga_device_bytes(expecto_beluga_t h) { return h ? h->bytes : 0; }
+size_t expecto_beluga_device_bytes(expecto_beluga_t h) {
+  return h ? h->bytes + (h->kmer ? kKmerFloats * sizeof(float) : 0) : 0;
+}
 
 int expecto_beluga_forward_onehot(expecto_beluga_t h, const float* x, int n, float* y, void* stream) {
   EXPECTO_REQUIRE(h != nullptr, "null handle");

@@ -15,7 +15,8 @@
  *                                   compute_expecto_features.py:121-122)
  *   expecto_beluga_forward_codes   encodeSeqs(...) one-hot + Beluga.forward, fused: the
  *                                  one-hot / reverse-complement of chromatin.py:153-171
- *                                  is generated inside the conv1 kernel from base codes
+ *                                  is generated from base codes inside the conv1 + conv2
+ *                                  k-mer gather (or the conv1 kernel)
  *   expecto_variant_windows        fetchSeqs window splice for SNVs (chromatin.py:175-209)
  *                                  from a device-resident genome
  *   expecto_indel_windows          fetchSeqs splice + centre crop for indels / MNPs
@@ -95,7 +96,8 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
                           expecto_beluga_t* out);
 void expecto_beluga_destroy(expecto_beluga_t h);
 
-/* Bytes of device memory the handle owns (weights + workspace). */
+/* Bytes of device memory the handle owns (weights + workspace) plus the k-mer tables it
+ * holds (20.7 GB, shared with other handles of the same conv1 / conv2 weights). */
 size_t expecto_beluga_device_bytes(expecto_beluga_t h);
 
 /* y[n,2002] = Beluga.forward(x[n,4,1,2000]) (x contiguous fp32, any values). */
