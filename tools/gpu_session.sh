@@ -9,7 +9,7 @@
 #   power    rocm-smi power / clock samples during 200 headline steps       -> gpurun_out/power.log
 #   gb       tools/gemm_bench $GB_ARGS (e.g. "8192 5 fc1 8")                -> gpurun_out/gb.log
 #   gbpmc    SQ stall counter sets of gemm_bench $GB_ARGS, VARIANT=$V
-#   writes   tools/write_probe.py, 8 writers at configs[3]'s full size, plain and staggered
+#   writes   tools/write_probe.py, 8 writers at configs[3]'s full size: plain, staggered, staggered with 4 threads
 #
 #   STEPS=tests,bench TAG=r04 /usr/local/graft/bin/gpurun -- bash tools/gpu_session.sh
 #
@@ -69,5 +69,6 @@ fi
 if has writes; then
   run writes_plain 600 python -u tools/write_probe.py --ranks 8 --variants 100000 --dir /tmp/wp
   run writes_stagger 600 python -u tools/write_probe.py --ranks 8 --variants 100000 --dir /tmp/wp --stagger
+  run writes_stagger_t4 600 python -u tools/write_probe.py --ranks 8 --variants 100000 --dir /tmp/wp --stagger --threads 4
 fi
 echo "=== done" >> $OUT/steps.log
