@@ -77,10 +77,10 @@ DTYPES = {
 }
 
 
-def conv2_table_on() -> bool:
-    """f16x3 conv1 + conv2 + pool1 from the k-mer table (the library default; EXPECTO_CONV2_TABLE=0
-    runs them on the MFMAs)."""
-    return os.environ.get("EXPECTO_CONV2_TABLE", "1") != "0"
+def conv2_table_on(precision: str = "f16x3") -> bool:
+    """conv1 + conv2 + pool1 from the k-mer table (the library default for f16x3 and bf16x6 forwards
+    from codes; EXPECTO_CONV2_TABLE=0 runs them on the MFMAs)."""
+    return precision in ("f16x3", "bf16x6") and os.environ.get("EXPECTO_CONV2_TABLE", "1") != "0"
 
 
 # 200-window segment (41,800 bp): pooled conv2 rows per segment, and the k-mer gather's algorithmic
@@ -112,13 +112,13 @@ def kernel_name(layer: str, precision: str, segments: bool = True) -> str:
     l, e = GEMM_LAYER_EPI[layer]
     if segments and layer == "conv4":
         e = 0
+    if layer == "conv2" and conv2_table_on(precision):
+        return "conv2_kmer_pool"                           # conv1 + conv2 + pool1 gathered from the k-mer table
     if precision == "bf16x6":
         return f"beluga_gemm_x6q<{l}, {e}, 0>"
     if precision == "f16x3":
         if l in (7, 8):   # split-K FC GEMMs on 336-column tiles (beluga_fc_h3w)
             return f"beluga_fc_h3w<{l}, {e}, 0>"
-        if layer == "conv2" and conv2_table_on():
-            return "conv2_kmer_pool"                       # conv1 + conv2 + pool1 gathered from the k-mer table
         if layer == "conv2" and os.environ.get("EXPECTO_FUSE_CONV1", "1") != "0":
             return f"beluga_conv_h3p<{l}, {e}, 16640, 4>"   # conv1 fused into the producers (256 | 16384)
         return f"beluga_conv_h3p<{l}, {e}, 256, 4>"   # producer / consumer 256-row tiles (every conv layer)
@@ -388,7 +388,7 @@ def products_and_peak(precision):
 def roofline(layers, precision, segments=True):
     """MFMA roofline of the dominant GEMM kernel from executed work per launch (library counts)
     and its average launch duration (HIP events on the launch stream)."""
-    gemm = [k for k in GEMM_LAYER_EPI if not (k == "conv2" and precision == "f16x3" and conv2_table_on())]
+    gemm = [k for k in GEMM_LAYER_EPI if not (k == "conv2" and conv2_table_on(precision))]
     dom = max(gemm, key=lambda k: layers[k][0])   # (the f16x3 conv2 is a gather: conv2_table_roofline)
     ms, calls, macs = layers[dom]
     fp32_flops_launch = 2.0 * macs / calls
@@ -775,7 +775,7 @@ def main():
         "step_mfma_frac": mult * 2.0 * m["exec_macs_step"] / step_s / 1e12 / peak,
         "roofline": roof,
         "conv2_table_gather": (conv2_table_roofline(m["layers"], n)
-                               if eng.precision == "f16x3" and conv2_table_on() else None),
+                               if conv2_table_on(eng.precision) else None),
         "layer_ms_per_step": ms_l,
         "layer_tflops": tf_l,
         "layer_timing": f"separate profiled pass of {m['prof_steps']} steps (HIP events per launch); the "
