@@ -136,11 +136,12 @@ def test_kmer_tables_are_shared_and_freed():
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     free0 = torch.cuda.mem_get_info()[0]
-    a = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=64).cuda()
+    # a seed no other test uses, so no live handle elsewhere already holds these weights' tables
+    a = beluga.seeded(4242, gain=math.sqrt(6.0), max_batch=64).cuda()
     ea = a.engine()
     free1 = torch.cuda.mem_get_info()[0]
     assert free0 - free1 >= table, (free0 - free1) / 1e9
-    b = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=64).cuda()
+    b = beluga.seeded(4242, gain=math.sqrt(6.0), max_batch=64).cuda()
     eb = b.engine()
     free2 = torch.cuda.mem_get_info()[0]
     assert free1 - free2 < table / 2, (free1 - free2) / 1e9          # b shares a's tables
