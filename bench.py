@@ -673,6 +673,72 @@ def cli_e2e(n=CFG3_PER_RANK, tmp_root=None):
         shutil.rmtree(d, ignore_errors=True)
 
 
+def operator_api(model, genome, dev, seconds=2.0):
+    """The reference's own call of the operator: `input =
+    torch.from_numpy(encoded[i*B:(i+1)*B]).unsqueeze(2).cuda(); model.forward(input).cpu().numpy()`
+    (chromatin.py:266-279, batch 32 = chromatin.py:37-38; compute_expecto_features.py:115-122,
+    batch 200; scripts/sed_immune_atlas, batch 512) on host one-hot float32 windows (pageable, as
+    the reference's numpy arrays), H2D and D2H included.  `device_only`: the same forward on an
+    input already resident in HBM.  `mfma_conv2`: a handle with EXPECTO_ONEHOT_CODES=0 (one-hot
+    floats through conv1 / conv2 on the MFMAs, round 4's path) for comparison; same weights."""
+    from expecto_amd.encode import encodeSeqs
+    rng = np.random.default_rng(9)
+    names = sorted(genome)
+    seqs = []
+    for _ in range(512):
+        c = names[int(rng.integers(0, len(names)))]
+        p = int(rng.integers(30000, len(genome[c]) - 30000))
+        seqs.append(genome[c][p - 1000:p + 1000].decode())
+    enc = encodeSeqs(seqs).astype(np.float32)[:512]           # [512, 4, 2000] fwd windows
+    os.environ["EXPECTO_ONEHOT_CODES"] = "0"
+    try:
+        alt_model = beluga.Beluga(max_batch=MAX_BATCH)
+        alt_model.load_state_dict(model.state_dict())
+        alt_model = alt_model.cuda()
+        alt_model.engine()
+    finally:
+        del os.environ["EXPECTO_ONEHOT_CODES"]
+
+    def rate(fn, batch):
+        fn()
+        torch.cuda.synchronize()
+        done, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            done += batch
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        return done / el
+
+    eng = model.engine()
+    eng.set_overflow_check(deferred=False)       # the drop-in's default: outputs final when forward returns
+    out = {"table_active": eng.conv2_table_active}
+    for batch in (32, 200, 512):
+        host = enc[:batch]
+        xd = torch.from_numpy(host).unsqueeze(2).to(dev)
+        rec = {}
+        for name, m in (("k_mer", model), ("mfma_conv2", alt_model)):
+            def api(m=m):
+                inp = torch.from_numpy(host).unsqueeze(2).cuda(dev)
+                return m.forward(inp).cpu().detach().numpy()
+
+            def device_only(m=m):
+                return m.forward(xd)
+            rec[name] = {"windows_per_s": rate(api, batch), "device_only_windows_per_s": rate(device_only, batch)}
+        rec["speedup_k_mer_vs_mfma"] = rec["k_mer"]["windows_per_s"] / rec["mfma_conv2"]["windows_per_s"]
+        out[f"batch_{batch}"] = rec
+    del alt_model
+    torch.cuda.empty_cache()
+    eng.set_overflow_check(deferred=True)
+    out["what"] = ("Beluga.forward drop-in (expecto_beluga_forward_onehot) on host one-hot float32 batches: H2D + "
+                   "forward + D2H per batch, windows/s; k_mer = exact one-hot converted to codes on the device and "
+                   "gathered from the k-mer tables (default), mfma_conv2 = the MFMA conv1 / conv2 path")
+    return out
+
+
 def cfg3_rank_shard(pipe, eng, genome, rank, world, dev):
     """configs[3] per rank (100k SNVs over 8 GPUs = 12.5k SNVs x 9 shifts, +-800), computed once
     (timed, max over ranks), then its y + diff gathered to rank 0 one shift at a time (RCCL gather
@@ -717,6 +783,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the extra workloads")
     ap.add_argument("--no-e2e", action="store_true", help="skip the hg19-sized CLI end-to-end extra")
+    ap.add_argument("--extras", default="all", help="comma-separated extra workloads to run (default all): "
+                    "headline_other,cfg1,cfg2,cfg4,operator_api,cli_streamed,replicate_rank,cli_e2e,hbm")
     ap.add_argument("--precision", default=None, help="GEMM arithmetic (default: the engine default)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for the scaling runs; gloo to "
                     "rehearse several ranks on one GPU")
@@ -781,6 +849,7 @@ def main():
         "layer_timing": f"separate profiled pass of {m['prof_steps']} steps (HIP events per launch); the "
                         f"*_delta slots run on the second stream beside the ref launches (upper bounds)",
         "f16_fallback_steps": m["fallbacks"],
+        "conv2_table": dict(zip(("active", "state"), eng.conv2_table_state())),
         "profile_key": key,
         "reuse": "segments (conv trunk shared by the 200 shifts) + alt-cone (the alt allele recomputes only the "
                  "rows its SNV changes; windows without it copy the ref row); bit-identical to per-window forwards",
@@ -790,27 +859,35 @@ def main():
         rec["f16x3"] = {"fallback_calls": fb, "activation_scale_exp": sx}
     if world == 1 and not args.no_extras:
         extras = {}
-        # the same headline workload in the fp32-faithful bf16x6 split
-        other = "bf16x6" if eng.precision != "bf16x6" else "f16x3"
-        with eng.precision_override(other):
-            mo = measure(head, eng, n, 3, 1, 1, dev)
-        extras[f"headline_{other}"] = extra_record(mo, "variants_per_s", n, WIN_PER_VARIANT_200, other)
-        # configs[1]: 1k SNVs, shift 0 (per-window pair path)
-        c1 = ShiftSweep(pipe, genome, 1000, 1, shift_order(0), dev)
-        extras["cfg1_1k_snv_shift0"] = extra_record(measure(c1, eng, 1000, 10, 3, 1, dev, segments=False), "variants_per_s",
-                                                    1000, 4, eng.precision)
-        del c1
-        # configs[2]: +-800 sweep (9 shifts, segment path)
-        c2 = ShiftSweep(pipe, genome, 400, 101, shift_order(800), dev)
-        extras["cfg2_shift_sweep_800"] = extra_record(measure(c2, eng, 400, 2, 1, 1, dev), "variants_per_s",
-                                                      400, 36, eng.precision)
-        del c2
-        extras["cfg4_tss_features"] = tss_workload(eng, genome, pipe.dg, dev)
-        extras["cli_streamed"] = cli_streamed(genome)
-        extras["replicate_rank"] = replicate_rank(genome)
-        if not args.no_e2e:
+        want = set(args.extras.split(",")) if args.extras != "all" else None
+        run = lambda name: want is None or name in want   # noqa: E731
+        if run("headline_other"):   # the same headline workload in the fp32-faithful bf16x6 split
+            other = "bf16x6" if eng.precision != "bf16x6" else "f16x3"
+            with eng.precision_override(other):
+                mo = measure(head, eng, n, 3, 1, 1, dev)
+            extras[f"headline_{other}"] = extra_record(mo, "variants_per_s", n, WIN_PER_VARIANT_200, other)
+        if run("cfg1"):   # configs[1]: 1k SNVs, shift 0 (per-window pair path)
+            c1 = ShiftSweep(pipe, genome, 1000, 1, shift_order(0), dev)
+            extras["cfg1_1k_snv_shift0"] = extra_record(measure(c1, eng, 1000, 10, 3, 1, dev, segments=False),
+                                                        "variants_per_s", 1000, 4, eng.precision)
+            del c1
+        if run("cfg2"):   # configs[2]: +-800 sweep (9 shifts, segment path)
+            c2 = ShiftSweep(pipe, genome, 400, 101, shift_order(800), dev)
+            extras["cfg2_shift_sweep_800"] = extra_record(measure(c2, eng, 400, 2, 1, 1, dev), "variants_per_s",
+                                                          400, 36, eng.precision)
+            del c2
+        if run("cfg4"):
+            extras["cfg4_tss_features"] = tss_workload(eng, genome, pipe.dg, dev)
+        if run("operator_api"):
+            extras["operator_api"] = operator_api(model, genome, dev)
+        if run("cli_streamed"):
+            extras["cli_streamed"] = cli_streamed(genome)
+        if run("replicate_rank"):
+            extras["replicate_rank"] = replicate_rank(genome)
+        if run("cli_e2e") and not args.no_e2e:
             extras["cli_e2e"] = cli_e2e()
-        extras["hbm_reductions"] = hbm_reductions(dev)
+        if run("hbm"):
+            extras["hbm_reductions"] = hbm_reductions(dev)
         rec["extra_workloads"] = extras
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from expecto_amd.encode import seqs_to_codes

@@ -9,7 +9,9 @@ reproduces the reference's default initialisation bit for bit under the same see
 
 ``forward(x)`` takes ``x`` = ``[B,4,1,2000]`` (or ``[B,4,2000]``) fp32 on the GPU and
 returns ``[B,2002]`` sigmoid outputs, computed by ``libexpecto_hip.so``.  There is no
-CPU path: a CPU tensor, or a missing library, raises ``RuntimeError``.
+CPU path: a CPU tensor, or a missing library, raises ``RuntimeError``.  One-hot input as
+``encodeSeqs`` writes it (``chromatin.py:138-172``) runs through the k-mer gather, the same
+bits as ``forward_codes``; any other fp32 input keeps conv1 / conv2 on the MFMAs.
 """
 from __future__ import annotations
 
@@ -266,7 +268,23 @@ class BelugaEngine:
         return {_lib.LAYER_NAMES[i]: (ms[i], calls[i], macs[i]) for i in range(_lib.N_LAYERS)}
 
     def device_bytes(self) -> int:
+        """Device bytes of the handle; shared k-mer tables count only for their first holder."""
         return int(self.lib.expecto_beluga_device_bytes(self.handle))
+
+    CONV2_TABLE_REASONS = {0: "held", 1: "off (EXPECTO_CONV2_TABLE=0)", 2: "no room"}
+
+    def conv2_table_state(self):
+        """(active, reason): whether forwards from codes / exact one-hot floats gather conv1 + conv2
+        + pool1 from the k-mer tables, and why not (include/expecto_hip.h)."""
+        why = ctypes.c_int(0)
+        r = self.lib.expecto_beluga_conv2_table_active(self.handle, ctypes.byref(why))
+        if r < 0:
+            _lib.check(int(r), "conv2_table_active")
+        return bool(r), self.CONV2_TABLE_REASONS.get(why.value, str(why.value))
+
+    @property
+    def conv2_table_active(self) -> bool:
+        return self.conv2_table_state()[0]
 
 
 class Beluga(nn.Module):

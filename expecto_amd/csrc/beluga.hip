@@ -926,9 +926,9 @@ using namespace expecto;
 // conv2 (k = 8) at p is  sum_{j<8} W2_j relu(conv1(p + j)) = sum_{i<4} T_i(9-mer at p + 2i)  with
 //   T_i(x_0..x_8) = W2_{2i} relu(conv1(x_0..x_7)) + W2_{2i+1} relu(conv1(x_1..x_8))
 // (Beluga.py:23-26 regrouped: a tap pair shares 9 bases).  Over the code alphabet A,G,C,T,N (N =
-// the zero one-hot column, chromatin.py:155-160) T has 4 x 5^9 rows of 320 values (10 GB fp32);
-// the quad tables Q_h (kmer_quad: taps 4h..4h+3 over 11-mers of A,G,C,T, 10.7 GB) halve the
-// gathers again.  Built once per weight set in fp64 -- the conv1 sums, the 320-deep conv2
+// the zero one-hot column, chromatin.py:155-160) the 4 pair tables T_i have 5^9 rows of 320 values
+// each (10.0 GB fp32); the 2 quad tables Q_h (kmer_quad: taps 4h..4h+3 over 11-mers of A,G,C,T,
+// 10.7 GB) halve the gathers again: 20.7 GB in all (kKmerFloats).  Built once per weight set in fp64 -- the conv1 sums, the 320-deep conv2
 // products and the pair / quad sums -- and rounded to fp32 once.  The conv2 + pool1 layer of every
 // f16x3 / bf16x6 forward from codes then is a gather (conv2_kmer_pool): a pooled row reads 8 table
 // rows (4 conv2 rows x 2 tap quads, 10 KB) and adds them, in place of 4 x 819,200 multiply-adds x
@@ -1061,7 +1061,7 @@ __global__ __launch_bounds__(640) void conv2_kmer_pool(const uint8_t* __restrict
     unsigned c = 4;
     if (pos < len) {
       c = codes[src * stride + (rc ? len - 1 - pos : pos)];
-      if (rc && c < 4) c = 3 - c;
+      c = c < 4 ? (rc ? 3 - c : c) : 4;   // any code >= 4 is the zero column (as conv1 reads it): rows stay in the table
     }
     cl[tid] = (unsigned char)c;
   }
@@ -1128,6 +1128,48 @@ __global__ __launch_bounds__(640) void conv2_kmer_pool(const uint8_t* __restrict
   *reinterpret_cast<halfx4*>(d) = hv;
   *reinterpret_cast<halfx4*>(d + 64) = lv;
   if (!(vmax < 65504.f)) *ovf = 1;   // out of fp16 range: the call is recomputed (bf16x6)
+}
+
+// Beluga.forward's input (x[n][4][len] fp32, Beluga.py:50-51) as base codes: a column holding
+// exactly one 1.0f and three +0.0f is that channel's code (A, G, C, T = channels 0..3 as encodeSeqs
+// writes them, chromatin.py:155-160), an all-zero column is code 4 (N).  Any other column (another
+// value, -0.0f, NaN, two ones) sets *bad: the call then keeps conv1 / conv2 on the MFMAs.  codes
+// may be null (check only).  4 positions per thread, a 16-B load per channel (x 16-B aligned and
+// len % 4 == 0, checked by the caller); HBM-bound, 32 KB read per window.
+__global__ __launch_bounds__(256) void onehot_codes(const float* __restrict__ x, long long n, int len,
+                                                    uint8_t* __restrict__ codes, int* __restrict__ bad) {
+  const int len4 = len >> 2;
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n * len4) return;
+  const long long w = q / len4;
+  const int p = (int)(q - w * len4) * 4;
+  const float* xr = x + w * 4LL * len + p;
+  unsigned b[4][4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const floatx4 v = *reinterpret_cast<const floatx4*>(xr + (long long)c * len);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) b[c][e] = __float_as_uint(v[e]);
+  }
+  bool ok = true;
+  unsigned packed = 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    unsigned code = 4, ones = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (b[c][e] == 0x3f800000u) {
+        ++ones;
+        code = c;
+      } else if (b[c][e] != 0u) {
+        ok = false;
+      }
+    }
+    ok &= ones <= 1;
+    packed |= code << (8 * e);
+  }
+  if (!ok) *bad = 1;
+  if (codes) *reinterpret_cast<unsigned*>(codes + w * len + p) = packed;
 }
 
 // ---- handle -----------------------------------------------------------------------------
@@ -1239,6 +1281,10 @@ struct expecto_beluga {
   float* kmer = nullptr;              //   the table (shared by handles with the same conv1 / conv2 weights)
   uint64_t kmer_key = 0;
   bool kmer_quad = true;              //   conv2 rows from the quad tables (EXPECTO_KMER_QUAD=0: pair tables only)
+  int kmer_state = 1;                 //   0 held, 1 off (EXPECTO_CONV2_TABLE=0), 2 no room (conv2_table_active)
+  bool onehot_as_codes = true;        // forward_onehot: exact one-hot input through the k-mer gather (EXPECTO_ONEHOT_CODES)
+  uint8_t* oh_codes = nullptr;        //   its codes, max_batch x 2000 (allocated on first use)
+  int* oh_bad = nullptr;              //   its check flag
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, int>> pending;  // (layer, event index of start)
@@ -1274,7 +1320,7 @@ struct KmerEntry {
   uint64_t key;
   std::vector<float> w;   // the conv1 / conv2 weights the tables were built from (exact match, not just the hash)
   float* T;
-  int refs;
+  std::vector<const expecto_beluga*> holders;   // the first one reports the bytes (expecto_beluga_device_bytes)
 };
 std::mutex g_kmer_mu;
 std::vector<KmerEntry> g_kmer;
@@ -1286,8 +1332,20 @@ uint64_t fnv1a(const void* p, size_t n, uint64_t hsh = 1469598103934665603ULL) {
 }
 
 // Build (or share) the handle's k-mer table from its conv1 weights (w1, b1) and repacked conv2
-// weights.  If its 10 GB do not fit, the handle runs conv2 on the MFMAs instead (kmer stays null).
+// weights.  If its 20.7 GB (plus 9 GB of fp64 scratch while building) do not fit, or exceed
+// EXPECTO_KMER_MAX_BYTES, the handle runs conv2 on the MFMAs instead (kmer stays null,
+// kmer_state 2, one line on stderr; expecto_beluga_conv2_table_active reports it).
+int kmer_no_room(expecto_beluga* h, const char* why) {
+  h->kmer_state = 2;
+  fprintf(stderr, "expecto_hip: no k-mer tables on device %d (%s): conv2 runs on the MFMAs (about -25%% throughput)\n",
+          h->device, why);
+  return EXPECTO_OK;
+}
+
 int kmer_acquire(expecto_beluga* h, const float* const* params, hipStream_t st) {
+  const size_t tb = kKmerFloats * sizeof(float), fb = (size_t)kMer8 * 320 * sizeof(double);
+  if (const char* e = getenv("EXPECTO_KMER_MAX_BYTES"))
+    if ((double)tb > atof(e)) return kmer_no_room(h, "EXPECTO_KMER_MAX_BYTES");
   std::vector<float> hw(320 * 32 + 320 + 320 * 320 * 8);
   EXPECTO_HIP_CHECK(hipMemcpyAsync(hw.data(), params[0], 320 * 32 * sizeof(float), hipMemcpyDeviceToHost, st));
   EXPECTO_HIP_CHECK(hipMemcpyAsync(hw.data() + 320 * 32, params[1], 320 * sizeof(float), hipMemcpyDeviceToHost, st));
@@ -1298,18 +1356,18 @@ int kmer_acquire(expecto_beluga* h, const float* const* params, hipStream_t st) 
   std::lock_guard<std::mutex> lock(g_kmer_mu);
   for (KmerEntry& e : g_kmer)
     if (e.device == h->device && e.key == key && e.w == hw) {
-      ++e.refs;
+      e.holders.push_back(h);
       h->kmer = e.T;
       h->kmer_key = key;
+      h->kmer_state = 0;
       return EXPECTO_OK;
     }
   void *t = nullptr, *f = nullptr, *gg = nullptr;
-  const size_t tb = kKmerFloats * sizeof(float), fb = (size_t)kMer8 * 320 * sizeof(double);
   if (hipMalloc(&t, tb) != hipSuccess || hipMalloc(&f, fb) != hipSuccess || hipMalloc(&gg, 8 * fb) != hipSuccess) {
     (void)hipGetLastError();
     for (void* x : {t, f, gg})
       if (x) (void)hipFree(x);
-    return EXPECTO_OK;   // no table: conv2 on the MFMAs
+    return kmer_no_room(h, "device allocation failed");   // no table: conv2 on the MFMAs
   }
   float* T = static_cast<float*>(t);
   double* F = static_cast<double*>(f);
@@ -1332,9 +1390,10 @@ int kmer_acquire(expecto_beluga* h, const float* const* params, hipStream_t st) 
     (void)hipFree(t);
     return rc;
   }
-  g_kmer.push_back({h->device, key, std::move(hw), T, 1});
+  g_kmer.push_back({h->device, key, std::move(hw), T, {h}});
   h->kmer = T;
   h->kmer_key = key;
+  h->kmer_state = 0;
   return EXPECTO_OK;
 }
 
@@ -1343,13 +1402,25 @@ void kmer_release(expecto_beluga* h) {
   std::lock_guard<std::mutex> lock(g_kmer_mu);
   for (size_t i = 0; i < g_kmer.size(); ++i)
     if (g_kmer[i].T == h->kmer) {
-      if (--g_kmer[i].refs == 0) {
+      auto& hs = g_kmer[i].holders;
+      hs.erase(std::find(hs.begin(), hs.end(), h));
+      if (hs.empty()) {
         (void)hipFree(g_kmer[i].T);
         g_kmer.erase(g_kmer.begin() + (long)i);
       }
       break;
     }
   h->kmer = nullptr;
+}
+
+// Bytes of the k-mer tables h reports: all of them if h is their first live holder, else 0, so
+// device_bytes summed over the handles sharing one table counts it once.
+size_t kmer_reported_bytes(const expecto_beluga* h) {
+  if (!h->kmer) return 0;
+  std::lock_guard<std::mutex> lock(g_kmer_mu);
+  for (const KmerEntry& e : g_kmer)
+    if (e.T == h->kmer) return e.holders.front() == h ? kKmerFloats * sizeof(float) : 0;
+  return 0;
 }
 
 
@@ -2548,6 +2619,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   if (const char* e = getenv("EXPECTO_FUSE_CONV1")) h->fuse_conv1 = atoi(e) != 0;         // same bits either way
   if (const char* e = getenv("EXPECTO_CONV2_TABLE")) h->kmer_on = atoi(e) != 0;   // conv2 on the MFMAs (parity, not bits)
   if (const char* e = getenv("EXPECTO_KMER_QUAD")) h->kmer_quad = atoi(e) != 0;    // pair tables only (parity, not bits)
+  if (const char* e = getenv("EXPECTO_ONEHOT_CODES")) h->onehot_as_codes = atoi(e) != 0;   // parity, not bits
   if (const char* e = getenv("EXPECTO_SEG_CHUNK_WINDOWS")) h->seg_chunk_windows = atoi(e);   // same bits either way
   if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)
     const int v = atoi(e);
@@ -2607,7 +2679,13 @@ void expecto_beluga_destroy(expecto_beluga_t h) {
 }
 
 size_t expecto_beluga_device_bytes(expecto_beluga_t h) {
-  return h ? h->bytes + (h->kmer ? kKmerFloats * sizeof(float) : 0) : 0;
+  return h ? h->bytes + kmer_reported_bytes(h) : 0;
+}
+
+int expecto_beluga_conv2_table_active(expecto_beluga_t h, int* reason) {
+  EXPECTO_REQUIRE(h != nullptr, "null handle");
+  if (reason) *reason = h->kmer_state;
+  return h->kmer ? 1 : 0;
 }
 
 int expecto_beluga_forward_onehot(expecto_beluga_t h, const float* x, int n, float* y, void* stream) {
@@ -2617,10 +2695,50 @@ int expecto_beluga_forward_onehot(expecto_beluga_t h, const float* x, int n, flo
   EXPECTO_REQUIRE(x != nullptr && y != nullptr, "null input/output");
   EXPECTO_HIP_CHECK(hipSetDevice(h->device));
   hipStream_t st = as_stream(stream);
+  // The reference's own call (Beluga.forward on encodeSeqs' one-hot floats, chromatin.py:266-279):
+  // when every column of x is an exact one-hot or all-zero column, the call runs as
+  // forward_codes(FWD) on codes converted chunk by chunk -- conv1 + conv2 + pool1 from the k-mer
+  // tables, the same bits as forward_codes -- else conv1 / conv2 stay on the MFMAs (any fp32
+  // input, like the reference).  Deciding costs one check pass over x and one stream sync.
+  bool as_codes = false;
+  if (h->onehot_as_codes && h->kmer && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+      (h->precision == EXPECTO_PRECISION_F16X3 || h->precision == EXPECTO_PRECISION_BF16X6)) {
+    if (!h->oh_codes) {
+      float *c = nullptr, *f = nullptr;
+      int rc;
+      if ((rc = dalloc(h, &c, ((size_t)h->max_batch * kLen + 3) / 4)) || (rc = dalloc(h, &f, 1))) return rc;
+      h->oh_codes = reinterpret_cast<uint8_t*>(c);
+      h->oh_bad = reinterpret_cast<int*>(f);
+    }
+    int bad = 0;
+    {
+      LayerTimer lt(h, 0, st);
+      EXPECTO_HIP_CHECK(hipMemsetAsync(h->oh_bad, 0, sizeof(int), st));
+      const long long q = (long long)n * (kLen / 4);
+      onehot_codes<<<dim3((unsigned)((q + 255) / 256)), dim3(256), 0, st>>>(x, n, kLen, nullptr, h->oh_bad);
+      int rc = check_launch("onehot_codes check");
+      if (rc) return rc;
+    }
+    EXPECTO_HIP_CHECK(hipMemcpyAsync(&bad, h->oh_bad, sizeof(int), hipMemcpyDeviceToHost, st));
+    EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
+    as_codes = bad == 0;
+  }
   return run_checked(h, st, [&]() {
     for (long long r0 = 0; r0 < n; r0 += h->max_batch) {
       const int nb = (int)std::min<long long>(h->max_batch, n - r0);
-      int rc = forward_chunk(h, x, nullptr, 0, 0, 0, r0, nb, y + r0 * kNFeat, st);
+      int rc;
+      if (as_codes) {
+        {
+          LayerTimer lt(h, 0, st);
+          const long long q = (long long)nb * (kLen / 4);
+          onehot_codes<<<dim3((unsigned)((q + 255) / 256)), dim3(256), 0, st>>>(x + r0 * 4 * kLen, nb, kLen,
+                                                                              h->oh_codes, nullptr);
+          if ((rc = check_launch("onehot_codes"))) return rc;
+        }
+        rc = forward_chunk(h, nullptr, h->oh_codes, kLen, nb, EXPECTO_STRAND_FWD, 0, nb, y + r0 * kNFeat, st);
+      } else {
+        rc = forward_chunk(h, x, nullptr, 0, 0, 0, r0, nb, y + r0 * kNFeat, st);
+      }
       if (rc) return rc;
     }
     return (int)EXPECTO_OK;

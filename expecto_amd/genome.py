@@ -9,7 +9,8 @@ pyfasta does.
 
 **Code cache** (round 4; the role pyfasta's ``.flat`` + ``.gdx`` play for the reference: it
 flattens the FASTA once and memory-maps it on every later open).  The first open of a FASTA
-writes, next to it (or under ``$EXPECTO_CACHE_DIR`` when its directory is read-only):
+writes (about 2x the genome's size; one line on stderr says where), next to it, or under
+``$EXPECTO_CACHE_DIR`` when that is set or the FASTA's directory is read-only:
 
 * ``<fa>.expecto.flat``  -- the contigs' sequence bytes, newlines removed (case kept);
 * ``<fa>.expecto.codes`` -- the device layout: one uint8 code per base (0=A 1=G 2=C 3=T
@@ -55,10 +56,11 @@ def _stat_key(path: str) -> dict:
 
 
 def cache_prefix(path: str) -> str:
-    """Where the cache files of FASTA ``path`` live: next to it when that directory is writable,
-    else ``$EXPECTO_CACHE_DIR`` (default ``~/.cache/expecto_amd``) keyed by the real path."""
+    """Where the cache files of FASTA ``path`` live: under ``$EXPECTO_CACHE_DIR`` keyed by the
+    real path when it is set, else next to the FASTA when that directory is writable, else under
+    ``~/.cache/expecto_amd``."""
     d = os.path.dirname(os.path.abspath(path))
-    if os.access(d, os.W_OK):
+    if not os.environ.get("EXPECTO_CACHE_DIR") and os.access(d, os.W_OK):
         return os.path.abspath(path) + ".expecto"
     root = os.environ.get("EXPECTO_CACHE_DIR") or os.path.join(os.path.expanduser("~"), ".cache", "expecto_amd")
     os.makedirs(root, exist_ok=True)
@@ -112,7 +114,11 @@ def build_cache(path: str, prefix: str | None = None) -> str:
     each contig.  Files are written under temporary names and renamed, the index last."""
     prefix = prefix or cache_prefix(path)
     key = _stat_key(path)
-    tmp = f".tmp{os.getpid()}"
+    import secrets
+    import socket
+    # unique per builder even where flock does not reach across nodes (a shared / network file
+    # system): host, pid and a random token, so two builders never write the same temp files
+    tmp = f".tmp.{socket.gethostname()}.{os.getpid()}.{secrets.token_hex(4)}"
     names, lengths, flat_off, code_off = [], [], [], []
     bad_off, bad_chr = [], []
     guard = np.full(GUARD, CODE_ZERO, np.uint8)
@@ -181,6 +187,9 @@ def build_cache(path: str, prefix: str | None = None) -> str:
                  invalid_chars=inv_chr)
     for ext in (".flat", ".codes", ".gdx.npz"):
         os.replace(prefix + ext + tmp, prefix + ext)
+    import sys
+    print(f"expecto_amd.genome: built the code cache of {path} at {prefix}.{{flat,codes,gdx.npz}} "
+          f"({(fpos + cpos) / 1e9:.2f} GB; EXPECTO_CACHE_DIR moves it)", file=sys.stderr)
     return prefix
 
 
@@ -198,7 +207,9 @@ def open_cache(path: str):
             return None
         if any(not os.path.exists(prefix + e) for e in (".flat", ".codes")):
             return None
-        if os.path.getsize(prefix + ".codes") != idx[0]["code_total"]:
+        # both data files at the byte lengths the index recorded (a torn or foreign write is rebuilt)
+        if (os.path.getsize(prefix + ".codes") != idx[0]["code_total"]
+                or os.path.getsize(prefix + ".flat") != idx[0]["flat_total"]):
             return None
         return idx
 
@@ -336,7 +347,8 @@ def upload_codes(host: CodeGenome, device, chunk: int = 256 << 20):
     n = int(host.codes.size)
     out = torch.empty(n, dtype=torch.uint8, device=device)
     if host.codes_path is None or n <= chunk:
-        out.copy_(torch.from_numpy(np.ascontiguousarray(host.codes)))
+        src = host.codes if host.codes.flags.writeable else np.array(host.codes)   # a read-only map: copy (torch
+        out.copy_(torch.from_numpy(np.ascontiguousarray(src)))                      # warns on non-writable arrays)
         return out
     bufs = [torch.empty(chunk, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
     events = [None, None]

@@ -336,7 +336,8 @@ class VariantPipeline:
         overflow -- then recompute just the flagged slices in bf16x6 into `out`.  Cost 1 + 2f
         batch-times for a flagged fraction f, against 2 for the whole batch.  If no slice flags
         again, the whole batch is recomputed in bf16x6 (counted once).  Returns the number of
-        slices recomputed (each flagged slice counted by the engine's fallback counter)."""
+        bf16x6 recomputations, as the engine's fallback counter counts them: one per flagged
+        slice, or 1 when the whole batch was recomputed."""
         eng = self.engine
         n = len(vs)
         if n == 0:
@@ -368,7 +369,7 @@ class VariantPipeline:
             with eng.precision_override("bf16x6"):
                 self.predict(self.prepare(vs, shifts, rows), out=out)
             eng.count_fallback()
-            redone = k
+            redone = 1
         return redone
 
     def sed_features(self, y: torch.Tensor, weights: torch.Tensor, out: torch.Tensor | None = None,

@@ -97,10 +97,23 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
 void expecto_beluga_destroy(expecto_beluga_t h);
 
 /* Bytes of device memory the handle owns (weights + workspace) plus the k-mer tables it
- * holds (20.7 GB, shared with other handles of the same conv1 / conv2 weights). */
+ * holds (20.7 GB) if it is their first live holder: summed over handles that share one set of
+ * tables, the tables count once. */
 size_t expecto_beluga_device_bytes(expecto_beluga_t h);
 
-/* y[n,2002] = Beluga.forward(x[n,4,1,2000]) (x contiguous fp32, any values). */
+/* 1 if the handle's forwards from base codes (and exact one-hot floats) gather conv1 + conv2 +
+ * pool1 from the k-mer tables, 0 if they run conv1 / conv2 on the MFMAs (same parity bar, other
+ * bits; about -25 % throughput).  *reason (may be NULL): 0 tables held, 1 switched off
+ * (EXPECTO_CONV2_TABLE=0), 2 no room (the device allocation failed, or the tables exceed
+ * EXPECTO_KMER_MAX_BYTES; the library then prints one line on stderr at creation). */
+int expecto_beluga_conv2_table_active(expecto_beluga_t h, int* reason);
+
+/* y[n,2002] = Beluga.forward(x[n,4,1,2000]) (x contiguous fp32, any values).  When the handle
+ * holds the k-mer tables, runs F16X3 or BF16X6, x is 16-byte aligned and every column of x is an
+ * exact one-hot column (one 1.0f, three +0.0f) or all zeros, as encodeSeqs writes them
+ * (chromatin.py:138-172), the call converts x to base codes and equals
+ * expecto_beluga_forward_codes(FWD) bit for bit; otherwise conv1 / conv2 run on the MFMAs.  The
+ * check costs one pass over x and one stream sync. */
 int expecto_beluga_forward_onehot(expecto_beluga_t h, const float* x, int n, float* y, void* stream);
 
 /* Windows given as base codes (uint8, 0=A 1=G 2=C 3=T 4=zero column for N/n/H/-),
