@@ -73,6 +73,12 @@ class BelugaEngine:
                        "set_precision")
         self.precision = precision
 
+    def set_fc1_role(self, role: int):
+        """Block-Karatsuba FC1 role (0..3) of this engine's per-window forwards (include/expecto_hip.h
+        expecto_beluga_set_fc1_role): a segment-path window of role r equals a per-window forward
+        in role r bit for bit (pipeline.fc1_role gives a segment window's role)."""
+        _lib.check(self.lib.expecto_beluga_set_fc1_role(self.handle, int(role)), "set_fc1_role")
+
     def set_f16_target(self, target_log2: int):
         """f16x3 calibration target: the largest calibration activation maps to 2^target_log2."""
         with torch.cuda.device(self.device):

@@ -797,6 +797,207 @@ __global__ void pair_rows(long long* __restrict__ c_rows, int M, int nv, int v0,
   if (m < M) c_rows[m] = (long long)(m / nv) * strand_stride + v0 + m % nv;
 }
 
+// ---- FC1 as a block-Karatsuba convolution (f16x3, round 5) ---------------------------------
+// FC1 (Beluga.py:43-44) of a window reads its 106 conv6 rows x[0..105] as y = sum_{q<4} V_q X_q +
+// T x[100..105], with X_q the 25-row block x[25q .. 25q+24] and V_q the matching 2003 x 16000
+// slice of the weights.  On a 200-bp shift sweep, windows 400 bp apart in one pool2-phase block
+// are 25 conv6 rows apart, so 4 such windows y_a (a = 0..3, blocks X_{a..a+3} of one sequence) are
+// a 4-tap convolution over blocks, and two nested Karatsuba steps (F(2,2) x F(2,2)) give them
+// from 9 block products instead of 16 (-41 % of FC1's multiply-adds on the headline):
+//   m0 = V0 DD@0        m1 = (V0+V1) D2@1       m2 = -V1 DD@1
+//   m3 = (V0+V2) D1@2   m4 = (V0+V1+V2+V3) X@3  m5 = -(V1+V3) D1@3
+//   m6 = -V2 DD@2       m7 = -(V2+V3) D2@3      m8 = V3 DD@3
+//   y0 = m0+m1+m3+m4   y1 = m1+m2+m4+m5   y2 = m3+m4+m6+m7   y3 = m4+m5+m7+m8   (+ the tail each)
+// with S@b the rows 25b .. 25b+24 (from the group's first window) of the row sequences
+//   D1[r] = x[r] - x[r+25],  D2[r] = x[r] - x[r+50],  DD[r] = (x[r] - x[r+25]) - (x[r+50] - x[r+75]).
+// Every product of window a's sum reads only rows of window a itself, so a window can be computed
+// alone in its role a (its position in the group: (conv6 offset / 25) mod 4): the per-window
+// forwards use role 0 (EXPECTO_FC1_ROLE), the segment path gives each window the role of its
+// offset and shares each group's products, and every path computes a window's FC1 as the same
+// sum of the same partial products -- bitwise equal (tests/test_gpu_fc1_karatsuba.py).  Weights
+// of the 9 products are formed once per handle in fp64 and rounded to fp32 once; the sequences
+// are formed in fp32 from the stored f16x3 planes and stored as planes (22-bit) like any
+// activation.  tests/test_fc1_karatsuba_identity.py checks the algebra in float64.
+constexpr int kFkK = 16000;                        // one 25-row block of conv6 rows (25 x 640)
+constexpr int kFkKb = kFkK / GBK;                  // 500 K blocks
+constexpr int kFkSlabs = 2;                        // K slabs per product (250 K blocks, as FC1's 265)
+constexpr int kFkTailK = kFc1In - 4 * kFkK;        // 3840: rows 100..105
+constexpr int kFkKbTotal = 9 * kFkKb + kFkTailK / GBK;   // 4620 K blocks per weight row
+constexpr long long kFkKTotal = 9LL * kFkK + kFkTailK;   // 147,840
+constexpr int kFkSeq[9] = {3, 2, 3, 1, 0, 1, 3, 2, 3};   // product g reads sequence (0 x, 1 D1, 2 D2, 3 DD)
+constexpr int kFkBlk[9] = {0, 1, 1, 2, 3, 3, 2, 3, 3};   //   at block kFkBlk[g] of its group
+constexpr int kFkRole[4][4] = {{0, 1, 3, 4}, {1, 2, 4, 5}, {3, 4, 6, 7}, {4, 5, 7, 8}};
+constexpr int kFkW[9][4] = {{1, 0, 0, 0}, {1, 1, 0, 0}, {0, -1, 0, 0}, {1, 0, 1, 0}, {1, 1, 1, 1},
+                            {0, -1, 0, -1}, {0, 0, -1, 0}, {0, 0, -1, -1}, {0, 0, 0, 1}};   // V_q coefficients
+constexpr int kFkParts = 4 * kFkSlabs + 1;         // partial rows a window's FC1 sums (8 + the tail)
+
+// Karatsuba FC1 weights (fp32, K = 9 x 16000 + 3840 per row) from the repacked FC1 weights
+// (w1 [rows][67840], K = t*640 + c): product g's row = sum_q kFkW[g][q] V_q in fp64, then the tail.
+__global__ void fk_weights(const float* __restrict__ w1, long long rows, float* __restrict__ wk) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * kFkKTotal) return;
+  const long long n = i / kFkKTotal;
+  const int k = (int)(i - n * kFkKTotal);
+  const float* wr = w1 + n * kFc1In;
+  if (k >= 9 * kFkK) {
+    wk[i] = wr[4 * kFkK + (k - 9 * kFkK)];
+    return;
+  }
+  const int g = k / kFkK, kk = k - g * kFkK;
+  double s = 0.0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (kFkW[g][q]) s += kFkW[g][q] * (double)wr[q * kFkK + kk];
+  wk[i] = (float)s;
+}
+
+// The row sequences D1, D2, DD of f16x3 conv6 rows (x: blocks of `s` rows, the first T valid):
+// row r of a block gets D1 / D2 / DD where its last input row r + 25 / 50 / 75 is in [lo, hi).
+// Values from the stored planes (x = hi + lo), fp32 arithmetic in a fixed order, plain split (the
+// planes are consumed as stored), the overflow flag as any f16x3 store.  [lo, hi) = [0, T), or
+// with `tab` (segment pairs: the alt blocks seg_alt_blocks filled, n_ph blocks per segment) the
+// rows that alt block holds.  320 threads = 4 rows x 80 eight-channel pieces (16 B of hi + 16 B of lo).
+__global__ __launch_bounds__(320) void fk_seq_h2(const float* __restrict__ x, int T, int s, const int* __restrict__ tab,
+                                                 int n_ph, float* __restrict__ d1, float* __restrict__ d2,
+                                                 float* __restrict__ dd, int* __restrict__ ovf) {
+  const int c8 = threadIdx.x % 80;
+  const int rq = (T + 3) >> 2;   // 4-row groups per block; grid = blocks x rq (1-D)
+  const long long blk = blockIdx.x / rq;
+  const int r = (int)(blockIdx.x - blk * rq) * 4 + threadIdx.x / 80;
+  int lo = 0, hi = T;
+  if (tab) {
+    const int q = tab[(blk / n_ph) * kSegTab];
+    lo = q >= 1999 ? (q - 1999) >> 4 : 0;
+    hi = min(T, (q >> 4) + 106);
+  }
+  if (r < lo || r + 25 >= hi) return;
+  constexpr long long rb = 640 * 4;   // bytes per row (20 groups of [32 hi | 32 lo] fp16)
+  const int cofs = (c8 >> 2) * 128 + (c8 & 3) * 16;
+  const long long o = (blk * s + r) * rb + cofs;
+  const char* src = reinterpret_cast<const char*>(x) + o;
+  float v[4][8];
+  const int nrow = r + 75 < hi ? 4 : r + 50 < hi ? 3 : 2;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (j < nrow) {
+      const halfx8 h = *reinterpret_cast<const halfx8*>(src + j * 25 * rb);
+      const halfx8 l = *reinterpret_cast<const halfx8*>(src + j * 25 * rb + 64);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[j][e] = (float)h[e] + (float)l[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[j][e] = 0.f;
+    }
+  }
+  bool bad = false;
+  auto put = [&](float* dst, const float (&y)[8]) {
+    halfx8 h, l;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bad |= !(fabsf(y[e]) < 65504.f);
+      _Float16 a, b;
+      split_h2p(y[e], a, b);
+      h[e] = a;
+      l[e] = b;
+    }
+    char* d = reinterpret_cast<char*>(dst) + o;
+    *reinterpret_cast<halfx8*>(d) = h;
+    *reinterpret_cast<halfx8*>(d + 64) = l;
+  };
+  float a[8], y[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = v[0][e] - v[1][e];
+  put(d1, a);
+  if (nrow >= 3) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) y[e] = v[0][e] - v[2][e];
+    put(d2, y);
+  }
+  if (nrow == 4) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) y[e] = a[e] - (v[2][e] - v[3][e]);
+    put(dd, y);
+  }
+  if (bad) *ovf = 1;
+}
+
+// FC1 output rows of the block Karatsuba: row m = sum of its kFkParts partial rows prow[m][j] (its
+// 4 products x 2 K slabs in product order, then the tail), unscaled, + bias, ReLU, f16x3 planes
+// for FC2 (the same per-element steps as fc1_reduce_h2).  4 columns per thread.
+__global__ void fk_reduce_h2(const float* __restrict__ part, const int* __restrict__ prow, long long count4,
+                             const float* __restrict__ bias, float* __restrict__ h1, const float* __restrict__ col_scale,
+                             float osc, int* __restrict__ ovf) {
+  const long long i4 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i4 >= count4) return;
+  const long long row = i4 / (kHidLd / 4);
+  const int n = (int)(i4 - row * (kHidLd / 4)) * 4;
+  floatx4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < kFkParts; ++j) {
+    const floatx4 v = *reinterpret_cast<const floatx4*>(part + (long long)prow[row * kFkParts + j] * kHidLd + n);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s[e] += v[e];
+  }
+  halfx4 hv, lv;
+  bool bad = false;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float t = s[e] * col_scale[n + e];
+    const float v = n + e < kFc1Out ? fmaxf(t + bias[min(n + e, kFc1Out - 1)], 0.f) : 0.f;
+    const float x = v * osc;
+    bad |= !(fabsf(x) < 65504.f);
+    _Float16 hh, ll;
+    split_h2p(x, hh, ll);
+    hv[e] = hh;
+    lv[e] = ll;
+  }
+  if (bad && ovf) *ovf = 1;
+  _Float16* d = reinterpret_cast<_Float16*>(h1) + act_index<2>(row, kHidLd, n);
+  *reinterpret_cast<halfx4*>(d) = hv;
+  *reinterpret_cast<halfx4*>(d + 32) = lv;
+}
+
+// Per-window block Karatsuba (every window alone in role `role`, its 106 rows at m * rstride rows):
+// group starts g_rows[m] = (m * rstride - 25 role) * 640, window starts w_rows[m] = m * rstride * 640,
+// partial rows of window m: (2j + s) * M + m for its j-th product and slab s, then 8 M + m.
+__global__ void fk_window_tables(int M, int rstride, int role, long long* __restrict__ g_rows,
+                                 long long* __restrict__ w_rows, int* __restrict__ prow) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  g_rows[m] = ((long long)m * rstride - 25LL * role) * 640;
+  w_rows[m] = (long long)m * rstride * 640;
+#pragma unroll
+  for (int j = 0; j < kFkParts; ++j) prow[(long long)m * kFkParts + j] = j * M + m;
+}
+
+// Alt masks of the per-window block Karatsuba (pair path): window m's alt conv6 differs from its
+// ref rows only in [r6, r6 + 20) (window rows), so partial (product j, slab s) -- sequence rows
+// 25 (blk - role) + [13 s - (s ? 1 : 0), 13 s + 12] with their lags -- and the tail (rows 100..105)
+// are recomputed only where a dependency row falls in that run: bit 0 of mask[d * tiles + m / 256]
+// for descriptor d = 2j + s (8 = the tail).  Unset descriptors keep the ref partials in place.
+__global__ void fk_window_mask(const int* __restrict__ var_pos, int nv, int v0, int R, int role, int tiles,
+                               unsigned* __restrict__ mask) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= R) return;
+  const int r6 = delta_rows(pair_pos(var_pos, m, nv, v0)).r[6], r6e = r6 + kDW[6];
+  for (int j = 0; j < 4; ++j) {
+    const int g = kFkRole[role][j], sq = kFkSeq[g];
+    const int nl = sq == 0 ? 1 : sq == 3 ? 4 : 2;
+    const int lag1 = sq == 2 ? 50 : 25;
+    for (int s = 0; s < kFkSlabs; ++s) {
+      // K elements [s * 8000, (s + 1) * 8000) of the product = its rows [12.5 s, 12.5 (s + 1))
+      const int i0 = 25 * (kFkBlk[g] - role) + (s * 8000) / 640, i1 = 25 * (kFkBlk[g] - role) + ((s + 1) * 8000 - 1) / 640;
+      bool hit = false;
+      for (int l = 0; l < nl; ++l) {
+        const int lag = l == 0 ? 0 : (nl == 2 ? lag1 : 25 * l);
+        hit |= i0 + lag < r6e && i1 + lag >= r6;
+      }
+      if (hit) atomicOr(mask + (2 * j + s) * tiles + m / 256, 1u);
+    }
+  }
+  if (100 < r6e && 105 >= r6) atomicOr(mask + 8 * tiles + m / 256, 1u);
+}
+
 // ---- weight repacking (reference layouts -> kernel layouts) --------------------------
 __global__ void repack_conv(const float* __restrict__ W, int cout, int cin, int npad, float* __restrict__ Wt) {
   const long long K = 8LL * cin;
@@ -1282,6 +1483,17 @@ struct expecto_beluga {
   uint64_t kmer_key = 0;
   bool kmer_quad = true;              //   conv2 rows from the quad tables (EXPECTO_KMER_QUAD=0: pair tables only)
   int kmer_state = 1;                 //   0 held, 1 off (EXPECTO_CONV2_TABLE=0), 2 no room (conv2_table_active)
+  bool fk_on = true;                  // f16x3 FC1 as a block-Karatsuba convolution (EXPECTO_FC1_KARATSUBA)
+  int fk_role = 0;                    //   role of per-window forwards (EXPECTO_FC1_ROLE, 0..3)
+  float* fkw = nullptr;               //   the 9 products' + tail weight planes [npad][kFkKbTotal][2][32] fp16
+  int* fk_sw = nullptr;               //   their per-row scale exponents
+  float* fk_cs = nullptr;             //   column unscale 2^-(sx[5] + fk_sw[n])
+  float* fk_seq[3] = {};              //   row sequences D1, D2, DD (x's row layout), fk_seq_rows rows each
+  long long fk_seq_rows = 0;
+  long long* fk_grows = nullptr;      //   group starts (per product), window starts, partial rows, alt masks
+  long long* fk_wrows = nullptr;
+  int* fk_prow = nullptr;
+  unsigned* fk_mask = nullptr;
   bool onehot_as_codes = true;        // forward_onehot: exact one-hot input through the k-mer gather (EXPECTO_ONEHOT_CODES)
   uint8_t* oh_codes = nullptr;        //   its codes, max_batch x 2000 (allocated on first use)
   int* oh_bad = nullptr;              //   its check flag
@@ -1871,6 +2083,218 @@ int run_fc(expecto_beluga* h, const float* act, const long long* a_rows, int nb,
   return run_fc2(h, h->h1, nb, y, st, c_rows);
 }
 
+int count_desc_macs(expecto_beluga* h, const unsigned* mask, int tiles, double per_tile, hipStream_t st);
+
+// ---- FC1 block Karatsuba (f16x3): host side (kernels and algebra: "FC1 as a block-Karatsuba
+// convolution" above) ------------------------------------------------------------------------
+bool fk_use(const expecto_beluga* h) {
+  return h->fk_on && h->fkw && g_precision == EXPECTO_PRECISION_F16X3 && fc_wide_tiles(h);
+}
+
+// Table buffers, allocated with the first Karatsuba FC1: group starts (9 lists of <= max_batch),
+// window starts, kFkParts partial rows per window, kFkParts x tiles alt-mask words.
+int fk_tables(expecto_beluga* h) {
+  if (h->fk_grows) return EXPECTO_OK;
+  const size_t mb = h->max_batch, tiles = (mb + 255) / 256;
+  float *a = nullptr, *b = nullptr, *c = nullptr, *d = nullptr;
+  int rc;
+  if ((rc = dalloc(h, &a, 2 * 9 * mb)) || (rc = dalloc(h, &b, 2 * mb)) || (rc = dalloc(h, &c, kFkParts * mb)) ||
+      (rc = dalloc(h, &d, kFkParts * tiles)))
+    return rc;
+  h->fk_grows = reinterpret_cast<long long*>(a);
+  h->fk_wrows = reinterpret_cast<long long*>(b);
+  h->fk_prow = reinterpret_cast<int*>(c);
+  h->fk_mask = reinterpret_cast<unsigned*>(d);
+  return EXPECTO_OK;
+}
+
+// The D1 / D2 / DD sequence buffers for `rows` conv6 rows (grown on demand; hipFree synchronises,
+// so they are sized once for the largest call).
+int fk_seq_alloc(expecto_beluga* h, long long rows) {
+  if (rows <= h->fk_seq_rows) return EXPECTO_OK;
+  for (float*& p : h->fk_seq)
+    if (p) {
+      EXPECTO_HIP_CHECK(hipFree(p));
+      p = nullptr;
+    }
+  h->bytes -= (size_t)h->fk_seq_rows * 640 * 4 * 3;
+  h->fk_seq_rows = 0;
+  for (float*& p : h->fk_seq) {
+    hipError_t e = hipMalloc(&p, (size_t)rows * 640 * 4 + 16 * 640 * 4);
+    if (e != hipSuccess) {
+      set_error(std::string("hipMalloc (FC1 sequences): ") + hipGetErrorString(e));
+      return EXPECTO_ENOMEM;
+    }
+  }
+  h->fk_seq_rows = rows;
+  h->bytes += (size_t)rows * 640 * 4 * 3;
+  return EXPECTO_OK;
+}
+
+// D1 / D2 / DD of `blocks` blocks of T conv6 rows at a stride of s rows (tab: alt blocks, see fk_seq_h2)
+int fk_sequences(expecto_beluga* h, const float* x, long long blocks, int T, int s, const int* tab, int n_ph,
+                 hipStream_t st) {
+  int rc;
+  if ((rc = fk_seq_alloc(h, blocks * s))) return rc;
+  LayerTimer lt(h, 7, st);   // the sequences are timed with the FC1 reduction (slot fc1_reduce)
+  const long long nblk = blocks * ((T + 3) / 4);
+  EXPECTO_REQUIRE(nblk > 0 && nblk < (1LL << 31), "FC1 sequence grid");
+  fk_seq_h2<<<dim3((unsigned)nblk), dim3(320), 0, st>>>(x, T, s, tab, n_ph, h->fk_seq[0], h->fk_seq[1], h->fk_seq[2],
+                                                       h->ovf);
+  return check_launch("fk_seq_h2");
+}
+
+// Which products a window set needs: product g's group rows are cnt[g] starts at g_rows + off[g].
+struct FkProducts {
+  const long long* g_rows;
+  int off[9];
+  int cnt[9];
+};
+
+// One grouped launch of the Karatsuba FC1 over n windows: per product g with cnt[g] groups, its
+// kFkSlabs K slabs, then the tail over the windows (w_rows: window starts), as split-K partial rows
+// of `part` in that order (the layout prow was built for); then fk_reduce_h2 into h1.  x: conv6 rows
+// (the product X@3 and the tail), seq: their D1 / D2 / DD.  mask (alt, in place): descriptor d runs
+// only the M tiles with bit 0 of mask[d * tiles + tile] set.
+int fk_fc1(expecto_beluga* h, const float* x, float* const* seq, const FkProducts& pr, const long long* w_rows, int n,
+           const int* prow, float* h1, hipStream_t st, const unsigned* mask = nullptr, int tiles = 0) {
+  FcGroup G{};
+  G.kb_total = kFkKbTotal;
+  G.n_tiles = (kHidLd + FCW_BN - 1) / FCW_BN;
+  G.n_store = kHidLd;
+  G.ldc = kHidLd;
+  const char* wb = reinterpret_cast<const char*>(h->fkw);
+  long long row = 0;
+  long long blk = 0;
+  double macs = 0.0;
+  auto add = [&](const float* A, const long long* ar, long long aoff, int kb0, int nk, int M) {
+    FcDesc& d = G.d[G.n];
+    d.A = A;
+    d.a_rows = ar;
+    d.a_off = aoff;
+    d.Bp = wb + (long long)kb0 * 128;
+    d.C = h->part + row * kHidLd;
+    d.mask = mask ? mask + (size_t)G.n * tiles : nullptr;
+    d.M = M;
+    d.m_tiles = (M + X6P_BM - 1) / X6P_BM;
+    d.nk = nk;
+    d.blk0 = (int)blk;
+    blk += (long long)d.m_tiles * G.n_tiles;
+    row += M;
+    macs += (double)M * kFc1Out * nk * GBK;
+    ++G.n;
+  };
+  for (int g = 0; g < 9; ++g)
+    for (int s = 0; pr.cnt[g] > 0 && s < kFkSlabs; ++s)
+      add(kFkSeq[g] ? seq[kFkSeq[g] - 1] : x, pr.g_rows + pr.off[g], 25LL * kFkBlk[g] * 640 + (long long)s * kFkK / kFkSlabs,
+          g * kFkKb + s * kFkKb / kFkSlabs, kFkKb / kFkSlabs, pr.cnt[g]);
+  add(x, w_rows, 100LL * 640, 9 * kFkKb, kFkTailK / GBK, n);
+  EXPECTO_REQUIRE(G.n <= FCK_MAX && blk < (1LL << 31), "Karatsuba FC1 descriptors");
+  EXPECTO_REQUIRE(row <= (long long)std::max(h->fc_splits, kFkParts) * h->max_batch, "Karatsuba FC1 partial rows");
+  {
+    LayerTimer lt(h, 6, st);
+    if (h->profiling) {
+      if (!mask) {
+        h->macs[h->timer_base + 6] += macs;
+      } else {   // executed share of the masked descriptors, counted on the device (no sync)
+        for (int i = 0; i < G.n; ++i) {
+          const FcDesc& d = G.d[i];
+          int rc = count_desc_macs(h, d.mask, d.m_tiles, (double)d.M / d.m_tiles * kFc1Out * d.nk * GBK, st);
+          if (rc) return rc;
+        }
+      }
+    }
+    beluga_fc_h3k<0><<<dim3((unsigned)blk), dim3(512), 0, st>>>(G);
+    int rc = check_launch("beluga_fc_h3k");
+    if (rc) return rc;
+  }
+  LayerTimer lt(h, 7, st);
+  const long long count4 = (long long)n * (kHidLd / 4);
+  fk_reduce_h2<<<dim3((unsigned)((count4 + 255) / 256)), dim3(256), 0, st>>>(h->part, prow, count4, h->fc1b, h1, h->fk_cs,
+                                                                           exp2i(h->sx[6]), h->ovf);
+  return check_launch("fk_reduce_h2");
+}
+
+// A window of the segment path for the Karatsuba FC1: its conv6 block (segment - s0, pool2 phase) and
+// offset in conv6 rows (as seg_a_rows computes them); its role is its 25-row step mod 4 and its
+// group the windows of its block with the same group start off6 - 25 role.
+struct FkWin {
+  int w, blk, off6;
+};
+int fk_role_of(int off6) { return (off6 / 25) & 3; }
+FkWin fk_win(int w, const int* win_seg, const int* win_off, int s0, bool rc, int L, int n_ph, const int* ph_idx) {
+  const int o = rc ? L - kLen - win_off[w] : win_off[w];
+  const int q = o >> 2, p = q & 3;
+  return {w, (win_seg[w] - s0) * n_ph + ph_idx[p], (q - p) >> 2};
+}
+bool fk_same_group(const FkWin& a, const FkWin& b) {
+  return a.blk == b.blk && a.off6 - 25 * fk_role_of(a.off6) == b.off6 - 25 * fk_role_of(b.off6);
+}
+
+// Tables of windows ws[i0, i1) (whole groups, group order) for fk_fc1: per product the starts of
+// the groups that need it (element offsets into the block rows, T6 rows per block) and each
+// window's partial rows, in fk_fc1's descriptor order (products, slabs, then the tail).
+void fk_slice_tables(const std::vector<FkWin>& ws, int i0, int i1, int T6, std::vector<long long>& grows,
+                     FkProducts& pr, std::vector<int>& prow) {
+  const int n = i1 - i0;
+  std::vector<int> gi(n);
+  std::vector<long long> gst;
+  std::vector<unsigned> need;
+  for (int i = i0; i < i1; ++i) {
+    const FkWin& w = ws[i];
+    if (i == i0 || !fk_same_group(w, ws[i - 1])) {
+      gst.push_back(((long long)w.blk * T6 + w.off6 - 25 * fk_role_of(w.off6)) * 640);
+      need.push_back(0u);
+    }
+    gi[i - i0] = (int)gst.size() - 1;
+    for (int j = 0; j < 4; ++j) need.back() |= 1u << kFkRole[fk_role_of(w.off6)][j];
+  }
+  const int ng = (int)gst.size();
+  std::vector<int> ridx((size_t)9 * ng, -1);
+  grows.clear();
+  for (int g = 0; g < 9; ++g) {
+    pr.off[g] = (int)grows.size();
+    int c = 0;
+    for (int k = 0; k < ng; ++k)
+      if ((need[k] >> g) & 1u) {
+        ridx[(size_t)g * ng + k] = c++;
+        grows.push_back(gst[k]);
+      }
+    pr.cnt[g] = c;
+  }
+  int base[9][kFkSlabs] = {};
+  int row = 0;
+  for (int g = 0; g < 9; ++g)
+    for (int s = 0; pr.cnt[g] > 0 && s < kFkSlabs; ++s) {
+      base[g][s] = row;
+      row += pr.cnt[g];
+    }
+  prow.assign((size_t)n * kFkParts, 0);
+  for (int i = 0; i < n; ++i) {
+    const int role = fk_role_of(ws[i0 + i].off6);
+    for (int j = 0; j < 4; ++j) {
+      const int g = kFkRole[role][j];
+      for (int s = 0; s < kFkSlabs; ++s) prow[(size_t)i * kFkParts + kFkSlabs * j + s] = base[g][s] + ridx[(size_t)g * ng + gi[i]];
+    }
+    prow[(size_t)i * kFkParts + kFkParts - 1] = row + i;
+  }
+}
+
+// Karatsuba FC1 + FC2 of R windows whose conv6 rows are at act (106 rows per window), each alone in
+// the handle's per-window role; mask (alt, in place over the same R rows' ref partials): per
+// descriptor and M tile, see fk_window_mask.
+int fk_windows(expecto_beluga* h, const float* act, int R, float* y, hipStream_t st, const long long* c_rows,
+               const unsigned* mask = nullptr, int tiles = 0) {
+  int rc;
+  if ((rc = fk_tables(h)) || (rc = fk_sequences(h, act, R, 106, 106, nullptr, 1, st))) return rc;
+  fk_window_tables<<<dim3((R + 255) / 256), dim3(256), 0, st>>>(R, 106, h->fk_role, h->fk_grows, h->fk_wrows, h->fk_prow);
+  if ((rc = check_launch("fk_window_tables"))) return rc;
+  FkProducts pr{h->fk_grows, {}, {}};
+  for (int j = 0; j < 4; ++j) pr.cnt[kFkRole[h->fk_role][j]] = R;
+  if ((rc = fk_fc1(h, act, h->fk_seq, pr, h->fk_wrows, R, h->fk_prow, h->h1, st, mask, tiles))) return rc;
+  return run_fc2(h, h->h1, R, y, st, c_rows);
+}
+
 // Profiling: the executed MACs of an alt FC1 that runs only the masked split-K slabs of its
 // `tiles` M tiles (nb rows) go to the device counter of the fc1_delta slot.
 int count_slab_macs(expecto_beluga* h, const unsigned* mask, int tiles, long long nb, hipStream_t st) {
@@ -1883,6 +2307,20 @@ int count_slab_macs(expecto_beluga* h, const unsigned* mask, int tiles, long lon
   }
   const double per_bit = (double)nb * kFc1Out * kFc1In / ((double)tiles * h->fc_splits);
   slab_macs<<<dim3(1), dim3(64), 0, st>>>(mask, tiles, per_bit, h->macs_d + kNumLayers + 6);   // fc1_delta
+  return check_launch("slab_macs");
+}
+
+// Profiling: executed MACs of one masked descriptor of the grouped Karatsuba FC1 (set M-tile bits x
+// per_tile MACs) into the device counter of the current FC1 slot.
+int count_desc_macs(expecto_beluga* h, const unsigned* mask, int tiles, double per_tile, hipStream_t st) {
+  if (!h->macs_d) {
+    float* f = nullptr;
+    int rc = dalloc(h, &f, 4 * kNumLayers);
+    if (rc) return rc;
+    h->macs_d = reinterpret_cast<double*>(f);
+    EXPECTO_HIP_CHECK(hipMemsetAsync(h->macs_d, 0, 2 * kNumLayers * sizeof(double), st));
+  }
+  slab_macs<<<dim3(1), dim3(64), 0, st>>>(mask, tiles, per_tile, h->macs_d + h->timer_base + 6);
   return check_launch("slab_macs");
 }
 
@@ -1906,6 +2344,7 @@ int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long 
     if (rc) return rc;
     std::swap(src, dst);
   }
+  if (fk_use(h)) return fk_windows(h, src, nb, y, st, nullptr);   // FC1 as the block Karatsuba, role fk_role
   return run_fc(h, src, nullptr, nb, y, st);  // src = act5 (buffer Q), 106 x 640 rows per window
 }
 
@@ -2012,7 +2451,7 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
     h->win_cap = 0;
     for (int** b : {&h->win_seg_d, &h->win_off_d, &h->win_row_d, &h->alt_w_d, &h->copy_w_d})
       EXPECTO_HIP_CHECK(hipMalloc(b, n_win * sizeof(int)));
-    EXPECTO_HIP_CHECK(hipMalloc(&h->fc_perm_d, 2 * n_win * sizeof(int)));
+    EXPECTO_HIP_CHECK(hipMalloc(&h->fc_perm_d, 4 * n_win * sizeof(int)));   // per strand: FC order, alt order
     h->win_cap = n_win;
   }
   std::vector<int> alt_w, copy_w;
@@ -2087,6 +2526,42 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
           if (!is_alt[w]) out[k++] = w;
       }
     }
+    copies.push_back({h->fc_perm_d, fc_perm.data(), fc_perm.size() * sizeof(int)});
+  }
+  // FC1 as the block Karatsuba (f16x3): per strand and chunk the windows in group order (conv6
+  // block, group start, role), the FC order of every launch and (segment pairs) the alt windows in
+  // the same order; fc_perm_d holds [strand][n_win] FC orders, then [strand][n_win] alt orders
+  const bool fkm = fk_use(h);
+  std::vector<std::vector<FkWin>> fk_ref, fk_alt;   // [strand * chunks + chunk]
+  if (fkm) {
+    fc_perm.assign((size_t)4 * n_win, 0);
+    std::vector<char> is_alt(n_win, 0);
+    for (int w : alt_w) is_alt[w] = 1;
+    for (int sd = 0; sd < strands; ++sd) {
+      const bool rcs = (mode == EXPECTO_STRAND_RC) || sd == 1;
+      for (const auto& c : chunks) {
+        const int w0 = first[c.first], w1 = first[c.second];
+        std::vector<FkWin> ref, alt;
+        for (int w = w0; w < w1; ++w) {
+          const FkWin fw = fk_win(w, win_seg, win_off, c.first, rcs, L, n_ph, ph_idx);
+          ref.push_back(fw);
+          if (is_alt[w]) alt.push_back(fw);
+        }
+        auto before = [](const FkWin& a, const FkWin& b) {
+          const int ga = a.off6 - 25 * fk_role_of(a.off6), gb = b.off6 - 25 * fk_role_of(b.off6);
+          if (a.blk != b.blk) return a.blk < b.blk;
+          if (ga != gb) return ga < gb;
+          return a.off6 != b.off6 ? a.off6 < b.off6 : a.w < b.w;
+        };
+        std::sort(ref.begin(), ref.end(), before);
+        std::sort(alt.begin(), alt.end(), before);
+        for (size_t k = 0; k < ref.size(); ++k) fc_perm[(size_t)sd * n_win + w0 + k] = ref[k].w;
+        for (size_t k = 0; k < alt.size(); ++k) fc_perm[(size_t)(2 + sd) * n_win + w0 + k] = alt[k].w;
+        fk_ref.push_back(std::move(ref));
+        fk_alt.push_back(std::move(alt));
+      }
+    }
+    if (pr) copies.pop_back();   // the pair order above is replaced by the group order
     copies.push_back({h->fc_perm_d, fc_perm.data(), fc_perm.size() * sizeof(int)});
   }
   // the tables are caller-owned (and local) host memory: stage them through pinned memory
@@ -2220,7 +2695,66 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
         if ((rc = alt_gemm(4, n_ph, kDA[6], kDW[6], false, h->D0))) return rc;
         if (sa != st) EXPECTO_HIP_CHECK(hipEventRecord(h->pev[13], sa));   // all alt runs of the chunk
       }
-      if (nw > 0) {
+      if (nw > 0 && fkm) {
+        // FC1 as the block Karatsuba: the conv6 blocks' D1 / D2 / DD, then slices of whole window
+        // groups (<= max_batch windows) in group order: window starts and output rows (seg_a_rows),
+        // the slice's product and partial-row tables (host, staged), one grouped FC1 launch, FC2.
+        // Segment pairs: then the alt windows, over the alt conv6 blocks (Q), the same way.
+        const int4 phi = make_int4(ph_idx[0], ph_idx[1], ph_idx[2], ph_idx[3]);
+        const long long row_base = (long long)sd * strand_rows;
+        const size_t ci = (size_t)sd * chunks.size() + (size_t)(&chunk - chunks.data());
+        auto fk_run = [&](const std::vector<FkWin>& ws, const int* perm, const float* x, float* yout) -> int {
+          int r;
+          for (size_t i0 = 0; i0 < ws.size();) {
+            size_t i1 = i0;
+            while (i1 < ws.size()) {   // whole groups, <= max_batch windows
+              size_t j = i1 + 1;
+              while (j < ws.size() && fk_same_group(ws[j], ws[i1])) ++j;
+              if (j - i0 > (size_t)h->max_batch && i1 > i0) break;
+              i1 = j;
+            }
+            EXPECTO_REQUIRE(i1 - i0 <= (size_t)h->max_batch, "a Karatsuba FC1 window group exceeds max_batch");
+            const int fn = (int)(i1 - i0);
+            std::vector<long long> grows;
+            std::vector<int> prow;
+            FkProducts prd{h->fk_grows, {}, {}};
+            fk_slice_tables(ws, (int)i0, (int)i1, g.T6, grows, prd, prow);
+            if ((r = stage_copies(h, {{h->fk_grows, grows.data(), grows.size() * sizeof(long long)},
+                                      {h->fk_prow, prow.data(), prow.size() * sizeof(int)}}, st)))
+              return r;
+            seg_a_rows<<<dim3((fn + 255) / 256), dim3(256), 0, st>>>(
+                h->win_seg_d, h->win_off_d, win_row ? h->win_row_d : nullptr, perm + i0, 0, fn, s0, is_rc ? 1 : 0, L,
+                n_ph, phi, g.T6, row_base, h->a_rows, h->c_rows);
+            if ((r = check_launch("seg_a_rows")) || (r = fk_fc1(h, x, h->fk_seq, prd, h->a_rows, fn, h->fk_prow, h->h1, st)) ||
+                (r = run_fc2(h, h->h1, fn, yout, st, h->c_rows)))
+              return r;
+            i0 = i1;
+          }
+          return EXPECTO_OK;
+        };
+        if ((rc = fk_tables(h)) || (rc = fk_sequences(h, h->P, nb, g.T6, g.T6, nullptr, n_ph, st)) ||
+            (rc = fk_run(fk_ref[ci], h->fc_perm_d + (size_t)sd * n_win + w0, h->P, y)))
+          return rc;
+        if (pr) {
+          if (!fk_alt[ci].empty()) {
+            if ((rc = st_wait(h->pev[13]))) return rc;   // alt conv6 runs (and the Q reads of their patches)
+            seg_alt_blocks<<<dim3(kAltRows6, (unsigned)nb), dim3(64), 0, st>>>(h->P, h->D0, n_ph, g.T6, h->seg_tab,
+                                                                              640 * eb / 16, h->Q);
+            if ((rc = check_launch("seg_alt_blocks"))) return rc;
+            DeltaScope ds(h);
+            if ((rc = fk_sequences(h, h->Q, nb, g.T6, g.T6, h->seg_tab, n_ph, st)) ||
+                (rc = fk_run(fk_alt[ci], h->fc_perm_d + (size_t)(2 + sd) * n_win + w0, h->Q, pr->y_alt)))
+              return rc;
+          }
+          const int ic0 = (int)(std::lower_bound(copy_w.begin(), copy_w.end(), w0) - copy_w.begin());
+          const int ic1 = (int)(std::lower_bound(copy_w.begin(), copy_w.end(), w0 + nw) - copy_w.begin());
+          if (ic1 > ic0) {
+            copy_rows<<<dim3(ic1 - ic0), dim3(256), 0, st>>>(y, pr->y_alt, h->copy_w_d + ic0,
+                                                             win_row ? h->win_row_d : nullptr, row_base);
+            if ((rc = check_launch("copy_rows"))) return rc;
+          }
+        }
+      } else if (nw > 0) {
         const int4 phi = make_int4(ph_idx[0], ph_idx[1], ph_idx[2], ph_idx[3]);
         const long long row_base = (long long)sd * strand_rows;
         const int* widx = pr ? h->fc_perm_d + (size_t)sd * n_win + w0 : nullptr;   // FC row order
@@ -2389,9 +2923,20 @@ int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int
     float* act6 = src;   // ref conv6 rows; dprev = the alt runs' conv6 rows
     pair_rows<<<dim3((R + 255) / 256), dim3(256), 0, st>>>(h->c_rows, R, nv, v0, strand_stride);
     if ((rc = check_launch("pair_rows"))) return rc;
-    if ((rc = run_fc(h, act6, nullptr, R, y_ref, st, h->c_rows))) return rc;
+    const bool fk = fk_use(h);
+    if ((rc = fk ? fk_windows(h, act6, R, y_ref, st, h->c_rows) : run_fc(h, act6, nullptr, R, y_ref, st, h->c_rows)))
+      return rc;
     pair_patch_apply<<<dim3(R), dim3(256), 0, st>>>(dprev, act6, nv, v0, var_pos, 640 * eb / 16);
     if ((rc = check_launch("pair_patch_apply"))) return rc;
+    if (fk) {   // alt FC1: only the partials (product, slab, tail) the 20 changed conv6 rows reach, in place
+      const int tiles = (R + X6P_BM - 1) / X6P_BM;
+      EXPECTO_HIP_CHECK(hipMemsetAsync(h->fk_mask, 0, (size_t)kFkParts * tiles * sizeof(unsigned), st));
+      fk_window_mask<<<dim3((R + 255) / 256), dim3(256), 0, st>>>(var_pos, nv, v0, R, h->fk_role, tiles, h->fk_mask);
+      if ((rc = check_launch("fk_window_mask"))) return rc;
+      DeltaScope ds(h);
+      if ((rc = fk_windows(h, act6, R, y_alt, st, h->c_rows, h->fk_mask, tiles))) return rc;
+      continue;
+    }
     // alt FC1: only the split-K slabs the 20 changed conv6 rows touch (planes GEMMs)
     const unsigned* mask = nullptr;
     double frac = 1.0;
@@ -2425,6 +2970,10 @@ int f16_col_scales(expecto_beluga* h, hipStream_t st) {
     col_scales<<<dim3((np[g] + 255) / 256), dim3(256), 0, st>>>(h->swd[g], np[g], h->sx[g], h->cs[g]);
     int rc = check_launch("col_scales");
     if (rc) return rc;
+  }
+  if (h->fkw) {   // the Karatsuba FC1 weights: FC1's input scale, their own row exponents
+    col_scales<<<dim3((np[5] + 255) / 256), dim3(256), 0, st>>>(h->fk_sw, np[5], h->sx[5], h->fk_cs);
+    return check_launch("col_scales (FC1 Karatsuba)");
   }
   return EXPECTO_OK;
 }
@@ -2525,6 +3074,27 @@ int f16_prepare(expecto_beluga* h, hipStream_t st) {
     col_scales<<<dim3(2), dim3(256), 0, st>>>(reinterpret_cast<int*>(sw1), 320, 0, h->cs1);
     if ((rc = check_launch("conv1 planes"))) return rc;
   }
+  if (h->fk_on) {   // FC1 block Karatsuba: the 9 products' weights + the tail, fp64 sums rounded once,
+    const int np1 = npad_of(kFc1Out);   // one exponent per row over all of them (a shared column unscale)
+    float* wk = nullptr;
+    EXPECTO_HIP_CHECK(hipMalloc(&wk, (size_t)np1 * kFkKTotal * sizeof(float)));
+    float *swf = nullptr;
+    if ((rc = dalloc(h, &swf, np1)) || (rc = dalloc(h, &h->fk_cs, np1)) ||
+        (rc = dalloc(h, &h->fkw, (size_t)np1 * kFkKTotal))) {
+      (void)hipFree(wk);
+      return rc;
+    }
+    h->fk_sw = reinterpret_cast<int*>(swf);
+    const long long tot = (long long)np1 * kFkKTotal;
+    fk_weights<<<dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st>>>(h->fc1w, np1, wk);
+    row_scale_exp<<<dim3(np1), dim3(256), 0, st>>>(wk, (int)kFkKTotal, h->fk_sw);
+    split_planes_h2<<<dim3((unsigned)((tot / 4 + 255) / 256)), dim3(256), 0, st>>>(
+        wk, np1, (int)kFkKTotal, h->fk_sw, reinterpret_cast<_Float16*>(h->fkw));
+    rc = check_launch("FC1 Karatsuba weights");
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(wk);
+    if (rc) return rc;
+  }
   if ((rc = f16_calibrate(h, st))) return rc;
   h->f16_ready = true;
   return EXPECTO_OK;
@@ -2620,6 +3190,12 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   if (const char* e = getenv("EXPECTO_CONV2_TABLE")) h->kmer_on = atoi(e) != 0;   // conv2 on the MFMAs (parity, not bits)
   if (const char* e = getenv("EXPECTO_KMER_QUAD")) h->kmer_quad = atoi(e) != 0;    // pair tables only (parity, not bits)
   if (const char* e = getenv("EXPECTO_ONEHOT_CODES")) h->onehot_as_codes = atoi(e) != 0;   // parity, not bits
+  if (const char* e = getenv("EXPECTO_FC1_KARATSUBA")) h->fk_on = atoi(e) != 0;       // parity, not bits
+  if (const char* e = getenv("EXPECTO_FC1_ROLE")) {    // per-window forwards' Karatsuba role (tests)
+    const int v = atoi(e);
+    EXPECTO_REQUIRE(v >= 0 && v <= 3, "EXPECTO_FC1_ROLE must be 0..3");
+    h->fk_role = v;
+  }
   if (const char* e = getenv("EXPECTO_SEG_CHUNK_WINDOWS")) h->seg_chunk_windows = atoi(e);   // same bits either way
   if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)
     const int v = atoi(e);
@@ -2632,7 +3208,8 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   h->fc2_rows = h->fc2_splits == 1 ? 4 * max_batch : max_batch;
   if (const char* e = getenv("EXPECTO_FC2_ROWS"))
     if (h->fc2_splits == 1) h->fc2_rows = std::max(max_batch, atoi(e));
-  const size_t partf = (size_t)h->fc_splits * max_batch * kHidLd;
+  // split-K partial rows: FC1's slabs, or the Karatsuba FC1's <= kFkParts partial rows per window
+  const size_t partf = (size_t)std::max(h->fc_splits, kFkParts) * max_batch * kHidLd;
   const size_t h1_rows = (size_t)h->fc2_rows + (h->fc2_splits == 1 ? max_batch : 0);
   if ((rc = dalloc(h, &h->P, act_alloc(pf))) || (rc = dalloc(h, &h->Q, act_alloc(qf))) ||
       (rc = dalloc(h, &h->part, partf)) || (rc = dalloc(h, &h->h1, act_alloc(h1_rows * kHidLd))) ||
@@ -2665,6 +3242,8 @@ void expecto_beluga_destroy(expecto_beluga_t h) {
   if (h->seg_var_d) (void)hipFree(h->seg_var_d);
   if (h->win_off_d) (void)hipFree(h->win_off_d);
   if (h->win_row_d) (void)hipFree(h->win_row_d);
+  for (float* p : h->fk_seq)
+    if (p) (void)hipFree(p);
   for (void* p : h->allocs) (void)hipFree(p);
   for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->pev)
@@ -2686,6 +3265,13 @@ int expecto_beluga_conv2_table_active(expecto_beluga_t h, int* reason) {
   EXPECTO_REQUIRE(h != nullptr, "null handle");
   if (reason) *reason = h->kmer_state;
   return h->kmer ? 1 : 0;
+}
+
+int expecto_beluga_set_fc1_role(expecto_beluga_t h, int role) {
+  EXPECTO_REQUIRE(h != nullptr, "null handle");
+  EXPECTO_REQUIRE(role >= 0 && role <= 3, "FC1 role must be 0..3");
+  h->fk_role = role;
+  return EXPECTO_OK;
 }
 
 int expecto_beluga_forward_onehot(expecto_beluga_t h, const float* x, int n, float* y, void* stream) {

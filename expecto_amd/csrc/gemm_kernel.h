@@ -1023,45 +1023,19 @@ constexpr int FCW_STAGE = 2 * FCW_APLANE + 2 * FCW_BPLANE;   // 75,776 B
 constexpr int FCW_EROW = 176 * 4 + 16;                 // epilogue staging row stride (720 B)
 constexpr int FCW_EWAVE = 16 * FCW_EROW;               // 11,520 B per wave
 
-template <int LAYER, int EPI, int TM>
-__device__ __forceinline__ void gemm_fc_h3w_body(const GemmArgs& p, char* smem) {
-  static_assert(EPI == EPI_PARTIAL, "split-K partial slabs only");
+// One 256 x 336 split-K partial tile of the wide FC GEMM: A row m (< M) starts at element
+// (a_rows ? a_rows[m] + a_off : m * 32 * lda_kb) of A and is read for nk 32-deep K blocks from
+// K block kb0; Bb = the weight planes of column n0 at the same first K block (kb_total K blocks
+// per weight row); the fp32 partial row m goes to cbase + m * ldc (columns < n_store).  Shared by
+// beluga_fc_h3w (one split-K GEMM) and beluga_fc_h3k (a group of GEMMs in one launch): the same
+// pieces, products and k order per output.
+template <int TM>
+__device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_rows, long long a_off, long long lda_kb,
+                                            int kb0a, long long M, const char* Bb, int kb_total, int nk, float* cbase,
+                                            long long ldc, int n_store, long long m0, int n0, char* smem) {
   constexpr int ROW_KB = 128;
-  const unsigned nblk = gridDim.x, bid = blockIdx.x;
-  const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
-  const unsigned lin =
-      p.linear_order ? bid : (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
-  long long mt;
-  int nt, ks;
-  if (p.m_fastest == 3) {
-    const long long per_ks = p.m_tiles * p.n_tiles;
-    ks = (int)(lin / per_ks);
-    const long long r = lin - ks * per_ks;
-    const long long g = r / ((long long)p.m_group * p.n_tiles);
-    const int i = (int)(r - g * p.m_group * p.n_tiles);
-    const int gm = (int)min((long long)p.m_group, p.m_tiles - g * p.m_group);
-    nt = i / gm;
-    mt = g * p.m_group + i % gm;
-  } else if (p.m_fastest) {
-    mt = lin % p.m_tiles;
-    const long long rest = lin / p.m_tiles;
-    nt = (int)(rest % p.n_tiles);
-    ks = (int)(rest / p.n_tiles);
-  } else {
-    nt = (int)(lin % (unsigned)p.n_tiles);
-    const long long rest = lin / (unsigned)p.n_tiles;
-    mt = rest % p.m_tiles;
-    ks = (int)(rest / p.m_tiles);
-  }
-  if (p.ks_mask && !((p.ks_mask[mt] >> ks) & 1u)) return;   // slab unchanged: partials already in C
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const long long m0 = mt * X6P_BM;
-  const int n0 = nt * FCW_BN;
-  const int kb_total = (int)(p.ldb / GBK);
-  const int gs0 = ks * (p.kper / GBK);
-  const long long lda_kb = p.lda / GBK;
-  const int nk = p.kper / GBK;
   auto swz = [](int r) { return (-(r >> 2)) & 3; };
   // this wave's LDS-DMA pieces: A pieces P = wave + 8i (i < 4) of 32 (plane P & 1, rows
   // 16 (P >> 1) ..), B pieces Q = min(wave + 8j, 41) (j < 6) of 42 (plane Q / 21, cols 16 (Q % 21) ..)
@@ -1072,13 +1046,12 @@ __device__ __forceinline__ void gemm_fc_h3w_body(const GemmArgs& p, char* smem) 
     const int P = wave + 8 * i, g = P >> 1, pl = P & 1;
     const int r = 16 * g + (lane >> 2);
     long long m = m0 + r;
-    if (m > p.M - 1) m = p.M - 1;
-    const long long kb0 = (p.a_rows ? p.a_rows[m] / GBK : m * lda_kb) + gs0;
+    if (m > M - 1) m = M - 1;
+    const long long kb0 = (a_rows ? (a_rows[m] + a_off) / GBK : m * lda_kb) + kb0a;
     const int c = (lane & 3) ^ swz(r);
-    asrc[i] = (const char*)p.A + kb0 * ROW_KB + pl * 64 + 16 * c;
+    asrc[i] = (const char*)A + kb0 * ROW_KB + pl * 64 + 16 * c;
     adst[i] = (unsigned)(pl * FCW_APLANE + g * 1024);
   }
-  const char* Bb = (const char*)p.Bp + ((long long)n0 * kb_total + gs0) * ROW_KB;
   unsigned boff[6], bdst[6];
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
@@ -1168,7 +1141,6 @@ __device__ __forceinline__ void gemm_fc_h3w_body(const GemmArgs& p, char* smem) 
     asm volatile("" ::: "memory");
   }
   // split-K partial epilogue: 16-row x (176 | 160)-column passes through the wave's LDS area
-  float* const cbase = p.C + (long long)ks * p.split_stride;
   char* const lds = smem + wave * FCW_EWAVE;
 #pragma unroll
   for (int mb = 0; mb < 2; ++mb) {
@@ -1189,18 +1161,99 @@ __device__ __forceinline__ void gemm_fc_h3w_body(const GemmArgs& p, char* smem) 
         const int row = i / chunks, ch = i - row * chunks;
         const long long m = m0 + wave * 32 + mb * 16 + row;
         const int n = n0 + nb0 * 16 + 4 * ch;
-        if (m < p.M && n < p.n_store)
-          *(floatx4v*)(cbase + m * p.ldc + n) = *(const floatx4v*)(lds + row * FCW_EROW + ch * 16);
+        if (m < M && n < n_store)
+          *(floatx4v*)(cbase + m * ldc + n) = *(const floatx4v*)(lds + row * FCW_EROW + ch * 16);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
   }
 }
 
+template <int LAYER, int EPI, int TM>
+__device__ __forceinline__ void gemm_fc_h3w_body(const GemmArgs& p, char* smem) {
+  static_assert(EPI == EPI_PARTIAL, "split-K partial slabs only");
+  const unsigned nblk = gridDim.x, bid = blockIdx.x;
+  const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
+  const unsigned lin =
+      p.linear_order ? bid : (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  long long mt;
+  int nt, ks;
+  if (p.m_fastest == 3) {
+    const long long per_ks = p.m_tiles * p.n_tiles;
+    ks = (int)(lin / per_ks);
+    const long long r = lin - ks * per_ks;
+    const long long g = r / ((long long)p.m_group * p.n_tiles);
+    const int i = (int)(r - g * p.m_group * p.n_tiles);
+    const int gm = (int)min((long long)p.m_group, p.m_tiles - g * p.m_group);
+    nt = i / gm;
+    mt = g * p.m_group + i % gm;
+  } else if (p.m_fastest) {
+    mt = lin % p.m_tiles;
+    const long long rest = lin / p.m_tiles;
+    nt = (int)(rest % p.n_tiles);
+    ks = (int)(rest / p.n_tiles);
+  } else {
+    nt = (int)(lin % (unsigned)p.n_tiles);
+    const long long rest = lin / (unsigned)p.n_tiles;
+    mt = rest % p.m_tiles;
+    ks = (int)(rest / p.m_tiles);
+  }
+  if (p.ks_mask && !((p.ks_mask[mt] >> ks) & 1u)) return;   // slab unchanged: partials already in C
+  const long long m0 = mt * X6P_BM;
+  const int n0 = nt * FCW_BN;
+  const int kb_total = (int)(p.ldb / GBK);
+  const int gs0 = ks * (p.kper / GBK);
+  constexpr int ROW_KB = 128;
+  fc_h3w_tile<TM>(p.A, p.a_rows, 0, p.lda / GBK, gs0, p.M, (const char*)p.Bp + ((long long)n0 * kb_total + gs0) * ROW_KB,
+                  kb_total, p.kper / GBK, p.C + (long long)ks * p.split_stride, p.ldc, p.n_store, m0, n0, smem);
+}
+
 template <int LAYER, int EPI, int TM = 0>
 __global__ __launch_bounds__(512, 1) void beluga_fc_h3w(GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * FCW_STAGE];
   gemm_fc_h3w_body<LAYER, EPI, TM>(p, smem);
+}
+
+// ---- grouped wide FC GEMM: several split-K partial GEMMs in one launch ----------------------
+// FC1's block Karatsuba (beluga.hip, "FC1 as a block-Karatsuba convolution") runs up to 9
+// products x 2 K slabs + the tail per window group as separate GEMMs with their own A rows,
+// weight planes and partial rows; one launch over all of them fills the chip's rounds as one
+// GEMM would (the r04 probe ran them as 4 launches and lost most of the saving to part-filled
+// rounds).  Descriptor d covers launch blocks [blk0, blk0 + m_tiles * n_tiles), N tiles fastest
+// (the 6 N tiles of an M tile run together; an XCD's ~32 concurrent workgroups share ~5 M tiles'
+// weight tiles, as beluga_fc_h3w's N-fastest order).
+constexpr int FCK_MAX = 24;
+struct FcDesc {
+  const float* A;            // activation rows (f16x3 planes)
+  const long long* a_rows;   // element offset of each of the M rows
+  long long a_off;           // + this element offset (the product's block, the K slab)
+  const char* Bp;            // weight planes of column 0 at the first K block
+  float* C;                  // partial row m at C + m * ldc
+  const unsigned* mask;      // optional: mask[m_tile] & 1 = compute (else the partials stay)
+  int M, m_tiles, nk, blk0;
+};
+struct FcGroup {
+  FcDesc d[FCK_MAX];
+  int n, kb_total, n_tiles, n_store;
+  long long ldc;
+};
+
+template <int TM = 0>
+__global__ __launch_bounds__(512, 1) void beluga_fc_h3k(FcGroup g) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * FCW_STAGE];
+  const unsigned nblk = gridDim.x, bid = blockIdx.x;
+  const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
+  const int lin = (int)((xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3));
+  int k = 0;
+  while (k + 1 < g.n && lin >= g.d[k + 1].blk0) ++k;
+  const FcDesc& d = g.d[k];
+  const int r = lin - d.blk0;
+  const int nt = r % g.n_tiles, mt = r / g.n_tiles;
+  if (d.mask && !(d.mask[mt] & 1u)) return;
+  const int n0 = nt * FCW_BN;
+  constexpr int ROW_KB = 128;
+  fc_h3w_tile<TM>(d.A, d.a_rows, d.a_off, 0, 0, d.M, d.Bp + (long long)n0 * g.kb_total * ROW_KB, g.kb_total, d.nk, d.C,
+                  g.ldc, g.n_store, (long long)mt * X6P_BM, n0, smem);
 }
 
 // ---- f16x3 conv GEMM with the Toeplitz A tile staged once per channel chunk -------------

@@ -32,6 +32,23 @@ def shift_order(maxshift: int):
     return [0] + list(range(-200, -maxshift - 1, -200)) + list(range(200, maxshift + 1, 200))
 
 
+def fc1_role(offset: int, seg_len: int, rc: bool = False) -> int:
+    """Block-Karatsuba FC1 role of the window at bp `offset` of a segment of `seg_len` bp on the
+    segment path (include/expecto_hip.h expecto_beluga_set_fc1_role): its 25-conv6-row (400 bp)
+    step within its pool2-phase block, mod 4; on the rc strand the window's offset in the
+    reverse-complemented segment."""
+    o = seg_len - 2000 - offset if rc else offset
+    return ((o >> 4) // 25) % 4
+
+
+def sweep_roles(shifts) -> np.ndarray:
+    """[2 strands, S] FC1 roles of a variant sweep's windows on the segment path (segment layout of
+    VariantPipeline.prepare: window j at offset shifts[j] - min(shifts))."""
+    lo, hi = min(shifts), max(shifts)
+    L = 2000 + hi - lo
+    return np.array([[fc1_role(s - lo, L, rc) for s in shifts] for rc in (False, True)], np.int64)
+
+
 def _allele_code(a: str) -> int:
     c = int(_LUT[ord(a)]) if len(a) == 1 and ord(a) < 256 else 255
     if c == 255:

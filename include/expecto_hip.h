@@ -108,6 +108,15 @@ size_t expecto_beluga_device_bytes(expecto_beluga_t h);
  * EXPECTO_KMER_MAX_BYTES; the library then prints one line on stderr at creation). */
 int expecto_beluga_conv2_table_active(expecto_beluga_t h, int* reason);
 
+/* F16X3 computes FC1 (Beluga.py:43-44) as a block-Karatsuba convolution over 25-row blocks of the
+ * conv6 rows: 4 windows 400 bp apart in one pool2-phase block of a segment share 9 block products
+ * instead of 16 (DESIGN.md "FC1 as a block-Karatsuba convolution"; EXPECTO_FC1_KARATSUBA=0: the
+ * direct FC1).  A window's FC1 is a sum of products of its own rows fixed by its ROLE, its position
+ * in such a group: on the segment path (conv6 offset / 25) mod 4, every per-window forward (codes,
+ * one-hot, pairs) the handle's role, 0 by default.  A window computed in the same role gives the
+ * same bits on every path; other roles agree to the parity bar.  Sets the per-window role (0..3). */
+int expecto_beluga_set_fc1_role(expecto_beluga_t h, int role);
+
 /* y[n,2002] = Beluga.forward(x[n,4,1,2000]) (x contiguous fp32, any values).  When the handle
  * holds the k-mer tables, runs F16X3 or BF16X6, x is 16-byte aligned and every column of x is an
  * exact one-hot column (one 1.0f, three +0.0f) or all zeros, as encodeSeqs writes them

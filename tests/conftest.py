@@ -48,3 +48,30 @@ def assert_close(got, want, rtol=RTOL, atol=ATOL, what=""):
     assert not bad.any(), f"{what}: {bad.sum()} elements out of tolerance, max err {err.max():.3g}"
     if want.size and np.abs(want).max() > 0:
         assert err.max() / np.abs(want).max() <= rtol, f"{what}: max err ratio {err.max() / np.abs(want).max():.3g}"
+
+
+def run_in_roles(eng, fn):
+    """{role: fn()} with the engine's per-window forwards in each block-Karatsuba FC1 role 0..3
+    (include/expecto_hip.h expecto_beluga_set_fc1_role); the role is reset to 0 afterwards."""
+    ys = {}
+    try:
+        for r in range(4):
+            eng.set_fc1_role(r)
+            ys[r] = fn().clone()
+    finally:
+        eng.set_fc1_role(0)
+    return ys
+
+
+def sweep_in_roles(eng, fn, shifts):
+    """Per-window sweep predictions y[2 strands, 2 alleles, S, n, 2002] (fn() with rows="shift")
+    with window (strand, shift j) taken in the FC1 role the segment path gives it
+    (pipeline.sweep_roles): what the segment path must equal bit for bit."""
+    from expecto_amd.pipeline import sweep_roles
+    ys = run_in_roles(eng, fn)
+    roles = sweep_roles(shifts)
+    out = ys[0].clone()
+    for s in range(2):
+        for j in range(len(shifts)):
+            out[s, :, j] = ys[int(roles[s, j])][s, :, j]
+    return out

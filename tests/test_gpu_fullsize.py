@@ -10,6 +10,8 @@ import numpy as np
 import pytest
 import torch
 
+from conftest import sweep_in_roles
+
 pytestmark = pytest.mark.gpu
 
 
@@ -39,7 +41,8 @@ def test_configs2_full_size_properties():
     idx = np.sort(rng.choice(n, 48, replace=False))
     it = torch.from_numpy(idx).cuda()
     sub = VariantSet([vs.chrom[i] for i in idx], vs.pos[idx], [vs.ref[i] for i in idx], [vs.alt[i] for i in idx])
-    yw = VariantPipeline(eng, fa, dg, use_segments=False, use_pairs=False).predict(sub, shifts)
+    pw = VariantPipeline(eng, fa, dg, use_segments=False, use_pairs=False)
+    yw = sweep_in_roles(eng, lambda: pw.predict(sub, shifts), shifts)   # each window in its FC1 role
     assert torch.equal(yw, y.index_select(3, it))
     assert torch.equal(d.index_select(2, it), y[:, 1].index_select(2, it) - y[:, 0].index_select(2, it))
 

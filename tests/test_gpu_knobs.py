@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import assert_close
+from conftest import assert_close, sweep_in_roles
 
 pytestmark = pytest.mark.gpu
 
@@ -26,7 +26,8 @@ def _setup(n=12, shifts=None):
     return fa, DeviceGenome(fa), vs, shifts or list(range(-20000, 20000, 200))
 
 
-def _run(monkeypatch, env, fa, dg, vs, shifts, max_batch=2048, use_segments=True, use_pairs=True):
+def _run(monkeypatch, env, fa, dg, vs, shifts, max_batch=2048, use_segments=True, use_pairs=True, roles=False):
+    """roles: per-window runs with each window in the FC1 role the segment path gives it."""
     from expecto_amd import beluga
     from expecto_amd.pipeline import VariantPipeline
     for k, v in env.items():
@@ -35,7 +36,7 @@ def _run(monkeypatch, env, fa, dg, vs, shifts, max_batch=2048, use_segments=True
     for k in env:
         monkeypatch.delenv(k)
     pipe = VariantPipeline(eng, fa, dg, use_segments=use_segments, use_pairs=use_pairs)
-    y = pipe.predict(vs, shifts).clone()
+    y = sweep_in_roles(eng, lambda: pipe.predict(vs, shifts), shifts) if roles else pipe.predict(vs, shifts).clone()
     torch.cuda.synchronize()
     return y
 
@@ -57,7 +58,7 @@ def test_fc2_without_split_k(monkeypatch):
     shifts = [-800, -400, 0, 400, 800]
     base = _run(monkeypatch, {}, fa, dg, vs, shifts)
     seg = _run(monkeypatch, {"EXPECTO_FC2_SPLITS": "1"}, fa, dg, vs, shifts)
-    per_window = _run(monkeypatch, {"EXPECTO_FC2_SPLITS": "1"}, fa, dg, vs, shifts, use_segments=False)
+    per_window = _run(monkeypatch, {"EXPECTO_FC2_SPLITS": "1"}, fa, dg, vs, shifts, use_segments=False, roles=True)
     assert torch.equal(seg, per_window)
     assert_close(seg.cpu().numpy(), base.cpu().numpy(), what="FC2 split 1 vs split 7")
 
@@ -85,7 +86,7 @@ def test_conv2_table_paths_bitwise_and_parity(monkeypatch, use_segments, use_pai
     fa, dg, vs, _ = _setup(n=24)
     shifts = [-800, -400, 0, 400, 800]
     tab = _run(monkeypatch, {}, fa, dg, vs, shifts, use_segments=use_segments, use_pairs=use_pairs)
-    ref = _run(monkeypatch, {}, fa, dg, vs, shifts, use_segments=False, use_pairs=False)
+    ref = _run(monkeypatch, {}, fa, dg, vs, shifts, use_segments=False, use_pairs=False, roles=use_segments)
     assert torch.equal(tab, ref), f"max|diff| {float((tab - ref).abs().max())}"
     mfma = _run(monkeypatch, {"EXPECTO_CONV2_TABLE": "0"}, fa, dg, vs, shifts, use_segments=use_segments,
                 use_pairs=use_pairs)

@@ -6,7 +6,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, assert_close
+from conftest import GOLDEN, assert_close, run_in_roles, sweep_in_roles
 
 pytestmark = pytest.mark.gpu
 
@@ -117,7 +117,7 @@ def test_segment_path_is_bitwise_equal_to_per_window_variants(precision):
     dg = DeviceGenome(fa)
     full = VariantPipeline(eng, fa, dg, use_segments=False, use_pairs=False)
     for shifts in (shift_order(800), shift_order(200), [0, 400, -400]):
-        b = full.predict(vs, shifts)
+        b = sweep_in_roles(eng, lambda: full.predict(vs, shifts), shifts)   # each window in its FC1 role
         for pairs in (True, False):
             seg = VariantPipeline(eng, fa, dg, use_segments=True, use_pairs=pairs)
             ps = seg.prepare(vs, shifts)
@@ -227,9 +227,12 @@ def test_segment_pairs_alt_runs_are_bitwise_equal(precision, max_batch):
     yf = y.view(4 * S * n, 2002)
     eng.forward_segment_pairs(ref, L, q, alt_code, win_seg, win_off, win_row, yf[0:],
                               yf[S * n:], 2 * S * n)
+    from expecto_amd.pipeline import fc1_role
     for a, src in enumerate((ref, alt)):
         wins = torch.stack([src[:, o:o + 2000] for o in offs], 0).reshape(S * n, 2000).contiguous()  # row j*n + v
-        want = eng.forward_codes(wins, 2).view(2, S * n, 2002)
+        by_role = run_in_roles(eng, lambda: eng.forward_codes(wins, 2).view(2, S, n, 2002))
+        want = torch.stack([torch.stack([by_role[fc1_role(int(o), L, sd == 1)][sd, j] for j, o in enumerate(offs)])
+                            for sd in range(2)]).view(2, S * n, 2002)   # each window in its FC1 role
         d = (y[:, a] - want).abs().amax(-1).view(2, S, n).cpu().numpy()
         assert (d == 0).all(), f"allele {a}: strand x offset x variant max|diff| {d} (q={q}, offsets={offs})"
 
