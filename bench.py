@@ -83,6 +83,12 @@ def conv2_table_on(precision: str = "f16x3") -> bool:
     return precision in ("f16x3", "bf16x6") and os.environ.get("EXPECTO_CONV2_TABLE", "1") != "0"
 
 
+def fc1_karatsuba_on(precision: str = "f16x3") -> bool:
+    """FC1 as the block-Karatsuba convolution (the library default for f16x3; EXPECTO_FC1_KARATSUBA=0
+    runs the direct split-K FC1): 9 block products per 4 windows instead of 16 on the headline."""
+    return precision == "f16x3" and os.environ.get("EXPECTO_FC1_KARATSUBA", "1") != "0"
+
+
 # 200-window segment (41,800 bp): pooled conv2 rows per segment, and the k-mer gather's algorithmic
 # bytes per pooled row (4 conv2 rows x 2 quad-table rows of 320 fp32 read, 320 fp16 hi + lo planes
 # written; a conv2 half whose 11-mer holds an N reads 2 pair-table rows instead of 1)
@@ -117,6 +123,8 @@ def kernel_name(layer: str, precision: str, segments: bool = True) -> str:
     if precision == "bf16x6":
         return f"beluga_gemm_x6q<{l}, {e}, 0>"
     if precision == "f16x3":
+        if l == 7 and fc1_karatsuba_on(precision):
+            return "beluga_fc_h3k"                         # FC1 products + tail: one grouped launch
         if l in (7, 8):   # split-K FC GEMMs on 336-column tiles (beluga_fc_h3w)
             return f"beluga_fc_h3w<{l}, {e}, 0>"
         if layer == "conv2" and os.environ.get("EXPECTO_FUSE_CONV1", "1") != "0":
@@ -405,7 +413,8 @@ def profile_key(n=None, precision="f16x3"):
     """Workload key a committed rocprofv3 profile (profiles/<tag>/traffic.json) must carry for
     its PMC numbers to be attached to this bench line."""
     return {"workload": "sed200", "variants": N200 if n is None else n, "precision": precision,
-            "max_batch": MAX_BATCH, "genome": "repeat-rich"}
+            "max_batch": MAX_BATCH, "genome": "repeat-rich",
+            "fc1": "karatsuba" if fc1_karatsuba_on(precision) else "direct"}
 
 
 def pmc_traffic(key, kernel):

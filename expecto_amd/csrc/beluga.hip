@@ -853,13 +853,13 @@ __global__ void fk_weights(const float* __restrict__ w1, long long rows, float* 
 
 // The row sequences D1, D2, DD of f16x3 conv6 rows (x: blocks of `s` rows, the first T valid):
 // row r of a block gets D1 / D2 / DD where its last input row r + 25 / 50 / 75 is in [lo, hi).
-// Values from the stored planes (x = hi + lo), fp32 arithmetic in a fixed order, plain split (the
+// (gres: only the rows the block's groups read.)  Values from the stored planes (x = hi + lo), fp32 arithmetic in a fixed order, plain split (the
 // planes are consumed as stored), the overflow flag as any f16x3 store.  [lo, hi) = [0, T), or
 // with `tab` (segment pairs: the alt blocks seg_alt_blocks filled, n_ph blocks per segment) the
 // rows that alt block holds.  320 threads = 4 rows x 80 eight-channel pieces (16 B of hi + 16 B of lo).
 __global__ __launch_bounds__(320) void fk_seq_h2(const float* __restrict__ x, int T, int s, const int* __restrict__ tab,
-                                                 int n_ph, float* __restrict__ d1, float* __restrict__ d2,
-                                                 float* __restrict__ dd, int* __restrict__ ovf) {
+                                                 int n_ph, const int* __restrict__ gres, float* __restrict__ d1,
+                                                 float* __restrict__ d2, float* __restrict__ dd, int* __restrict__ ovf) {
   const int c8 = threadIdx.x % 80;
   const int rq = (T + 3) >> 2;   // 4-row groups per block; grid = blocks x rq (1-D)
   const long long blk = blockIdx.x / rq;
@@ -871,6 +871,16 @@ __global__ __launch_bounds__(320) void fk_seq_h2(const float* __restrict__ x, in
     hi = min(T, (q >> 4) + 106);
   }
   if (r < lo || r + 25 >= hi) return;
+  // gres (optional): the block's group starts are all = gres[blk] mod 100 (>= 0; -1: unknown; -2: the
+  // block has no windows), so
+  // the products read D1 only at group rows 50..99 and D2 at 25..49 and 75..99 (DD at all rows)
+  bool need1 = true, need2 = true;
+  if (gres && gres[blk] == -2) return;   // no window reads this block
+  if (gres && gres[blk] >= 0) {
+    const int rel = ((r - gres[blk]) % 100 + 100) % 100;
+    need1 = rel >= 50;
+    need2 = (rel >= 25 && rel < 50) || rel >= 75;
+  }
   constexpr long long rb = 640 * 4;   // bytes per row (20 groups of [32 hi | 32 lo] fp16)
   const int cofs = (c8 >> 2) * 128 + (c8 & 3) * 16;
   const long long o = (blk * s + r) * rb + cofs;
@@ -907,8 +917,8 @@ __global__ __launch_bounds__(320) void fk_seq_h2(const float* __restrict__ x, in
   float a[8], y[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) a[e] = v[0][e] - v[1][e];
-  put(d1, a);
-  if (nrow >= 3) {
+  if (need1) put(d1, a);
+  if (nrow >= 3 && need2) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) y[e] = v[0][e] - v[2][e];
     put(d2, y);
@@ -1494,6 +1504,13 @@ struct expecto_beluga {
   long long* fk_wrows = nullptr;
   int* fk_prow = nullptr;
   unsigned* fk_mask = nullptr;
+  int fk_slice = 24576;               //   windows per Karatsuba FC1 launch on the segment path (EXPECTO_FC1K_SLICE):
+  float* fk_part = nullptr;           //   its partial rows, FC1 output rows, window / output rows, block residues
+  float* fk_h1 = nullptr;
+  long long* fk_arows = nullptr;
+  long long* fk_crows = nullptr;
+  int* fk_gres = nullptr;
+  long long fk_gres_cap = 0;
   bool onehot_as_codes = true;        // forward_onehot: exact one-hot input through the k-mer gather (EXPECTO_ONEHOT_CODES)
   uint8_t* oh_codes = nullptr;        //   its codes, max_batch x 2000 (allocated on first use)
   int* oh_bad = nullptr;              //   its check flag
@@ -2087,24 +2104,42 @@ int count_desc_macs(expecto_beluga* h, const unsigned* mask, int tiles, double p
 
 // ---- FC1 block Karatsuba (f16x3): host side (kernels and algebra: "FC1 as a block-Karatsuba
 // convolution" above) ------------------------------------------------------------------------
-bool fk_use(const expecto_beluga* h) {
-  return h->fk_on && h->fkw && g_precision == EXPECTO_PRECISION_F16X3 && fc_wide_tiles(h);
+bool fk_use(const expecto_beluga* h) {   // (its grouped launch always runs the 336-column tile)
+  return h->fk_on && h->fkw && g_precision == EXPECTO_PRECISION_F16X3;
 }
 
 // Table buffers, allocated with the first Karatsuba FC1: group starts (9 lists of <= max_batch),
 // window starts, kFkParts partial rows per window, kFkParts x tiles alt-mask words.
+int fk_cap(const expecto_beluga* h) { return std::max(h->max_batch, h->fk_slice); }
+
 int fk_tables(expecto_beluga* h) {
   if (h->fk_grows) return EXPECTO_OK;
-  const size_t mb = h->max_batch, tiles = (mb + 255) / 256;
+  const size_t mb = h->max_batch, tiles = (mb + 255) / 256, cap = fk_cap(h);
   float *a = nullptr, *b = nullptr, *c = nullptr, *d = nullptr;
   int rc;
-  if ((rc = dalloc(h, &a, 2 * 9 * mb)) || (rc = dalloc(h, &b, 2 * mb)) || (rc = dalloc(h, &c, kFkParts * mb)) ||
+  if ((rc = dalloc(h, &a, 2 * 9 * cap)) || (rc = dalloc(h, &b, 2 * mb)) || (rc = dalloc(h, &c, kFkParts * cap)) ||
       (rc = dalloc(h, &d, kFkParts * tiles)))
     return rc;
   h->fk_grows = reinterpret_cast<long long*>(a);
   h->fk_wrows = reinterpret_cast<long long*>(b);
   h->fk_prow = reinterpret_cast<int*>(c);
   h->fk_mask = reinterpret_cast<unsigned*>(d);
+  return EXPECTO_OK;
+}
+
+// Segment-path FC1 launches of up to fk_cap windows (one launch per strand for the 200-window
+// workload's 19,200 windows: one round structure instead of three part-filled ones): partial rows,
+// FC1 output rows, window starts and output rows, allocated with the first segment call.
+int fk_seg_buffers(expecto_beluga* h) {
+  if (h->fk_part) return EXPECTO_OK;
+  const size_t cap = fk_cap(h);
+  float *a = nullptr, *b = nullptr;
+  int rc;
+  if ((rc = dalloc(h, &h->fk_part, (size_t)kFkParts * cap * kHidLd)) || (rc = dalloc(h, &h->fk_h1, act_alloc(cap * kHidLd))) ||
+      (rc = dalloc(h, &a, 2 * cap)) || (rc = dalloc(h, &b, 2 * cap)))
+    return rc;
+  h->fk_arows = reinterpret_cast<long long*>(a);
+  h->fk_crows = reinterpret_cast<long long*>(b);
   return EXPECTO_OK;
 }
 
@@ -2133,14 +2168,14 @@ int fk_seq_alloc(expecto_beluga* h, long long rows) {
 
 // D1 / D2 / DD of `blocks` blocks of T conv6 rows at a stride of s rows (tab: alt blocks, see fk_seq_h2)
 int fk_sequences(expecto_beluga* h, const float* x, long long blocks, int T, int s, const int* tab, int n_ph,
-                 hipStream_t st) {
+                 hipStream_t st, const int* gres = nullptr) {
   int rc;
   if ((rc = fk_seq_alloc(h, blocks * s))) return rc;
   LayerTimer lt(h, 7, st);   // the sequences are timed with the FC1 reduction (slot fc1_reduce)
   const long long nblk = blocks * ((T + 3) / 4);
   EXPECTO_REQUIRE(nblk > 0 && nblk < (1LL << 31), "FC1 sequence grid");
-  fk_seq_h2<<<dim3((unsigned)nblk), dim3(320), 0, st>>>(x, T, s, tab, n_ph, h->fk_seq[0], h->fk_seq[1], h->fk_seq[2],
-                                                       h->ovf);
+  fk_seq_h2<<<dim3((unsigned)nblk), dim3(320), 0, st>>>(x, T, s, tab, n_ph, gres, h->fk_seq[0], h->fk_seq[1],
+                                                       h->fk_seq[2], h->ovf);
   return check_launch("fk_seq_h2");
 }
 
@@ -2157,7 +2192,12 @@ struct FkProducts {
 // (the product X@3 and the tail), seq: their D1 / D2 / DD.  mask (alt, in place): descriptor d runs
 // only the M tiles with bit 0 of mask[d * tiles + tile] set.
 int fk_fc1(expecto_beluga* h, const float* x, float* const* seq, const FkProducts& pr, const long long* w_rows, int n,
-           const int* prow, float* h1, hipStream_t st, const unsigned* mask = nullptr, int tiles = 0) {
+           const int* prow, float* h1, hipStream_t st, const unsigned* mask = nullptr, int tiles = 0,
+           float* part = nullptr, long long part_cap = 0) {
+  if (!part) {
+    part = h->part;
+    part_cap = (long long)std::max(h->fc_splits, kFkParts) * h->max_batch;
+  }
   FcGroup G{};
   G.kb_total = kFkKbTotal;
   G.n_tiles = (kHidLd + FCW_BN - 1) / FCW_BN;
@@ -2173,7 +2213,7 @@ int fk_fc1(expecto_beluga* h, const float* x, float* const* seq, const FkProduct
     d.a_rows = ar;
     d.a_off = aoff;
     d.Bp = wb + (long long)kb0 * 128;
-    d.C = h->part + row * kHidLd;
+    d.C = part + row * kHidLd;
     d.mask = mask ? mask + (size_t)G.n * tiles : nullptr;
     d.M = M;
     d.m_tiles = (M + X6P_BM - 1) / X6P_BM;
@@ -2190,7 +2230,7 @@ int fk_fc1(expecto_beluga* h, const float* x, float* const* seq, const FkProduct
           g * kFkKb + s * kFkKb / kFkSlabs, kFkKb / kFkSlabs, pr.cnt[g]);
   add(x, w_rows, 100LL * 640, 9 * kFkKb, kFkTailK / GBK, n);
   EXPECTO_REQUIRE(G.n <= FCK_MAX && blk < (1LL << 31), "Karatsuba FC1 descriptors");
-  EXPECTO_REQUIRE(row <= (long long)std::max(h->fc_splits, kFkParts) * h->max_batch, "Karatsuba FC1 partial rows");
+  EXPECTO_REQUIRE(row <= part_cap, "Karatsuba FC1 partial rows");
   {
     LayerTimer lt(h, 6, st);
     if (h->profiling) {
@@ -2210,7 +2250,7 @@ int fk_fc1(expecto_beluga* h, const float* x, float* const* seq, const FkProduct
   }
   LayerTimer lt(h, 7, st);
   const long long count4 = (long long)n * (kHidLd / 4);
-  fk_reduce_h2<<<dim3((unsigned)((count4 + 255) / 256)), dim3(256), 0, st>>>(h->part, prow, count4, h->fc1b, h1, h->fk_cs,
+  fk_reduce_h2<<<dim3((unsigned)((count4 + 255) / 256)), dim3(256), 0, st>>>(part, prow, count4, h->fc1b, h1, h->fk_cs,
                                                                            exp2i(h->sx[6]), h->ovf);
   return check_launch("fk_reduce_h2");
 }
@@ -2703,17 +2743,18 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
         const int4 phi = make_int4(ph_idx[0], ph_idx[1], ph_idx[2], ph_idx[3]);
         const long long row_base = (long long)sd * strand_rows;
         const size_t ci = (size_t)sd * chunks.size() + (size_t)(&chunk - chunks.data());
+        const long long cap = fk_cap(h);
         auto fk_run = [&](const std::vector<FkWin>& ws, const int* perm, const float* x, float* yout) -> int {
           int r;
           for (size_t i0 = 0; i0 < ws.size();) {
             size_t i1 = i0;
-            while (i1 < ws.size()) {   // whole groups, <= max_batch windows
+            while (i1 < ws.size()) {   // whole groups, <= fk_cap windows
               size_t j = i1 + 1;
               while (j < ws.size() && fk_same_group(ws[j], ws[i1])) ++j;
-              if (j - i0 > (size_t)h->max_batch && i1 > i0) break;
+              if (j - i0 > (size_t)cap && i1 > i0) break;
               i1 = j;
             }
-            EXPECTO_REQUIRE(i1 - i0 <= (size_t)h->max_batch, "a Karatsuba FC1 window group exceeds max_batch");
+            EXPECTO_REQUIRE(i1 - i0 <= (size_t)cap, "a Karatsuba FC1 window group exceeds the FC1 slice");
             const int fn = (int)(i1 - i0);
             std::vector<long long> grows;
             std::vector<int> prow;
@@ -2724,15 +2765,37 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
               return r;
             seg_a_rows<<<dim3((fn + 255) / 256), dim3(256), 0, st>>>(
                 h->win_seg_d, h->win_off_d, win_row ? h->win_row_d : nullptr, perm + i0, 0, fn, s0, is_rc ? 1 : 0, L,
-                n_ph, phi, g.T6, row_base, h->a_rows, h->c_rows);
-            if ((r = check_launch("seg_a_rows")) || (r = fk_fc1(h, x, h->fk_seq, prd, h->a_rows, fn, h->fk_prow, h->h1, st)) ||
-                (r = run_fc2(h, h->h1, fn, yout, st, h->c_rows)))
+                n_ph, phi, g.T6, row_base, h->fk_arows, h->fk_crows);
+            if ((r = check_launch("seg_a_rows")) ||
+                (r = fk_fc1(h, x, h->fk_seq, prd, h->fk_arows, fn, h->fk_prow, h->fk_h1, st, nullptr, 0, h->fk_part,
+                            kFkParts * cap)))
               return r;
+            for (int r0 = 0; r0 < fn; r0 += h->max_batch)   // FC2 over its workspace's max_batch rows at a time
+              if ((r = run_fc2(h, h->fk_h1 + (long long)r0 * kHidLd, std::min(h->max_batch, fn - r0), yout, st,
+                               h->fk_crows + r0)))
+                return r;
             i0 = i1;
           }
           return EXPECTO_OK;
         };
-        if ((rc = fk_tables(h)) || (rc = fk_sequences(h, h->P, nb, g.T6, g.T6, nullptr, n_ph, st)) ||
+        // per conv6 block: its groups' start residue mod 100 (all equal on 200-bp sweeps), so the
+        // sequences are formed only on the rows the products read; -2: a block no window reads
+        std::vector<int> gres((size_t)nb, -2);
+        for (const FkWin& w : fk_ref[ci]) {
+          const int r = (w.off6 - 25 * fk_role_of(w.off6)) % 100;
+          int& e = gres[(size_t)w.blk];
+          e = e == -2 ? r : (e == r ? r : -1);
+        }
+        if (nb > h->fk_gres_cap) {
+          if (h->fk_gres) EXPECTO_HIP_CHECK(hipFree(h->fk_gres));
+          h->fk_gres = nullptr;
+          h->fk_gres_cap = 0;
+          EXPECTO_HIP_CHECK(hipMalloc(&h->fk_gres, (size_t)nb * sizeof(int)));
+          h->fk_gres_cap = nb;
+        }
+        if ((rc = stage_copies(h, {{h->fk_gres, gres.data(), gres.size() * sizeof(int)}}, st))) return rc;
+        if ((rc = fk_tables(h)) || (rc = fk_seg_buffers(h)) ||
+            (rc = fk_sequences(h, h->P, nb, g.T6, g.T6, nullptr, n_ph, st, h->fk_gres)) ||
             (rc = fk_run(fk_ref[ci], h->fc_perm_d + (size_t)sd * n_win + w0, h->P, y)))
           return rc;
         if (pr) {
@@ -2742,7 +2805,7 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
                                                                               640 * eb / 16, h->Q);
             if ((rc = check_launch("seg_alt_blocks"))) return rc;
             DeltaScope ds(h);
-            if ((rc = fk_sequences(h, h->Q, nb, g.T6, g.T6, h->seg_tab, n_ph, st)) ||
+            if ((rc = fk_sequences(h, h->Q, nb, g.T6, g.T6, h->seg_tab, n_ph, st, h->fk_gres)) ||
                 (rc = fk_run(fk_alt[ci], h->fc_perm_d + (size_t)(2 + sd) * n_win + w0, h->Q, pr->y_alt)))
               return rc;
           }
@@ -3191,6 +3254,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   if (const char* e = getenv("EXPECTO_KMER_QUAD")) h->kmer_quad = atoi(e) != 0;    // pair tables only (parity, not bits)
   if (const char* e = getenv("EXPECTO_ONEHOT_CODES")) h->onehot_as_codes = atoi(e) != 0;   // parity, not bits
   if (const char* e = getenv("EXPECTO_FC1_KARATSUBA")) h->fk_on = atoi(e) != 0;       // parity, not bits
+  if (const char* e = getenv("EXPECTO_FC1K_SLICE")) h->fk_slice = std::max(1, atoi(e));  // same bits either way
   if (const char* e = getenv("EXPECTO_FC1_ROLE")) {    // per-window forwards' Karatsuba role (tests)
     const int v = atoi(e);
     EXPECTO_REQUIRE(v >= 0 && v <= 3, "EXPECTO_FC1_ROLE must be 0..3");
@@ -3244,6 +3308,7 @@ void expecto_beluga_destroy(expecto_beluga_t h) {
   if (h->win_row_d) (void)hipFree(h->win_row_d);
   for (float* p : h->fk_seq)
     if (p) (void)hipFree(p);
+  if (h->fk_gres) (void)hipFree(h->fk_gres);
   for (void* p : h->allocs) (void)hipFree(p);
   for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->pev)

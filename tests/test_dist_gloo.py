@@ -1,4 +1,4 @@
-"""CPU, world_size 2 over gloo: variant sharding, the all-gather and the gather to rank 0 (dist.py)."""
+"""CPU, world_size 2 and 4 over gloo: variant sharding, the all-gather and the gather to rank 0 (dist.py)."""
 import os
 import socket
 
@@ -45,21 +45,23 @@ def _worker(rank, world, port, n_total, q):
     torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("n_total", [7, 2, 1])
-def test_gather_rows_world2(n_total):
+@pytest.mark.parametrize("world,n_total", [(2, 7), (2, 2), (2, 1), (4, 7), (4, 3)])
+def test_gather_rows(world, n_total):
+    """World 4 with 7 variants: shards of 2, 2, 2, 1 (gather_blocks_to pads unequal blocks); with 3,
+    one rank holds none (the 4-rank gather before the 8-rank one)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, n_total, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=120) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (r0, lo0, hi0, s0, ok0), (r1, lo1, hi1, s1, ok1) = res
-    assert (lo0, hi1) == (0, n_total) and hi0 == lo1
-    assert tuple(s0) == (2, 2, 3, n_total, 5) and ok0 and ok1
+    assert res[0][1] == 0 and res[-1][2] == n_total
+    assert all(res[i][2] == res[i + 1][1] for i in range(world - 1))
+    assert all(tuple(r[3]) == (2, 2, 3, n_total, 5) and r[4] for r in res)
 
 
 def test_shard_range_covers_everything():

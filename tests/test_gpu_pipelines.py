@@ -277,14 +277,16 @@ def test_second_stream_overlap_is_bitwise_equal(monkeypatch):
     assert torch.equal(out["0"][1], out["1"][1])
 
 
-def test_chromatin_cli_two_ranks_equals_one(workdir):
-    """The CLI sharded over 2 ranks (torch.distributed.run; gloo, both ranks on this one GPU:
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_chromatin_cli_two_ranks_equals_one(workdir, ranks):
+    """The CLI sharded over 2 or 4 ranks (torch.distributed.run; gloo, every rank on this one GPU:
     the 8-GPU RCCL run is the driver's) and streamed in batches of 2 variants (uneven last
     batches) writes the same files byte for byte as one rank in one batch, in both output modes:
     every rank writing its own rows into the files rank 0 created (default), and each batch
-    gathered to rank 0 which writes it.  Shards are contiguous variant ranges; only rank 0 writes
-    snps_hg19.vcf; no .part file is left.  One rank streaming 2-variant batches writes the same
-    bytes too."""
+    gathered to rank 0 which writes it (4 ranks: shards of 2, 2, 1, 1 variants, so
+    gather_blocks_to pads 4 unequal blocks).  Shards are contiguous variant
+    ranges; only rank 0 writes snps_hg19.vcf; no .part file is left.  One rank streaming 2-variant
+    batches writes the same bytes too."""
     import socket
     import subprocess
     import sys
@@ -305,9 +307,9 @@ def test_chromatin_cli_two_ranks_equals_one(workdir):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
         s.close()
-        two = workdir / f"out_2rank_{mode}"
+        two = workdir / f"out_{ranks}rank_{mode}"
         env = dict(os.environ, EXPECTO_DIST_BACKEND="gloo", EXPECTO_SHARE_GPUS="1")
-        r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+        r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
                             "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "expecto_amd.chromatin",
                             str(vcf), "--output_dir", str(two), "--variant-batch", "2", "--output-mode", mode] + common,
                            env=env, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
