@@ -23,7 +23,9 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <tuple>
 #include <string>
 #include <vector>
 
@@ -860,47 +862,38 @@ __global__ void fk_weights(const float* __restrict__ w1, long long rows, float* 
 __global__ __launch_bounds__(320) void fk_seq_h2(const float* __restrict__ x, int T, int s, const int* __restrict__ tab,
                                                  int n_ph, const int* __restrict__ gres, float* __restrict__ d1,
                                                  float* __restrict__ d2, float* __restrict__ dd, int* __restrict__ ovf) {
+  // a thread walks one residue class k of a block's rows (k, k + 25, k + 50, ...) for one
+  // eight-channel piece, holding x[r .. r + 75 step 25] in registers: every row is loaded once
+  // (workgroup: 4 residues x 80 pieces; 7 workgroups cover the 25 residues of a block)
   const int c8 = threadIdx.x % 80;
-  const int rq = (T + 3) >> 2;   // 4-row groups per block; grid = blocks x rq (1-D)
-  const long long blk = blockIdx.x / rq;
-  const int r = (int)(blockIdx.x - blk * rq) * 4 + threadIdx.x / 80;
+  const long long blk = blockIdx.x / 7;
+  const int k = (int)(blockIdx.x - blk * 7) * 4 + threadIdx.x / 80;
+  if (k >= 25) return;
   int lo = 0, hi = T;
   if (tab) {
     const int q = tab[(blk / n_ph) * kSegTab];
     lo = q >= 1999 ? (q - 1999) >> 4 : 0;
     hi = min(T, (q >> 4) + 106);
   }
-  if (r < lo || r + 25 >= hi) return;
   // gres (optional): the block's group starts are all = gres[blk] mod 100 (>= 0; -1: unknown; -2: the
-  // block has no windows), so
-  // the products read D1 only at group rows 50..99 and D2 at 25..49 and 75..99 (DD at all rows)
-  bool need1 = true, need2 = true;
-  if (gres && gres[blk] == -2) return;   // no window reads this block
-  if (gres && gres[blk] >= 0) {
-    const int rel = ((r - gres[blk]) % 100 + 100) % 100;
-    need1 = rel >= 50;
-    need2 = (rel >= 25 && rel < 50) || rel >= 75;
-  }
+  // block has no windows), so the products read D1 only at group rows 50..99 and D2 at 25..49 and
+  // 75..99 (DD at all rows)
+  const int g = gres ? gres[blk] : -1;
+  if (g == -2) return;
+  int r = k;
+  if (r < lo) r += (lo - r + 24) / 25 * 25;
+  if (r + 25 >= hi) return;
   constexpr long long rb = 640 * 4;   // bytes per row (20 groups of [32 hi | 32 lo] fp16)
-  const int cofs = (c8 >> 2) * 128 + (c8 & 3) * 16;
-  const long long o = (blk * s + r) * rb + cofs;
-  const char* src = reinterpret_cast<const char*>(x) + o;
-  float v[4][8];
-  const int nrow = r + 75 < hi ? 4 : r + 50 < hi ? 3 : 2;
+  const long long base = blk * s * rb + (c8 >> 2) * 128 + (c8 & 3) * 16;
+  auto ld = [&](int row, float (&v)[8]) {
+    const char* p = reinterpret_cast<const char*>(x) + base + row * rb;
+    const halfx8 h = *reinterpret_cast<const halfx8*>(p);
+    const halfx8 l = *reinterpret_cast<const halfx8*>(p + 64);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (j < nrow) {
-      const halfx8 h = *reinterpret_cast<const halfx8*>(src + j * 25 * rb);
-      const halfx8 l = *reinterpret_cast<const halfx8*>(src + j * 25 * rb + 64);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[j][e] = (float)h[e] + (float)l[e];
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[j][e] = 0.f;
-    }
-  }
+    for (int e = 0; e < 8; ++e) v[e] = (float)h[e] + (float)l[e];
+  };
   bool bad = false;
-  auto put = [&](float* dst, const float (&y)[8]) {
+  auto put = [&](float* dst, int row, const float (&y)[8]) {
     halfx8 h, l;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -910,23 +903,45 @@ __global__ __launch_bounds__(320) void fk_seq_h2(const float* __restrict__ x, in
       h[e] = a;
       l[e] = b;
     }
-    char* d = reinterpret_cast<char*>(dst) + o;
+    char* d = reinterpret_cast<char*>(dst) + base + row * rb;
     *reinterpret_cast<halfx8*>(d) = h;
     *reinterpret_cast<halfx8*>(d + 64) = l;
   };
-  float a[8], y[8];
+  float v0[8], v1[8], v2[8] = {}, v3[8] = {};
+  ld(r, v0);
+  ld(r + 25, v1);
+  if (r + 50 < hi) ld(r + 50, v2);
+  if (r + 75 < hi) ld(r + 75, v3);
+  for (; r + 25 < hi; r += 25) {
+    float nv[8] = {};
+    if (r + 100 < hi) ld(r + 100, nv);   // the next row of the walk, in flight while this one is stored
+    bool need1 = true, need2 = true;
+    if (g >= 0) {
+      const int rel = ((r - g) % 100 + 100) % 100;
+      need1 = rel >= 50;
+      need2 = (rel >= 25 && rel < 50) || rel >= 75;
+    }
+    float a[8], y[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) a[e] = v[0][e] - v[1][e];
-  if (need1) put(d1, a);
-  if (nrow >= 3 && need2) {
+    for (int e = 0; e < 8; ++e) a[e] = v0[e] - v1[e];
+    if (need1) put(d1, r, a);
+    if (r + 50 < hi && need2) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) y[e] = v[0][e] - v[2][e];
-    put(d2, y);
-  }
-  if (nrow == 4) {
+      for (int e = 0; e < 8; ++e) y[e] = v0[e] - v2[e];
+      put(d2, r, y);
+    }
+    if (r + 75 < hi) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) y[e] = a[e] - (v[2][e] - v[3][e]);
-    put(dd, y);
+      for (int e = 0; e < 8; ++e) y[e] = a[e] - (v2[e] - v3[e]);
+      put(dd, r, y);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v0[e] = v1[e];
+      v1[e] = v2[e];
+      v2[e] = v3[e];
+      v3[e] = nv[e];
+    }
   }
   if (bad) *ovf = 1;
 }
@@ -1006,6 +1021,42 @@ __global__ void fk_window_mask(const int* __restrict__ var_pos, int nv, int v0, 
     }
   }
   if (100 < r6e && 105 >= r6) atomicOr(mask + 8 * tiles + m / 256, 1u);
+}
+
+// Alt masks of the segment path's in-place alt FC1 (segment pairs): descriptor slot d of the ref
+// layout (product g, slab s: rows i < cnt are groups rgrp[off + i], each (block, start row) in ginfo;
+// the last slot: the tail over windows i < nw, (block, conv6 offset) in winfo) is recomputed for the
+// M tiles holding a row whose partial reads -- the product's rows with its sequence's lags, or the
+// tail's rows 100..105 -- meet its block's changed conv6 rows [r6, r6 + 20) (seg_delta_table).
+struct FkMaskDesc {
+  int n;
+  int g[18], s[18], off[18], cnt[18];
+  int nw;
+};
+__global__ void fk_seg_mask(FkMaskDesc md, const int* __restrict__ rgrp, const int* __restrict__ ginfo,
+                            const int* __restrict__ winfo, const int* __restrict__ tab, int n_ph, int4 ph_unused,
+                            int tiles, unsigned* __restrict__ mask) {
+  const int d = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  auto r6_of = [&](int blk) { return tab[(blk / n_ph) * kSegTab + 13 + blk % n_ph]; };
+  if (d == md.n) {   // the tail
+    if (i >= md.nw) return;
+    const int r6 = r6_of(winfo[2 * i]), o = winfo[2 * i + 1];
+    if (o + 100 < r6 + kDW[6] && o + 105 >= r6) atomicOr(mask + (size_t)d * tiles + i / 256, 1u);
+    return;
+  }
+  if (i >= md.cnt[d]) return;
+  const int g = md.g[d], s = md.s[d], k = rgrp[md.off[d] + i];
+  const int r6 = r6_of(ginfo[2 * k]), r6e = r6 + kDW[6];
+  const int base = ginfo[2 * k + 1] + 25 * kFkBlk[g];
+  const int i0 = base + (s * 8000) / 640, i1 = base + ((s + 1) * 8000 - 1) / 640;
+  const int sq = kFkSeq[g], nl = sq == 0 ? 1 : sq == 3 ? 4 : 2, lag1 = sq == 2 ? 50 : 25;
+  bool hit = false;
+  for (int l = 0; l < nl; ++l) {
+    const int lag = l == 0 ? 0 : (nl == 2 ? lag1 : 25 * l);
+    hit |= i0 + lag < r6e && i1 + lag >= r6;
+  }
+  if (hit) atomicOr(mask + (size_t)d * tiles + i / 256, 1u);
 }
 
 // ---- weight repacking (reference layouts -> kernel layouts) --------------------------
@@ -1494,7 +1545,7 @@ struct expecto_beluga {
   bool kmer_quad = true;              //   conv2 rows from the quad tables (EXPECTO_KMER_QUAD=0: pair tables only)
   int kmer_state = 1;                 //   0 held, 1 off (EXPECTO_CONV2_TABLE=0), 2 no room (conv2_table_active)
   bool fk_on = true;                  // f16x3 FC1 as a block-Karatsuba convolution (EXPECTO_FC1_KARATSUBA)
-  int fk_role = 0;                    //   role of per-window forwards (EXPECTO_FC1_ROLE, 0..3)
+  int fk_role = 0;                    //   role of per-window forwards (EXPECTO_FC1_ROLE, 0..3; 4 = direct FC1)
   float* fkw = nullptr;               //   the 9 products' + tail weight planes [npad][kFkKbTotal][2][32] fp16
   int* fk_sw = nullptr;               //   their per-row scale exponents
   float* fk_cs = nullptr;             //   column unscale 2^-(sx[5] + fk_sw[n])
@@ -1511,6 +1562,14 @@ struct expecto_beluga {
   long long* fk_crows = nullptr;
   int* fk_gres = nullptr;
   long long fk_gres_cap = 0;
+  float* fk_aseq[3] = {};             //   segment pairs' in-place alt FC1: the alt blocks' sequences, row groups
+  long long fk_aseq_rows = 0;
+  int* fk_rgrp = nullptr;             //   of the product rows, group / window (block, row), alt windows'
+  int* fk_ginfo = nullptr;            //   partial rows and order, masks
+  int* fk_winfo = nullptr;
+  int* fk_aprow = nullptr;
+  int* fk_aperm = nullptr;
+  unsigned* fk_smask = nullptr;
   bool onehot_as_codes = true;        // forward_onehot: exact one-hot input through the k-mer gather (EXPECTO_ONEHOT_CODES)
   uint8_t* oh_codes = nullptr;        //   its codes, max_batch x 2000 (allocated on first use)
   int* oh_bad = nullptr;              //   its check flag
@@ -2104,9 +2163,11 @@ int count_desc_macs(expecto_beluga* h, const unsigned* mask, int tiles, double p
 
 // ---- FC1 block Karatsuba (f16x3): host side (kernels and algebra: "FC1 as a block-Karatsuba
 // convolution" above) ------------------------------------------------------------------------
-bool fk_use(const expecto_beluga* h) {   // (its grouped launch always runs the 336-column tile)
-  return h->fk_on && h->fkw && g_precision == EXPECTO_PRECISION_F16X3;
+// (its grouped launch always runs the 336-column tile); per-window forwards: role 4 = the direct FC1
+bool fk_use(const expecto_beluga* h) {
+  return h->fk_on && h->fkw && g_precision == EXPECTO_PRECISION_F16X3 && h->fk_role < 4;
 }
+bool fk_use_seg(const expecto_beluga* h) { return h->fk_on && h->fkw && g_precision == EXPECTO_PRECISION_F16X3; }
 
 // Table buffers, allocated with the first Karatsuba FC1: group starts (9 lists of <= max_batch),
 // window starts, kFkParts partial rows per window, kFkParts x tiles alt-mask words.
@@ -2140,42 +2201,54 @@ int fk_seg_buffers(expecto_beluga* h) {
     return rc;
   h->fk_arows = reinterpret_cast<long long*>(a);
   h->fk_crows = reinterpret_cast<long long*>(b);
+  float *c = nullptr, *d = nullptr, *e = nullptr, *f = nullptr, *q = nullptr, *m = nullptr;
+  if ((rc = dalloc(h, &c, 9 * cap)) || (rc = dalloc(h, &d, 2 * cap)) || (rc = dalloc(h, &e, 2 * cap)) ||
+      (rc = dalloc(h, &f, kFkParts * cap)) || (rc = dalloc(h, &q, cap)) || (rc = dalloc(h, &m, 19 * (cap / 256 + 1))))
+    return rc;
+  h->fk_rgrp = reinterpret_cast<int*>(c);
+  h->fk_ginfo = reinterpret_cast<int*>(d);
+  h->fk_winfo = reinterpret_cast<int*>(e);
+  h->fk_aprow = reinterpret_cast<int*>(f);
+  h->fk_aperm = reinterpret_cast<int*>(q);
+  h->fk_smask = reinterpret_cast<unsigned*>(m);
   return EXPECTO_OK;
 }
 
 // The D1 / D2 / DD sequence buffers for `rows` conv6 rows (grown on demand; hipFree synchronises,
 // so they are sized once for the largest call).
-int fk_seq_alloc(expecto_beluga* h, long long rows) {
-  if (rows <= h->fk_seq_rows) return EXPECTO_OK;
-  for (float*& p : h->fk_seq)
-    if (p) {
-      EXPECTO_HIP_CHECK(hipFree(p));
-      p = nullptr;
+int fk_seq_alloc(expecto_beluga* h, long long rows, int set = 0) {
+  float** b = set ? h->fk_aseq : h->fk_seq;
+  long long& cap = set ? h->fk_aseq_rows : h->fk_seq_rows;
+  if (rows <= cap && b[0]) return EXPECTO_OK;
+  for (int i = 0; i < 3; ++i)
+    if (b[i]) {
+      EXPECTO_HIP_CHECK(hipFree(b[i]));
+      b[i] = nullptr;
     }
-  h->bytes -= (size_t)h->fk_seq_rows * 640 * 4 * 3;
-  h->fk_seq_rows = 0;
-  for (float*& p : h->fk_seq) {
-    hipError_t e = hipMalloc(&p, (size_t)rows * 640 * 4 + 16 * 640 * 4);
+  h->bytes -= (size_t)cap * 640 * 4 * 3;
+  cap = 0;
+  for (int i = 0; i < 3; ++i) {
+    hipError_t e = hipMalloc(&b[i], (size_t)rows * 640 * 4 + 16 * 640 * 4);
     if (e != hipSuccess) {
       set_error(std::string("hipMalloc (FC1 sequences): ") + hipGetErrorString(e));
       return EXPECTO_ENOMEM;
     }
   }
-  h->fk_seq_rows = rows;
+  cap = rows;
   h->bytes += (size_t)rows * 640 * 4 * 3;
   return EXPECTO_OK;
 }
 
 // D1 / D2 / DD of `blocks` blocks of T conv6 rows at a stride of s rows (tab: alt blocks, see fk_seq_h2)
 int fk_sequences(expecto_beluga* h, const float* x, long long blocks, int T, int s, const int* tab, int n_ph,
-                 hipStream_t st, const int* gres = nullptr) {
+                 hipStream_t st, const int* gres = nullptr, int set = 0) {
   int rc;
-  if ((rc = fk_seq_alloc(h, blocks * s))) return rc;
+  if ((rc = fk_seq_alloc(h, blocks * s, set))) return rc;
+  float* const* out = set ? h->fk_aseq : h->fk_seq;
   LayerTimer lt(h, 7, st);   // the sequences are timed with the FC1 reduction (slot fc1_reduce)
-  const long long nblk = blocks * ((T + 3) / 4);
+  const long long nblk = blocks * 7;   // 7 workgroups of 4 residue walks per block
   EXPECTO_REQUIRE(nblk > 0 && nblk < (1LL << 31), "FC1 sequence grid");
-  fk_seq_h2<<<dim3((unsigned)nblk), dim3(320), 0, st>>>(x, T, s, tab, n_ph, gres, h->fk_seq[0], h->fk_seq[1],
-                                                       h->fk_seq[2], h->ovf);
+  fk_seq_h2<<<dim3((unsigned)nblk), dim3(320), 0, st>>>(x, T, s, tab, n_ph, gres, out[0], out[1], out[2], h->ovf);
   return check_launch("fk_seq_h2");
 }
 
@@ -2184,7 +2257,17 @@ struct FkProducts {
   const long long* g_rows;
   int off[9];
   int cnt[9];
+  int lay[9];   // partial-row layout counts (0: cnt); an in-place alt launch runs cnt <= lay rows of the ref layout
 };
+
+// FC1 output rows of n windows from their kFkParts partial rows each (prow), fk_reduce_h2
+int fk_reduce(expecto_beluga* h, const float* part, const int* prow, int n, float* h1, hipStream_t st) {
+  LayerTimer lt(h, 7, st);
+  const long long count4 = (long long)n * (kHidLd / 4);
+  fk_reduce_h2<<<dim3((unsigned)((count4 + 255) / 256)), dim3(256), 0, st>>>(part, prow, count4, h->fc1b, h1, h->fk_cs,
+                                                                           exp2i(h->sx[6]), h->ovf);
+  return check_launch("fk_reduce_h2");
+}
 
 // One grouped launch of the Karatsuba FC1 over n windows: per product g with cnt[g] groups, its
 // kFkSlabs K slabs, then the tail over the windows (w_rows: window starts), as split-K partial rows
@@ -2206,29 +2289,39 @@ int fk_fc1(expecto_beluga* h, const float* x, float* const* seq, const FkProduct
   const char* wb = reinterpret_cast<const char*>(h->fkw);
   long long row = 0;
   long long blk = 0;
+  int mslot = 0;   // mask slot: descriptor order of the full layout (2 per product in use, then the tail)
   double macs = 0.0;
-  auto add = [&](const float* A, const long long* ar, long long aoff, int kb0, int nk, int M) {
+  auto add = [&](const float* A, const long long* ar, long long aoff, int kb0, int nk, int M, int lay) {
     FcDesc& d = G.d[G.n];
     d.A = A;
     d.a_rows = ar;
     d.a_off = aoff;
     d.Bp = wb + (long long)kb0 * 128;
     d.C = part + row * kHidLd;
-    d.mask = mask ? mask + (size_t)G.n * tiles : nullptr;
+    d.mask = mask ? mask + (size_t)mslot * tiles : nullptr;
+    ++mslot;
     d.M = M;
     d.m_tiles = (M + X6P_BM - 1) / X6P_BM;
     d.nk = nk;
     d.blk0 = (int)blk;
     blk += (long long)d.m_tiles * G.n_tiles;
-    row += M;
+    row += lay;
     macs += (double)M * kFc1Out * nk * GBK;
     ++G.n;
   };
-  for (int g = 0; g < 9; ++g)
-    for (int s = 0; pr.cnt[g] > 0 && s < kFkSlabs; ++s)
-      add(kFkSeq[g] ? seq[kFkSeq[g] - 1] : x, pr.g_rows + pr.off[g], 25LL * kFkBlk[g] * 640 + (long long)s * kFkK / kFkSlabs,
-          g * kFkKb + s * kFkKb / kFkSlabs, kFkKb / kFkSlabs, pr.cnt[g]);
-  add(x, w_rows, 100LL * 640, 9 * kFkKb, kFkTailK / GBK, n);
+  for (int g = 0; g < 9; ++g) {
+    const int lay = pr.lay[g] ? pr.lay[g] : pr.cnt[g];
+    for (int s = 0; lay > 0 && s < kFkSlabs; ++s) {
+      if (pr.cnt[g] > 0)
+        add(kFkSeq[g] ? seq[kFkSeq[g] - 1] : x, pr.g_rows + pr.off[g], 25LL * kFkBlk[g] * 640 + (long long)s * kFkK / kFkSlabs,
+            g * kFkKb + s * kFkKb / kFkSlabs, kFkKb / kFkSlabs, pr.cnt[g], lay);
+      else {
+        row += lay;   // (in-place alt launch: no alt group needs this product; keep the ref layout)
+        ++mslot;
+      }
+    }
+  }
+  add(x, w_rows, 100LL * 640, 9 * kFkKb, kFkTailK / GBK, n, n);
   EXPECTO_REQUIRE(G.n <= FCK_MAX && blk < (1LL << 31), "Karatsuba FC1 descriptors");
   EXPECTO_REQUIRE(row <= part_cap, "Karatsuba FC1 partial rows");
   {
@@ -2248,11 +2341,7 @@ int fk_fc1(expecto_beluga* h, const float* x, float* const* seq, const FkProduct
     int rc = check_launch("beluga_fc_h3k");
     if (rc) return rc;
   }
-  LayerTimer lt(h, 7, st);
-  const long long count4 = (long long)n * (kHidLd / 4);
-  fk_reduce_h2<<<dim3((unsigned)((count4 + 255) / 256)), dim3(256), 0, st>>>(part, prow, count4, h->fc1b, h1, h->fk_cs,
-                                                                           exp2i(h->sx[6]), h->ovf);
-  return check_launch("fk_reduce_h2");
+  return prow ? fk_reduce(h, part, prow, n, h1, st) : EXPECTO_OK;
 }
 
 // A window of the segment path for the Karatsuba FC1: its conv6 block (segment - s0, pool2 phase) and
@@ -2275,7 +2364,8 @@ bool fk_same_group(const FkWin& a, const FkWin& b) {
 // the groups that need it (element offsets into the block rows, T6 rows per block) and each
 // window's partial rows, in fk_fc1's descriptor order (products, slabs, then the tail).
 void fk_slice_tables(const std::vector<FkWin>& ws, int i0, int i1, int T6, std::vector<long long>& grows,
-                     FkProducts& pr, std::vector<int>& prow) {
+                     FkProducts& pr, std::vector<int>& prow, std::vector<int>* rgrp = nullptr,
+                     std::vector<int>* ginfo = nullptr) {
   const int n = i1 - i0;
   std::vector<int> gi(n);
   std::vector<long long> gst;
@@ -2288,10 +2378,15 @@ void fk_slice_tables(const std::vector<FkWin>& ws, int i0, int i1, int T6, std::
     }
     gi[i - i0] = (int)gst.size() - 1;
     for (int j = 0; j < 4; ++j) need.back() |= 1u << kFkRole[fk_role_of(w.off6)][j];
+    if (ginfo && gi[i - i0] * 2 == (int)ginfo->size()) {   // (block, start row) of a new group
+      ginfo->push_back(w.blk);
+      ginfo->push_back(w.off6 - 25 * fk_role_of(w.off6));
+    }
   }
   const int ng = (int)gst.size();
   std::vector<int> ridx((size_t)9 * ng, -1);
   grows.clear();
+  if (rgrp) rgrp->clear();
   for (int g = 0; g < 9; ++g) {
     pr.off[g] = (int)grows.size();
     int c = 0;
@@ -2299,8 +2394,10 @@ void fk_slice_tables(const std::vector<FkWin>& ws, int i0, int i1, int T6, std::
       if ((need[k] >> g) & 1u) {
         ridx[(size_t)g * ng + k] = c++;
         grows.push_back(gst[k]);
+        if (rgrp) rgrp->push_back(k);
       }
     pr.cnt[g] = c;
+    pr.lay[g] = 0;
   }
   int base[9][kFkSlabs] = {};
   int row = 0;
@@ -2329,7 +2426,7 @@ int fk_windows(expecto_beluga* h, const float* act, int R, float* y, hipStream_t
   if ((rc = fk_tables(h)) || (rc = fk_sequences(h, act, R, 106, 106, nullptr, 1, st))) return rc;
   fk_window_tables<<<dim3((R + 255) / 256), dim3(256), 0, st>>>(R, 106, h->fk_role, h->fk_grows, h->fk_wrows, h->fk_prow);
   if ((rc = check_launch("fk_window_tables"))) return rc;
-  FkProducts pr{h->fk_grows, {}, {}};
+  FkProducts pr{h->fk_grows, {}, {}, {}};
   for (int j = 0; j < 4; ++j) pr.cnt[kFkRole[h->fk_role][j]] = R;
   if ((rc = fk_fc1(h, act, h->fk_seq, pr, h->fk_wrows, R, h->fk_prow, h->h1, st, mask, tiles))) return rc;
   return run_fc2(h, h->h1, R, y, st, c_rows);
@@ -2571,33 +2668,60 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
   // FC1 as the block Karatsuba (f16x3): per strand and chunk the windows in group order (conv6
   // block, group start, role), the FC order of every launch and (segment pairs) the alt windows in
   // the same order; fc_perm_d holds [strand][n_win] FC orders, then [strand][n_win] alt orders
-  const bool fkm = fk_use(h);
+  // Segment pairs where more than a third of the windows hold the SNV (short sweeps: +-800, every
+  // window) run the direct FC1 (role 4): an alt window's Karatsuba products mix rows 25-75 apart, so
+  // nearly all of them reach the changed rows and the alt recompute outweighs the saving
+  // (configs[2]: 14.4 k vs 16.6 k variants/s); the 200-window sweeps (5 % alt windows) gain.
+  const bool fkm = fk_use_seg(h) && !(pr && 3 * alt_w.size() > (size_t)n_win);
   std::vector<std::vector<FkWin>> fk_ref, fk_alt;   // [strand * chunks + chunk]
+  std::vector<char> fk_is_alt(pr ? n_win : 0, 0);
+  for (int w : alt_w) fk_is_alt[w] = 1;
   if (fkm) {
     fc_perm.assign((size_t)4 * n_win, 0);
-    std::vector<char> is_alt(n_win, 0);
-    for (int w : alt_w) is_alt[w] = 1;
     for (int sd = 0; sd < strands; ++sd) {
       const bool rcs = (mode == EXPECTO_STRAND_RC) || sd == 1;
       for (const auto& c : chunks) {
         const int w0 = first[c.first], w1 = first[c.second];
+        // group order: (segment pairs) the groups holding an alt window first, ordered by where the
+        // SNV falls in the group (so an M tile of the in-place alt FC1 holds groups whose changed
+        // products are the same and its masks stay sparse), then every other group; in a group its
+        // windows by role
+        struct Key {
+          int cls;
+          long long rel;
+          int blk, G, off6, w;
+        };
         std::vector<FkWin> ref, alt;
+        std::vector<Key> key;
+        std::map<std::pair<int, int>, int> galt;   // (block, group start) -> holds an alt window
         for (int w = w0; w < w1; ++w) {
           const FkWin fw = fk_win(w, win_seg, win_off, c.first, rcs, L, n_ph, ph_idx);
           ref.push_back(fw);
-          if (is_alt[w]) alt.push_back(fw);
+          if (pr && fk_is_alt[w]) {
+            alt.push_back(fw);
+            galt[{fw.blk, fw.off6 - 25 * fk_role_of(fw.off6)}] = 1;
+          }
         }
-        auto before = [](const FkWin& a, const FkWin& b) {
-          const int ga = a.off6 - 25 * fk_role_of(a.off6), gb = b.off6 - 25 * fk_role_of(b.off6);
-          if (a.blk != b.blk) return a.blk < b.blk;
-          if (ga != gb) return ga < gb;
-          return a.off6 != b.off6 ? a.off6 < b.off6 : a.w < b.w;
-        };
-        std::sort(ref.begin(), ref.end(), before);
-        std::sort(alt.begin(), alt.end(), before);
-        for (size_t k = 0; k < ref.size(); ++k) fc_perm[(size_t)sd * n_win + w0 + k] = ref[k].w;
-        for (size_t k = 0; k < alt.size(); ++k) fc_perm[(size_t)(2 + sd) * n_win + w0 + k] = alt[k].w;
-        fk_ref.push_back(std::move(ref));
+        for (const FkWin& fw : ref) {
+          const int G = fw.off6 - 25 * fk_role_of(fw.off6);
+          const bool ga = pr && galt.count({fw.blk, G});
+          long long rel = 0;
+          if (ga) {
+            const int q = pr->var_pos[win_seg[fw.w]];
+            rel = (long long)(rcs ? L - 1 - q : q) - 16LL * G;
+          }
+          key.push_back({ga ? 0 : 1, rel, fw.blk, G, fw.off6, fw.w});
+        }
+        std::vector<int> ord(ref.size());
+        for (size_t k = 0; k < ord.size(); ++k) ord[k] = (int)k;
+        std::sort(ord.begin(), ord.end(), [&](int a, int b) {
+          const Key &x = key[a], &y = key[b];
+          return std::tie(x.cls, x.rel, x.blk, x.G, x.off6, x.w) < std::tie(y.cls, y.rel, y.blk, y.G, y.off6, y.w);
+        });
+        std::vector<FkWin> sorted;
+        for (int k : ord) sorted.push_back(ref[k]);
+        for (size_t k = 0; k < sorted.size(); ++k) fc_perm[(size_t)sd * n_win + w0 + k] = sorted[k].w;
+        fk_ref.push_back(std::move(sorted));
         fk_alt.push_back(std::move(alt));
       }
     }
@@ -2737,51 +2861,22 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
       }
       if (nw > 0 && fkm) {
         // FC1 as the block Karatsuba: the conv6 blocks' D1 / D2 / DD, then slices of whole window
-        // groups (<= max_batch windows) in group order: window starts and output rows (seg_a_rows),
+        // groups (<= fk_cap windows) in group order: window starts and output rows (seg_a_rows),
         // the slice's product and partial-row tables (host, staged), one grouped FC1 launch, FC2.
-        // Segment pairs: then the alt windows, over the alt conv6 blocks (Q), the same way.
+        // Segment pairs: the groups holding alt windows come first in the first slice; right after
+        // it, the alt FC1 runs IN PLACE over that slice's partial rows -- the alt blocks' sequences
+        // (Q), only the (product, slab, tail) partials the SNV's changed conv6 rows reach (masks per
+        // M tile), the ref partials for the rest -- and the alt windows' rows are reduced and FC2'd.
         const int4 phi = make_int4(ph_idx[0], ph_idx[1], ph_idx[2], ph_idx[3]);
         const long long row_base = (long long)sd * strand_rows;
         const size_t ci = (size_t)sd * chunks.size() + (size_t)(&chunk - chunks.data());
         const long long cap = fk_cap(h);
-        auto fk_run = [&](const std::vector<FkWin>& ws, const int* perm, const float* x, float* yout) -> int {
-          int r;
-          for (size_t i0 = 0; i0 < ws.size();) {
-            size_t i1 = i0;
-            while (i1 < ws.size()) {   // whole groups, <= fk_cap windows
-              size_t j = i1 + 1;
-              while (j < ws.size() && fk_same_group(ws[j], ws[i1])) ++j;
-              if (j - i0 > (size_t)cap && i1 > i0) break;
-              i1 = j;
-            }
-            EXPECTO_REQUIRE(i1 - i0 <= (size_t)cap, "a Karatsuba FC1 window group exceeds the FC1 slice");
-            const int fn = (int)(i1 - i0);
-            std::vector<long long> grows;
-            std::vector<int> prow;
-            FkProducts prd{h->fk_grows, {}, {}};
-            fk_slice_tables(ws, (int)i0, (int)i1, g.T6, grows, prd, prow);
-            if ((r = stage_copies(h, {{h->fk_grows, grows.data(), grows.size() * sizeof(long long)},
-                                      {h->fk_prow, prow.data(), prow.size() * sizeof(int)}}, st)))
-              return r;
-            seg_a_rows<<<dim3((fn + 255) / 256), dim3(256), 0, st>>>(
-                h->win_seg_d, h->win_off_d, win_row ? h->win_row_d : nullptr, perm + i0, 0, fn, s0, is_rc ? 1 : 0, L,
-                n_ph, phi, g.T6, row_base, h->fk_arows, h->fk_crows);
-            if ((r = check_launch("seg_a_rows")) ||
-                (r = fk_fc1(h, x, h->fk_seq, prd, h->fk_arows, fn, h->fk_prow, h->fk_h1, st, nullptr, 0, h->fk_part,
-                            kFkParts * cap)))
-              return r;
-            for (int r0 = 0; r0 < fn; r0 += h->max_batch)   // FC2 over its workspace's max_batch rows at a time
-              if ((r = run_fc2(h, h->fk_h1 + (long long)r0 * kHidLd, std::min(h->max_batch, fn - r0), yout, st,
-                               h->fk_crows + r0)))
-                return r;
-            i0 = i1;
-          }
-          return EXPECTO_OK;
-        };
+        const std::vector<FkWin>& ws = fk_ref[ci];
+        const int* perm = h->fc_perm_d + (size_t)sd * n_win + w0;
         // per conv6 block: its groups' start residue mod 100 (all equal on 200-bp sweeps), so the
         // sequences are formed only on the rows the products read; -2: a block no window reads
         std::vector<int> gres((size_t)nb, -2);
-        for (const FkWin& w : fk_ref[ci]) {
+        for (const FkWin& w : ws) {
           const int r = (w.off6 - 25 * fk_role_of(w.off6)) % 100;
           int& e = gres[(size_t)w.blk];
           e = e == -2 ? r : (e == r ? r : -1);
@@ -2793,22 +2888,123 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
           EXPECTO_HIP_CHECK(hipMalloc(&h->fk_gres, (size_t)nb * sizeof(int)));
           h->fk_gres_cap = nb;
         }
-        if ((rc = stage_copies(h, {{h->fk_gres, gres.data(), gres.size() * sizeof(int)}}, st))) return rc;
-        if ((rc = fk_tables(h)) || (rc = fk_seg_buffers(h)) ||
-            (rc = fk_sequences(h, h->P, nb, g.T6, g.T6, nullptr, n_ph, st, h->fk_gres)) ||
-            (rc = fk_run(fk_ref[ci], h->fc_perm_d + (size_t)sd * n_win + w0, h->P, y)))
+        if ((rc = stage_copies(h, {{h->fk_gres, gres.data(), gres.size() * sizeof(int)}}, st)) || (rc = fk_tables(h)) ||
+            (rc = fk_seg_buffers(h)) || (rc = fk_sequences(h, h->P, nb, g.T6, g.T6, nullptr, n_ph, st, h->fk_gres)))
           return rc;
-        if (pr) {
-          if (!fk_alt[ci].empty()) {
-            if ((rc = st_wait(h->pev[13]))) return rc;   // alt conv6 runs (and the Q reads of their patches)
-            seg_alt_blocks<<<dim3(kAltRows6, (unsigned)nb), dim3(64), 0, st>>>(h->P, h->D0, n_ph, g.T6, h->seg_tab,
-                                                                              640 * eb / 16, h->Q);
-            if ((rc = check_launch("seg_alt_blocks"))) return rc;
-            DeltaScope ds(h);
-            if ((rc = fk_sequences(h, h->Q, nb, g.T6, g.T6, h->seg_tab, n_ph, st, h->fk_gres)) ||
-                (rc = fk_run(fk_alt[ci], h->fc_perm_d + (size_t)(2 + sd) * n_win + w0, h->Q, pr->y_alt)))
-              return rc;
+        const bool has_alt = pr && !fk_alt[ci].empty();
+        bool alt_ready = false;   // alt conv6 blocks (Q) and their sequences formed (once per chunk)
+        for (size_t i0 = 0; i0 < ws.size();) {
+          size_t i1 = i0;
+          while (i1 < ws.size()) {   // whole groups, <= fk_cap windows
+            size_t j = i1 + 1;
+            while (j < ws.size() && fk_same_group(ws[j], ws[i1])) ++j;
+            if (j - i0 > (size_t)cap && i1 > i0) break;
+            i1 = j;
           }
+          EXPECTO_REQUIRE(i1 - i0 <= (size_t)cap, "a Karatsuba FC1 window group exceeds the FC1 slice");
+          const int fn = (int)(i1 - i0);
+          std::vector<long long> grows;
+          std::vector<int> prow, rgrp, ginfo;
+          FkProducts prd{h->fk_grows, {}, {}, {}};
+          fk_slice_tables(ws, (int)i0, (int)i1, g.T6, grows, prd, prow, &rgrp, &ginfo);
+          if ((rc = stage_copies(h, {{h->fk_grows, grows.data(), grows.size() * sizeof(long long)},
+                                     {h->fk_prow, prow.data(), prow.size() * sizeof(int)}}, st)))
+            return rc;
+          seg_a_rows<<<dim3((fn + 255) / 256), dim3(256), 0, st>>>(
+              h->win_seg_d, h->win_off_d, win_row ? h->win_row_d : nullptr, perm + i0, 0, fn, s0, is_rc ? 1 : 0, L,
+              n_ph, phi, g.T6, row_base, h->fk_arows, h->fk_crows);
+          if ((rc = check_launch("seg_a_rows")) ||
+              (rc = fk_fc1(h, h->P, h->fk_seq, prd, h->fk_arows, fn, h->fk_prow, h->fk_h1, st, nullptr, 0, h->fk_part,
+                           kFkParts * cap)))
+            return rc;
+          for (int r0 = 0; r0 < fn; r0 += h->max_batch)   // FC2 over its workspace's max_batch rows at a time
+            if ((rc = run_fc2(h, h->fk_h1 + (long long)r0 * kHidLd, std::min(h->max_batch, fn - r0), y, st,
+                              h->fk_crows + r0)))
+              return rc;
+          // the slice's first groups holding alt windows (the alt groups lead the chunk's order, so
+          // they fill the first slices) and their windows
+          int n_ag = 0;
+          size_t nw_pre = 0;
+          for (size_t i = i0; has_alt && i < i1; ++i) {
+            bool galt = false;
+            size_t j = i;
+            for (; j < i1 && fk_same_group(ws[j], ws[i]); ++j) galt |= fk_is_alt[ws[j].w] != 0;
+            if (!galt) break;
+            ++n_ag;
+            nw_pre = j - i0;
+            i = j - 1;
+          }
+          if (n_ag > 0) {
+            FkProducts pa = prd;   // the alt groups' prefix of every product list, in the ref layout
+            FkMaskDesc md{};
+            for (int gq = 0; gq < 9; ++gq) {
+              int c = 0;
+              for (int i = 0; i < prd.cnt[gq]; ++i)
+                if (rgrp[prd.off[gq] + i] < n_ag) ++c;
+              pa.cnt[gq] = c;
+              pa.lay[gq] = prd.cnt[gq];
+              for (int sb = 0; prd.cnt[gq] > 0 && sb < kFkSlabs; ++sb) {
+                md.g[md.n] = gq;
+                md.s[md.n] = sb;
+                md.off[md.n] = prd.off[gq];
+                md.cnt[md.n] = c;
+                ++md.n;
+              }
+            }
+            md.nw = (int)nw_pre;
+            std::vector<int> winfo, aperm, aprow;
+            for (size_t i = 0; i < nw_pre; ++i) {
+              winfo.push_back(ws[i0 + i].blk);
+              winfo.push_back(ws[i0 + i].off6);
+              if (fk_is_alt[ws[i0 + i].w]) {
+                aperm.push_back(ws[i0 + i].w);
+                aprow.insert(aprow.end(), prow.begin() + (long long)i * kFkParts, prow.begin() + (long long)(i + 1) * kFkParts);
+              }
+            }
+            const int na = (int)aperm.size();
+            const int tiles = (int)(cap / 256 + 1);
+            if ((rc = stage_copies(h, {{h->fk_rgrp, rgrp.data(), rgrp.size() * sizeof(int)},
+                                       {h->fk_ginfo, ginfo.data(), ginfo.size() * sizeof(int)},
+                                       {h->fk_winfo, winfo.data(), winfo.size() * sizeof(int)},
+                                       {h->fk_aperm, aperm.data(), aperm.size() * sizeof(int)},
+                                       {h->fk_aprow, aprow.data(), aprow.size() * sizeof(int)}}, st)))
+              return rc;
+            if (!alt_ready) {
+              if ((rc = st_wait(h->pev[13]))) return rc;   // alt conv6 runs (and the Q reads of their patches)
+              seg_alt_blocks<<<dim3(kAltRows6, (unsigned)nb), dim3(64), 0, st>>>(h->P, h->D0, n_ph, g.T6, h->seg_tab,
+                                                                                640 * eb / 16, h->Q);
+              if ((rc = check_launch("seg_alt_blocks"))) return rc;
+              DeltaScope ds(h);
+              if ((rc = fk_sequences(h, h->Q, nb, g.T6, g.T6, h->seg_tab, n_ph, st, h->fk_gres, 1))) return rc;
+              alt_ready = true;
+            }
+            EXPECTO_HIP_CHECK(hipMemsetAsync(h->fk_smask, 0, (size_t)(md.n + 1) * tiles * sizeof(unsigned), st));
+            int rows_max = md.nw;
+            for (int i = 0; i < md.n; ++i) rows_max = std::max(rows_max, md.cnt[i]);
+            if (rows_max > 0) {
+              fk_seg_mask<<<dim3((rows_max + 255) / 256, md.n + 1), dim3(256), 0, st>>>(
+                  md, h->fk_rgrp, h->fk_ginfo, h->fk_winfo, h->seg_tab, n_ph, make_int4(0, 0, 0, 0), tiles, h->fk_smask);
+              if ((rc = check_launch("fk_seg_mask"))) return rc;
+            }
+            DeltaScope ds(h);
+            if ((rc = fk_fc1(h, h->Q, h->fk_aseq, pa, h->fk_arows, (int)nw_pre, nullptr, h->fk_h1, st, h->fk_smask, tiles,
+                             h->fk_part, kFkParts * cap)) ||
+                (na > 0 && (rc = fk_reduce(h, h->fk_part, h->fk_aprow, na, h->fk_h1, st))))
+              return rc;
+            if (na > 0) {
+              seg_a_rows<<<dim3((na + 255) / 256), dim3(256), 0, st>>>(
+                  h->win_seg_d, h->win_off_d, win_row ? h->win_row_d : nullptr, h->fk_aperm, 0, na, s0, is_rc ? 1 : 0,
+                  L, n_ph, phi, g.T6, row_base, h->fk_arows, h->fk_crows);
+              if ((rc = check_launch("seg_a_rows"))) return rc;
+              for (int r0 = 0; r0 < na; r0 += h->max_batch)
+                if ((rc = run_fc2(h, h->fk_h1 + (long long)r0 * kHidLd, std::min(h->max_batch, na - r0), pr->y_alt, st,
+                                  h->fk_crows + r0)))
+                  return rc;
+            }
+          }
+          i0 = i1;
+        }
+        if (pr) {
           const int ic0 = (int)(std::lower_bound(copy_w.begin(), copy_w.end(), w0) - copy_w.begin());
           const int ic1 = (int)(std::lower_bound(copy_w.begin(), copy_w.end(), w0 + nw) - copy_w.begin());
           if (ic1 > ic0) {
@@ -3257,7 +3453,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   if (const char* e = getenv("EXPECTO_FC1K_SLICE")) h->fk_slice = std::max(1, atoi(e));  // same bits either way
   if (const char* e = getenv("EXPECTO_FC1_ROLE")) {    // per-window forwards' Karatsuba role (tests)
     const int v = atoi(e);
-    EXPECTO_REQUIRE(v >= 0 && v <= 3, "EXPECTO_FC1_ROLE must be 0..3");
+    EXPECTO_REQUIRE(v >= 0 && v <= 4, "EXPECTO_FC1_ROLE must be 0..4");
     h->fk_role = v;
   }
   if (const char* e = getenv("EXPECTO_SEG_CHUNK_WINDOWS")) h->seg_chunk_windows = atoi(e);   // same bits either way
@@ -3308,6 +3504,8 @@ void expecto_beluga_destroy(expecto_beluga_t h) {
   if (h->win_row_d) (void)hipFree(h->win_row_d);
   for (float* p : h->fk_seq)
     if (p) (void)hipFree(p);
+  for (float* p : h->fk_aseq)
+    if (p) (void)hipFree(p);
   if (h->fk_gres) (void)hipFree(h->fk_gres);
   for (void* p : h->allocs) (void)hipFree(p);
   for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
@@ -3334,7 +3532,7 @@ int expecto_beluga_conv2_table_active(expecto_beluga_t h, int* reason) {
 
 int expecto_beluga_set_fc1_role(expecto_beluga_t h, int role) {
   EXPECTO_REQUIRE(h != nullptr, "null handle");
-  EXPECTO_REQUIRE(role >= 0 && role <= 3, "FC1 role must be 0..3");
+  EXPECTO_REQUIRE(role >= 0 && role <= 4, "FC1 role must be 0..4");
   h->fk_role = role;
   return EXPECTO_OK;
 }

@@ -41,11 +41,15 @@ def fc1_role(offset: int, seg_len: int, rc: bool = False) -> int:
     return ((o >> 4) // 25) % 4
 
 
-def sweep_roles(shifts) -> np.ndarray:
+def sweep_roles(shifts, pairs: bool = True) -> np.ndarray:
     """[2 strands, S] FC1 roles of a variant sweep's windows on the segment path (segment layout of
-    VariantPipeline.prepare: window j at offset shifts[j] - min(shifts))."""
+    VariantPipeline.prepare: window j at offset shifts[j] - min(shifts)).  Segment pairs in which
+    more than a third of the windows hold the SNV (shift in (-1001, 999]) run the direct FC1: role 4
+    for every window (include/expecto_hip.h expecto_beluga_set_fc1_role)."""
     lo, hi = min(shifts), max(shifts)
     L = 2000 + hi - lo
+    if pairs and 3 * sum(1 for s in shifts if -1001 < s <= 999) > len(shifts):
+        return np.full((2, len(shifts)), 4, np.int64)
     return np.array([[fc1_role(s - lo, L, rc) for s in shifts] for rc in (False, True)], np.int64)
 
 

@@ -113,8 +113,10 @@ int expecto_beluga_conv2_table_active(expecto_beluga_t h, int* reason);
  * instead of 16 (DESIGN.md "FC1 as a block-Karatsuba convolution"; EXPECTO_FC1_KARATSUBA=0: the
  * direct FC1).  A window's FC1 is a sum of products of its own rows fixed by its ROLE, its position
  * in such a group: on the segment path (conv6 offset / 25) mod 4, every per-window forward (codes,
- * one-hot, pairs) the handle's role, 0 by default.  A window computed in the same role gives the
- * same bits on every path; other roles agree to the parity bar.  Sets the per-window role (0..3). */
+ * one-hot, pairs) the handle's role, 0 by default.  Role 4 is the direct FC1: segment-pair calls in
+ * which more than a third of the windows hold the SNV run it for every window (their alt windows
+ * would recompute nearly every product).  A window computed in the same role gives the same bits
+ * on every path; other roles agree to the parity bar.  Sets the per-window role (0..4). */
 int expecto_beluga_set_fc1_role(expecto_beluga_t h, int role);
 
 /* y[n,2002] = Beluga.forward(x[n,4,1,2000]) (x contiguous fp32, any values).  When the handle

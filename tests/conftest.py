@@ -51,11 +51,11 @@ def assert_close(got, want, rtol=RTOL, atol=ATOL, what=""):
 
 
 def run_in_roles(eng, fn):
-    """{role: fn()} with the engine's per-window forwards in each block-Karatsuba FC1 role 0..3
-    (include/expecto_hip.h expecto_beluga_set_fc1_role); the role is reset to 0 afterwards."""
+    """{role: fn()} with the engine's per-window forwards in each block-Karatsuba FC1 role 0..3 and
+    the direct FC1 (role 4; include/expecto_hip.h expecto_beluga_set_fc1_role); reset to 0 after."""
     ys = {}
     try:
-        for r in range(4):
+        for r in range(5):
             eng.set_fc1_role(r)
             ys[r] = fn().clone()
     finally:
@@ -63,13 +63,13 @@ def run_in_roles(eng, fn):
     return ys
 
 
-def sweep_in_roles(eng, fn, shifts):
+def sweep_in_roles(eng, fn, shifts, pairs=True):
     """Per-window sweep predictions y[2 strands, 2 alleles, S, n, 2002] (fn() with rows="shift")
-    with window (strand, shift j) taken in the FC1 role the segment path gives it
-    (pipeline.sweep_roles): what the segment path must equal bit for bit."""
+    with window (strand, shift j) taken in the FC1 role the segment path (segment pairs if `pairs`)
+    gives it (pipeline.sweep_roles): what the segment path must equal bit for bit."""
     from expecto_amd.pipeline import sweep_roles
     ys = run_in_roles(eng, fn)
-    roles = sweep_roles(shifts)
+    roles = sweep_roles(shifts, pairs)
     out = ys[0].clone()
     for s in range(2):
         for j in range(len(shifts)):

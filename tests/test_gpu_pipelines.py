@@ -117,8 +117,8 @@ def test_segment_path_is_bitwise_equal_to_per_window_variants(precision):
     dg = DeviceGenome(fa)
     full = VariantPipeline(eng, fa, dg, use_segments=False, use_pairs=False)
     for shifts in (shift_order(800), shift_order(200), [0, 400, -400]):
-        b = sweep_in_roles(eng, lambda: full.predict(vs, shifts), shifts)   # each window in its FC1 role
         for pairs in (True, False):
+            b = sweep_in_roles(eng, lambda: full.predict(vs, shifts), shifts, pairs)   # each window in its FC1 role
             seg = VariantPipeline(eng, fa, dg, use_segments=True, use_pairs=pairs)
             ps = seg.prepare(vs, shifts)
             assert ps["seg"] is not None and ps["seg"]["pairs"] == pairs
@@ -231,8 +231,11 @@ def test_segment_pairs_alt_runs_are_bitwise_equal(precision, max_batch):
     for a, src in enumerate((ref, alt)):
         wins = torch.stack([src[:, o:o + 2000] for o in offs], 0).reshape(S * n, 2000).contiguous()  # row j*n + v
         by_role = run_in_roles(eng, lambda: eng.forward_codes(wins, 2).view(2, S, n, 2002))
-        want = torch.stack([torch.stack([by_role[fc1_role(int(o), L, sd == 1)][sd, j] for j, o in enumerate(offs)])
-                            for sd in range(2)]).view(2, S * n, 2002)   # each window in its FC1 role
+        # each window in its FC1 role; the direct FC1 (role 4) when > 1/3 of the windows hold the SNV
+        n_alt = int(sum(((o <= q) & (q < o + 2000)).sum() for o in offs))
+        role = (lambda o, sd: 4) if 3 * n_alt > S * n else (lambda o, sd: fc1_role(int(o), L, sd == 1))
+        want = torch.stack([torch.stack([by_role[role(o, sd)][sd, j] for j, o in enumerate(offs)])
+                            for sd in range(2)]).view(2, S * n, 2002)
         d = (y[:, a] - want).abs().amax(-1).view(2, S, n).cpu().numpy()
         assert (d == 0).all(), f"allele {a}: strand x offset x variant max|diff| {d} (q={q}, offsets={offs})"
 
