@@ -83,6 +83,12 @@ def conv2_table_on(precision: str = "f16x3") -> bool:
     return precision in ("f16x3", "bf16x6") and os.environ.get("EXPECTO_CONV2_TABLE", "1") != "0"
 
 
+def conv_karatsuba_on(precision: str = "f16x3") -> bool:
+    """conv3 / conv4 as pair Karatsuba GEMMs (f16x3, opt-in EXPECTO_CONV_KARATSUBA=1; the default runs
+    them direct): 13 instead of 16 K blocks per output pair (beluga_conv_h3k)."""
+    return precision == "f16x3" and os.environ.get("EXPECTO_CONV_KARATSUBA", "0") == "1"
+
+
 def fc1_karatsuba_on(precision: str = "f16x3") -> bool:
     """FC1 as the block-Karatsuba convolution (the library default for f16x3; EXPECTO_FC1_KARATSUBA=0
     runs the direct split-K FC1): 9 block products per 4 windows instead of 16 on the headline."""
@@ -127,6 +133,8 @@ def kernel_name(layer: str, precision: str, segments: bool = True) -> str:
             return "beluga_fc_h3k"                         # FC1 products + tail: one grouped launch
         if l in (7, 8):   # split-K FC GEMMs on 336-column tiles (beluga_fc_h3w)
             return f"beluga_fc_h3w<{l}, {e}, 0>"
+        if layer in ("conv3", "conv4") and conv_karatsuba_on(precision):
+            return f"beluga_conv_h3k<{l}, {e}>"             # pair Karatsuba, 128-pair x 160 tiles
         if layer == "conv2" and os.environ.get("EXPECTO_FUSE_CONV1", "1") != "0":
             return f"beluga_conv_h3p<{l}, {e}, 16640, 4>"   # conv1 fused into the producers (256 | 16384)
         return f"beluga_conv_h3p<{l}, {e}, 256, 4>"   # producer / consumer 256-row tiles (every conv layer)
@@ -414,7 +422,8 @@ def profile_key(n=None, precision="f16x3"):
     its PMC numbers to be attached to this bench line."""
     return {"workload": "sed200", "variants": N200 if n is None else n, "precision": precision,
             "max_batch": MAX_BATCH, "genome": "repeat-rich",
-            "fc1": "karatsuba" if fc1_karatsuba_on(precision) else "direct"}
+            "fc1": "karatsuba" if fc1_karatsuba_on(precision) else "direct",
+            **({"conv34": "karatsuba"} if conv_karatsuba_on(precision) else {})}
 
 
 def pmc_traffic(key, kernel):

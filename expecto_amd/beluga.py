@@ -79,6 +79,12 @@ class BelugaEngine:
         in role r bit for bit (pipeline.fc1_role gives a segment window's role)."""
         _lib.check(self.lib.expecto_beluga_set_fc1_role(self.handle, int(role)), "set_fc1_role")
 
+    def set_conv_role(self, role: int):
+        """conv3 / conv4 form of this engine's per-window forwards (include/expecto_hip.h
+        expecto_beluga_set_conv_role): 0 pair Karatsuba (default), 1 direct.  A forward_segments
+        call equals per-window forwards in role pipeline.conv_role(...) bit for bit."""
+        _lib.check(self.lib.expecto_beluga_set_conv_role(self.handle, int(role)), "set_conv_role")
+
     def set_f16_target(self, target_log2: int):
         """f16x3 calibration target: the largest calibration activation maps to 2^target_log2."""
         with torch.cuda.device(self.device):

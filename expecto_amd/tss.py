@@ -322,7 +322,8 @@ def replicate_run(args):
     loop_s = time.perf_counter() - t0
     REPLICATE_LAST.clear()
     REPLICATE_LAST.update(loop_s=loop_s, setup_s=t0 - t_start, total_s=time.perf_counter() - t_start, setup=setup,
-                          genes=len(mine), batches=nb, gene_batch=B, rank=rank, world=world, **tm)
+                          genes=len(mine), batches=nb, gene_batch=B, rank=rank, world=world,
+                          conv2_table=dict(zip(("active", "state"), eng.conv2_table_state())), **tm)
     return dict(REPLICATE_LAST)
 
 

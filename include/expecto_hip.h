@@ -119,6 +119,17 @@ int expecto_beluga_conv2_table_active(expecto_beluga_t h, int* reason);
  * on every path; other roles agree to the parity bar.  Sets the per-window role (0..4). */
 int expecto_beluga_set_fc1_role(expecto_beluga_t h, int role);
 
+/* With EXPECTO_CONV_KARATSUBA=1 at handle creation (opt-in: measured slower than the direct kernel,
+ * DESIGN.md "conv3 / conv4 as pair Karatsuba GEMMs"), F16X3 computes conv3 and conv4 (Beluga.py:29-32)
+ * in output pairs (y[2p], y[2p+1]) as a 2 x 2 Toeplitz Karatsuba: 13 instead of 16 (32-channel, tap)
+ * K blocks per pair.  Pairs are (even, odd) rows
+ * of a window's rows on every per-window path, and of the segment's pool1 rows on the segment
+ * path: a forward_segments call holding a window on an odd pool1 row (offset / 4 odd, in the
+ * computed strand's coordinates) runs conv3 / conv4 direct for every window.  ROLE of per-window
+ * forwards: 0 pairs (default), 1 direct; the same role gives the same bits on every path, the
+ * other agrees to the parity bar. */
+int expecto_beluga_set_conv_role(expecto_beluga_t h, int role);
+
 /* y[n,2002] = Beluga.forward(x[n,4,1,2000]) (x contiguous fp32, any values).  When the handle
  * holds the k-mer tables, runs F16X3 or BF16X6, x is 16-byte aligned and every column of x is an
  * exact one-hot column (one 1.0f, three +0.0f) or all zeros, as encodeSeqs writes them

@@ -227,10 +227,12 @@ def test_segment_pairs_alt_runs_are_bitwise_equal(precision, max_batch):
     yf = y.view(4 * S * n, 2002)
     eng.forward_segment_pairs(ref, L, q, alt_code, win_seg, win_off, win_row, yf[0:],
                               yf[S * n:], 2 * S * n)
-    from expecto_amd.pipeline import fc1_role
+    from expecto_amd.pipeline import conv_role, fc1_role
+    cr = conv_role(offs, L)            # offsets 4, 796, 1596: odd pool1 rows -> conv3 / conv4 direct
+    assert cr == 1
     for a, src in enumerate((ref, alt)):
         wins = torch.stack([src[:, o:o + 2000] for o in offs], 0).reshape(S * n, 2000).contiguous()  # row j*n + v
-        by_role = run_in_roles(eng, lambda: eng.forward_codes(wins, 2).view(2, S, n, 2002))
+        by_role = run_in_roles(eng, lambda: eng.forward_codes(wins, 2).view(2, S, n, 2002), conv=cr)
         # each window in its FC1 role; the direct FC1 (role 4) when > 1/3 of the windows hold the SNV
         n_alt = int(sum(((o <= q) & (q < o + 2000)).sum() for o in offs))
         role = (lambda o, sd: 4) if 3 * n_alt > S * n else (lambda o, sd: fc1_role(int(o), L, sd == 1))
