@@ -1398,6 +1398,7 @@ __device__ __forceinline__ int conv_swz(int r) {
   return ((r >> 2) & 1) << 1;
 }
 
+
 // Pool epilogue of the f16x3 conv kernels through LDS.  A lane's 4 accumulator rows of a
 // 16-row block are one pool group (rows 4*fq..4*fq+3; m0 and s_in are multiples of 4), so the
 // pooled value needs no shuffle: maxpool(relu(x*cs + b)) = relu(max(x)*cs + b) (monotone maps).
@@ -1895,7 +1896,7 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
     const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, 0x7fffffff, 0x00020000);
     auto issue_a = [&](int chunk, int i0, int ni) {
       char* base = aslab + (chunk & 1) * G::ASLAB;
-      const int src_chunk = (TM & 8) ? 0 : chunk;
+      const int src_chunk = (TM & (8 | 16)) ? 0 : chunk;   // timing probes: A L2-hot
       for (int i = i0; i < i0 + ni; ++i) {
         const int P = min(pw + 4 * i, G::PIECES - 1);
         char* dst = base + (P & 1) * G::APLANE + (P >> 1) * 1024;
@@ -1903,7 +1904,7 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
       }
     };
     auto issue_b = [&](int s, int slot) {
-      if constexpr ((TM & 8) != 0) s = 0;
+      if constexpr ((TM & (8 | 32)) != 0) s = 0;          // timing probes: B L2-hot
       char* base = bring + slot * H3C_BSTAGE;
 #pragma unroll
       for (int j = 0; j < 5; ++j)

@@ -60,9 +60,9 @@ Variant mkk(const char* name) {
   return {name, 2 * CK_PAIRS, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3k<L, EPI_RELU, PROBE><<<nblk, 512>>>(a); }};
 }
 
-template <int L>
+template <int L, int TM = 256>
 Variant mkp(const char* name) {
-  return {name, 256, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3p<L, EPI_RELU, 256, 4><<<nblk, 512>>>(a); }};
+  return {name, 256, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3p<L, EPI_RELU, TM, 4><<<nblk, 512>>>(a); }};
 }
 
 int main(int argc, char** argv) {
@@ -96,6 +96,9 @@ int main(int argc, char** argv) {
   std::vector<Variant> vs;
   if (c4) {
     vs.push_back(mkp<4>("direct_h3p"));
+    vs.push_back(mkp<4, 256 | 8>("direct_hotAB"));
+    vs.push_back(mkp<4, 256 | 16>("direct_hotA"));
+    vs.push_back(mkp<4, 256 | 32>("direct_hotB"));
     vs.push_back(mkk<4, 0>("karatsuba"));
     vs.push_back(mkk<4, 1>("k_no_s"));
     vs.push_back(mkk<4, 2>("k_no_barrier"));
@@ -105,6 +108,9 @@ int main(int argc, char** argv) {
     vs.push_back(mkk<4, 16>("k_s_valu_only"));
   } else {
     vs.push_back(mkp<3>("direct_h3p"));
+    vs.push_back(mkp<3, 256 | 8>("direct_hotAB"));
+    vs.push_back(mkp<3, 256 | 16>("direct_hotA"));
+    vs.push_back(mkp<3, 256 | 32>("direct_hotB"));
     vs.push_back(mkk<3, 0>("karatsuba"));
     vs.push_back(mkk<3, 1>("k_no_s"));
     vs.push_back(mkk<3, 2>("k_no_barrier"));
@@ -119,7 +125,7 @@ int main(int argc, char** argv) {
   std::vector<double> best(vs.size(), 1e30), sum(vs.size(), 0.0);
   for (int r = 0; r < rounds; ++r)
     for (size_t v = 0; v < vs.size(); ++v) {
-      const bool kar = vs[v].rows_per_tile == 2 * CK_PAIRS && vs[v].name != "direct_h3p";
+      const bool kar = vs[v].name.rfind("direct", 0) != 0;
       GemmArgs a{};
       a.A = reinterpret_cast<const float*>(X);
       a.lda = cin;
