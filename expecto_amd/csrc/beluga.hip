@@ -2433,7 +2433,10 @@ int fk_fc1(expecto_beluga* h, const float* x, float* const* seq, const FkProduct
         }
       }
     }
-    beluga_fc_h3k<0><<<dim3((unsigned)blk), dim3(512), 0, st>>>(G);
+    G.rr = mask ? 0 : 1;   // full launches: M tiles dealt round robin to the 8 XCDs (gemm_kernel.h)
+    const long long mtt = blk / G.n_tiles;
+    const long long grid = G.rr ? (mtt + 7) / 8 * 8 * G.n_tiles : blk;
+    beluga_fc_h3k<0><<<dim3((unsigned)grid), dim3(512), 0, st>>>(G);
     int rc = check_launch("beluga_fc_h3k");
     if (rc) return rc;
   }

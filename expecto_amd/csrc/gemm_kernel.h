@@ -1236,19 +1236,38 @@ struct FcGroup {
   FcDesc d[FCK_MAX];
   int n, kb_total, n_tiles, n_store;
   long long ldc;
+  int rr;                    // 1: M tiles dealt round robin to the XCDs (grid 8 * ceil(M tiles / 8) * n_tiles)
 };
 
+// rr: work is dealt to the XCDs by M tile, round robin over the descriptors' M tiles in order (a
+// workgroup's XCD is blockIdx mod 8): XCD x runs M tiles x, x + 8, x + 16, ... each with its N tiles
+// back to back (the A rows of an M tile are read on one XCD, its ~32 concurrent workgroups share ~5
+// M tiles' weight tiles, as the N-fastest order of beluga_fc_h3w).  Contiguous lin ranges per XCD
+// (the other kernels' remap, rr 0) give the last XCDs only the short tail GEMM (120 K blocks against
+// 250): they idle for the rest of the launch (SQ busy 3.48 of 4 per cycle against 3.89 in the direct
+// FC1; FC1 13.0 -> 12.2 ms per step with rr).  Blocks past the last M tile exit.  The masked in-place
+// alt launches keep rr 0 (measured slower with rr: 1.44 -> 1.90 ms per step).
 template <int TM = 0>
 __global__ __launch_bounds__(512, 1) void beluga_fc_h3k(FcGroup g) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * FCW_STAGE];
   const unsigned nblk = gridDim.x, bid = blockIdx.x;
-  const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
-  const int lin = (int)((xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3));
-  int k = 0;
-  while (k + 1 < g.n && lin >= g.d[k + 1].blk0) ++k;
+  int k = 0, mt, nt;
+  if (g.rr) {
+    const int slot = (int)(bid >> 3);
+    const int T = (slot / g.n_tiles) * 8 + (int)(bid & 7u);   // global M tile (descriptor order)
+    nt = slot % g.n_tiles;
+    while (k + 1 < g.n && T >= g.d[k + 1].blk0 / g.n_tiles) ++k;
+    mt = T - g.d[k].blk0 / g.n_tiles;
+    if (mt >= g.d[k].m_tiles) return;                 // past the last descriptor's M tiles
+  } else {
+    const unsigned xcd = bid & 7u, q = nblk >> 3, rr = nblk & 7u;
+    const int lin = (int)((xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3));
+    while (k + 1 < g.n && lin >= g.d[k + 1].blk0) ++k;
+    const int r = lin - g.d[k].blk0;
+    nt = r % g.n_tiles;
+    mt = r / g.n_tiles;
+  }
   const FcDesc& d = g.d[k];
-  const int r = lin - d.blk0;
-  const int nt = r % g.n_tiles, mt = r / g.n_tiles;
   if (d.mask && !(d.mask[mt] & 1u)) return;
   const int n0 = nt * FCW_BN;
   constexpr int ROW_KB = 128;
