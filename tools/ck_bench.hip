@@ -122,6 +122,13 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
+  // ONLY=<name>: that variant alone (counter passes under rocprofv3 --pmc)
+  if (const char* only = getenv("ONLY")) {
+    std::vector<Variant> keep;
+    for (auto& v : vs)
+      if (v.name == only) keep.push_back(v);
+    vs = keep;
+  }
   std::vector<double> best(vs.size(), 1e30), sum(vs.size(), 0.0);
   for (int r = 0; r < rounds; ++r)
     for (size_t v = 0; v < vs.size(); ++v) {
@@ -162,6 +169,6 @@ int main(int argc, char** argv) {
   printf("%s, %d windows, M %lld rows\n", c4 ? "conv4 (unpooled)" : "conv3", nb, M);
   for (size_t v = 0; v < vs.size(); ++v)
     printf("%-14s mean %.3f ms  best %.3f ms  dense-equivalent %.1f TF/s  (%.3fx direct)\n", vs[v].name.c_str(),
-           sum[v] / rounds, best[v], alg / (sum[v] / rounds * 1e-3) / 1e12, sum[0] / sum[v]);
+           sum[v] / rounds, best[v], alg / (sum[v] / rounds * 1e-3) / 1e12, vs.empty() ? 0.0 : sum[0] / sum[v]);
   return 0;
 }
