@@ -1567,6 +1567,8 @@ struct expecto_beluga {
   int fc1_m_group = 8;                // order 3: M tiles per group (EXPECTO_FC1_M_GROUP)
   bool fc_wide = true;                // f16x3 FC split-K GEMMs on 336-column tiles (EXPECTO_FC_WIDE; same bits)
   int conv_tile = 0;                  // f16x3 conv M tile: 0 = auto (conv_tile_rows), 256 or 384
+  int fc1_narrow = -1;                // grouped FC1 tile width: -1 auto (fc1_narrow), 0 336, 1 112 columns
+  int conv_narrow = -1;               // conv5 / conv6 tile width: -1 auto (conv_narrow), 0 160, 1 64 columns
   int seg_chunk_windows = 0;          // segment path: windows per chunk cap (0 = none; tuning knob)
   int cus = 0;                        // compute units of the device (workgroups per round)
   bool pool_one_pass = true;          // segment path: pool2 of all phases in one pass (same bits)
@@ -1893,6 +1895,20 @@ int conv_tile_rows(const expecto_beluga* h, int l, bool pool, long long M, int n
   return cost(384, 1.0) * 1.1 <= cost(256, 1.0) ? 384 : 256;
 }
 
+// 64-column tiles for conv5 / conv6 (640 outputs: 10 N tiles instead of 4; gemm_kernel.h
+// gemm_conv_h3p_body NB 4, same bits) when they need clearly fewer rounds of the chip's workgroups
+// than the layer's 160-column choice -- the per-window forwards of small batches (batch 32: 60
+// workgroups on 256 CUs).  EXPECTO_CONV_NARROW=0 / 1 forces it (same bits either way).
+bool conv_narrow(const expecto_beluga* h, int l, long long M, int bm, int n_tiles) {
+  if (g_precision != EXPECTO_PRECISION_F16X3 || (l != 3 && l != 4)) return false;
+  if (h->conv_narrow >= 0) return h->conv_narrow != 0;
+  const long long cus = h->cus > 0 ? h->cus : 256;
+  auto cost = [&](int rows, long long tiles, int cols) {
+    return (double)(((M + rows - 1) / rows * tiles + cus - 1) / cus) * rows * cols;
+  };
+  return cost(256, kConv[l].cout / 64, 64) * 1.1 <= cost(bm, n_tiles, GBN);
+}
+
 template <int LAYER, int EPI>
 int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
   if (bm == 0) bm = (int)gemm_bm();
@@ -1922,6 +1938,13 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
           beluga_conv_h3p<LAYER, EPI, 256 | H3P_FUSE_CONV1, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
         } else {
           EXPECTO_REQUIRE(false, "fused conv1: conv2 + pool1 only");
+        }
+      } else if (a.n_tile_cols == 64) {   // 64-column tiles (conv_narrow: conv5 / conv6 of small batches)
+        if constexpr ((LAYER == 5 || LAYER == 6) && EPI == EPI_RELU) {
+          EXPECTO_REQUIRE(bm == 256 && a.n_tiles * 64 >= a.n_store, "64-column conv tiles: 256 rows");
+          beluga_conv_h3p<LAYER, EPI, 256, 4, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
+        } else {
+          EXPECTO_REQUIRE(false, "64-column conv tiles: conv5 / conv6 only");
         }
       } else if (bm == 384)
         beluga_conv_h3r<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
@@ -2065,7 +2088,12 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
   a.kper = 8 * g.cin;
   a.taps = 8;
   a.n_tiles = npad_of(g.cout) / GBN;
-  const int bm = f1 ? 256 : conv_tile_rows(h, l, pool, a.M, (int)a.n_tiles);
+  int bm = f1 ? 256 : conv_tile_rows(h, l, pool, a.M, (int)a.n_tiles);
+  if (!f1 && !pool && conv_narrow(h, l, a.M, bm, (int)a.n_tiles)) {
+    bm = 256;
+    a.n_tile_cols = 64;
+    a.n_tiles = g.cout / 64;
+  }
   a.m_tiles = (a.M + bm - 1) / bm;
   a.m_fastest = 0;
   a.bias = h->bt[l];
@@ -2365,6 +2393,20 @@ int fk_reduce(expecto_beluga* h, const float* part, const int* prow, int n, floa
   return check_launch("fk_reduce_h2");
 }
 
+// Tile width of a full grouped FC1 launch over mtt M tiles (256 rows each): the 336-column tile
+// (6 N tiles) unless 112-column tiles (18 N tiles, a third of the work each; gemm_kernel.h
+// fc_h3w_tile NB 7, same bits) need clearly fewer rounds of the chip's workgroups -- the per-window
+// forwards of small batches (the reference's batch 32 / 200 calls: 9 M tiles, 54 workgroups on 256
+// CUs).  EXPECTO_FC1_NARROW=0 / 1 forces the choice (same bits either way).
+constexpr int kFcNarrowNb = 7;
+static_assert(kHidLd % (16 * kFcNarrowNb) == 0 && kHidLd % FCW_BN == 0, "FC1 N tiles");
+bool fc1_narrow(const expecto_beluga* h, long long mtt) {
+  if (h->fc1_narrow >= 0) return h->fc1_narrow != 0;
+  const long long cus = h->cus > 0 ? h->cus : 256;
+  const long long wide = (mtt * (kHidLd / FCW_BN) + cus - 1) / cus * 3, narrow = (mtt * (kHidLd / 112) + cus - 1) / cus;
+  return (double)narrow * 1.1 <= (double)wide;
+}
+
 // One grouped launch of the Karatsuba FC1 over n windows: per product g with cnt[g] groups, its
 // kFkSlabs K slabs, then the tail over the windows (w_rows: window starts), as split-K partial rows
 // of `part` in that order (the layout prow was built for); then fk_reduce_h2 into h1.  x: conv6 rows
@@ -2435,8 +2477,16 @@ int fk_fc1(expecto_beluga* h, const float* x, float* const* seq, const FkProduct
     }
     G.rr = mask ? 0 : 1;   // full launches: M tiles dealt round robin to the 8 XCDs (gemm_kernel.h)
     const long long mtt = blk / G.n_tiles;
-    const long long grid = G.rr ? (mtt + 7) / 8 * 8 * G.n_tiles : blk;
-    beluga_fc_h3k<0><<<dim3((unsigned)grid), dim3(512), 0, st>>>(G);
+    const bool narrow = !mask && fc1_narrow(h, mtt);
+    if (narrow) {   // 112-column tiles: same bits, 3x the workgroups
+      G.n_tiles = kHidLd / (16 * kFcNarrowNb);
+      for (int i = 0; i < G.n; ++i) G.d[i].blk0 = G.d[i].blk0 / (kHidLd / FCW_BN) * G.n_tiles;
+    }
+    const long long grid = G.rr ? (mtt + 7) / 8 * 8 * G.n_tiles : mtt * G.n_tiles;
+    if (narrow)
+      beluga_fc_h3k<0, kFcNarrowNb><<<dim3((unsigned)grid), dim3(512), 0, st>>>(G);
+    else
+      beluga_fc_h3k<0><<<dim3((unsigned)grid), dim3(512), 0, st>>>(G);
     int rc = check_launch("beluga_fc_h3k");
     if (rc) return rc;
   }
@@ -3599,6 +3649,16 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
     h->fk_role = v;
   }
   if (const char* e = getenv("EXPECTO_SEG_CHUNK_WINDOWS")) h->seg_chunk_windows = atoi(e);   // same bits either way
+  if (const char* e = getenv("EXPECTO_CONV_NARROW")) {   // conv5 / conv6 tile width (same bits either way)
+    const int v = atoi(e);
+    EXPECTO_REQUIRE(v >= -1 && v <= 1, "EXPECTO_CONV_NARROW must be -1 (auto), 0 or 1");
+    h->conv_narrow = v;
+  }
+  if (const char* e = getenv("EXPECTO_FC1_NARROW")) {   // grouped FC1 tile width (same bits either way)
+    const int v = atoi(e);
+    EXPECTO_REQUIRE(v >= -1 && v <= 1, "EXPECTO_FC1_NARROW must be -1 (auto), 0 or 1");
+    h->fc1_narrow = v;
+  }
   if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)
     const int v = atoi(e);
     EXPECTO_REQUIRE(v == 0 || v == 256 || v == 384, "EXPECTO_CONV_TILE must be 0 (auto), 256 or 384");

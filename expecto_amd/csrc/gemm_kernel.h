@@ -1023,22 +1023,38 @@ constexpr int FCW_STAGE = 2 * FCW_APLANE + 2 * FCW_BPLANE;   // 75,776 B
 constexpr int FCW_EROW = 176 * 4 + 16;                 // epilogue staging row stride (720 B)
 constexpr int FCW_EWAVE = 16 * FCW_EROW;               // 11,520 B per wave
 
-// One 256 x 336 split-K partial tile of the wide FC GEMM: A row m (< M) starts at element
+// One 256 x (16 NB) split-K partial tile of the wide FC GEMM: A row m (< M) starts at element
 // (a_rows ? a_rows[m] + a_off : m * 32 * lda_kb) of A and is read for nk 32-deep K blocks from
 // K block kb0; Bb = the weight planes of column n0 at the same first K block (kb_total K blocks
 // per weight row); the fp32 partial row m goes to cbase + m * ldc (columns < n_store).  Shared by
 // beluga_fc_h3w (one split-K GEMM) and beluga_fc_h3k (a group of GEMMs in one launch): the same
-// pieces, products and k order per output.
-template <int TM>
+// pieces, products and k order per output.  NB = 21 (336 columns) everywhere but the grouped FC1 of
+// small batches, which takes NB = 7 (112 columns, 3x the workgroups; fc_narrow in beluga.hip): an
+// output's products and k order do not depend on the tile width, so both give the same bits.  A wave
+// whose 32 rows all lie past M skips its MFMAs and fragment reads (it still issues its LDS-DMA
+// pieces and meets every barrier): in a part-filled M tile the live waves then have their SIMDs
+// to themselves.
+template <int NB>
+struct FcwGeo {
+  static constexpr int BPLANE = NB * 1024;
+  static constexpr int STAGE = 2 * FCW_APLANE + 2 * BPLANE;
+  static constexpr int JB = (2 * NB + 7) / 8;           // B pieces per wave and stage
+  static constexpr int NP = 4 + JB;                     // LDS-DMA pieces per wave and stage
+  static_assert(2 * STAGE >= 8 * FCW_EWAVE, "epilogue staging inside the stage ring");
+};
+
+template <int TM, int NB = FCW_NB>
 __device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_rows, long long a_off, long long lda_kb,
                                             int kb0a, long long M, const char* Bb, int kb_total, int nk, float* cbase,
                                             long long ldc, int n_store, long long m0, int n0, char* smem) {
+  using G = FcwGeo<NB>;
   constexpr int ROW_KB = 128;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   auto swz = [](int r) { return (-(r >> 2)) & 3; };
   // this wave's LDS-DMA pieces: A pieces P = wave + 8i (i < 4) of 32 (plane P & 1, rows
-  // 16 (P >> 1) ..), B pieces Q = min(wave + 8j, 41) (j < 6) of 42 (plane Q / 21, cols 16 (Q % 21) ..)
+  // 16 (P >> 1) ..), B pieces Q = min(wave + 8j, 2 NB - 1) (j < JB) of 2 NB (plane Q / NB, cols
+  // 16 (Q % NB) ..)
   const char* asrc[4];
   unsigned adst[4];
 #pragma unroll
@@ -1052,17 +1068,18 @@ __device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_r
     asrc[i] = (const char*)A + kb0 * ROW_KB + pl * 64 + 16 * c;
     adst[i] = (unsigned)(pl * FCW_APLANE + g * 1024);
   }
-  unsigned boff[6], bdst[6];
+  static_assert(G::JB <= 6, "B pieces per wave");
+  unsigned boff[6], bdst[6];   // (a dependent bound here fails the host pass of hipcc's lambdas)
 #pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    const int Q = min(wave + 8 * j, 2 * FCW_NB - 1);
-    const int pl = Q / FCW_NB, r = 16 * (Q % FCW_NB) + (lane >> 2);
+  for (int j = 0; j < G::JB; ++j) {
+    const int Q = min(wave + 8 * j, 2 * NB - 1);
+    const int pl = Q / NB, r = 16 * (Q % NB) + (lane >> 2);
     const int c = (lane & 3) ^ swz(r);
     boff[j] = (unsigned)((long long)r * kb_total * ROW_KB + pl * 64 + 16 * c);
     bdst[j] = (unsigned)(2 * FCW_APLANE + Q * 1024);
   }
   const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, 0x7fffffff, 0x00020000);
-  auto issue_piece = [&](int s, char* base, int k) {   // piece k < 10 of stage s: 0-3 A, 4-9 B
+  auto issue_piece = [&](int s, char* base, int k) {   // piece k < NP of stage s: 0-3 A, then B
     if constexpr ((TM & 8) != 0) s = 0;
     if (k < 4)
       glds16(asrc[k] + (long long)((TM & 16) ? 0 : s) * ROW_KB, base + adst[k]);
@@ -1071,11 +1088,11 @@ __device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_r
                                                (unsigned)(((TM & 32) ? 0 : s) * ROW_KB), 0, 0);
   };
 
-  floatx4v acc[2][FCW_NB];
+  floatx4v acc[2][NB];
 #pragma unroll
   for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
-    for (int nb = 0; nb < FCW_NB; ++nb)
+    for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[mb][nb][r] = 0.f;
   const int fr = lane & 15, fq = lane >> 4;
@@ -1091,7 +1108,7 @@ __device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_r
   auto read_b = [&](const char* base, int nb, bf16x8 (&b)[3]) {
     const char* br = base + brow + nb * 1024;
     b[0] = *(const bf16x8*)(br);
-    b[1] = *(const bf16x8*)(br + FCW_BPLANE);
+    b[1] = *(const bf16x8*)(br + G::BPLANE);
   };
   auto pin = [&](int nv) {   // one unit: 6 MFMAs, <= 1 LDS-DMA piece, the next unit's 2 B reads
 #pragma unroll
@@ -1104,50 +1121,65 @@ __device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_r
   };
   // prologue: stage 0
 #pragma unroll
-  for (int k = 0; k < 10; ++k) issue_piece(0, smem, k);
+  for (int k = 0; k < G::NP; ++k) issue_piece(0, smem, k);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   bf16x8 as[2][3];
   bf16x8 b0[3], b1[3];
-  for (int s = 0; s < nk; ++s) {
-    const char* base = smem + (s & 1) * FCW_STAGE;
-    char* nbase = smem + ((s + 1) & 1) * FCW_STAGE;
-    // the next stage's pieces are issued unconditionally (the last stage re-fetches its own K block
-    // into the free buffer, drained before the epilogue): a runtime `more` test compiled to a branch
-    // around every piece, and the block boundaries made the LDS-read waits lgkmcnt(0)
-    const int s_next = min(s + 1, nk - 1);
-    constexpr bool more = !(TM & 2);
-    read_b(base, 0, b0);
-    read_a(base, as);
+  const bool live = m0 + 32 * wave < M;   // wave-uniform: some of this wave's rows are real
+  if (live) {
+    for (int s = 0; s < nk; ++s) {
+      const char* base = smem + (s & 1) * G::STAGE;
+      char* nbase = smem + ((s + 1) & 1) * G::STAGE;
+      // the next stage's pieces are issued unconditionally (the last stage re-fetches its own K
+      // block into the free buffer, drained before the epilogue): a runtime `more` test compiled to
+      // a branch around every piece, and the block boundaries made the LDS-read waits lgkmcnt(0)
+      const int s_next = min(s + 1, nk - 1);
+      constexpr bool more = !(TM & 2);
+      read_b(base, 0, b0);
+      read_a(base, as);
 #pragma unroll
-    for (int nb = 0; nb < FCW_NB; ++nb) {
-      const int k = nb * 10 / FCW_NB;                   // units 0, 2, 4, ... issue pieces 0..9
-      const bool issue = more && (nb * 10 % FCW_NB) < 10;
-      if (issue) issue_piece(s_next, nbase, k);
-      if (nb + 1 < FCW_NB) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
-      // nothing crosses this point: the next unit's fragment reads stay ahead of this unit's
-      // MFMAs in their own registers.  Without it the scheduler (minimising registers) read
-      // every fragment right before its MFMA into the previous unit's registers, and the
-      // lgkmcnt(0) before each use exposed the full LDS latency (gemm_bench fc1 8192 rows:
-      // 499 vs 474 fp32-eq TF/s; without LDS-DMA 630 vs 533)
-      __builtin_amdgcn_sched_barrier(0);
+      for (int nb = 0; nb < NB; ++nb) {
+        const int k = nb * G::NP / NB;                  // units spread the NP pieces
+        const bool issue = more && (nb * G::NP % NB) < G::NP;
+        if (issue) issue_piece(s_next, nbase, k);
+        if (nb + 1 < NB) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
+        // nothing crosses this point: the next unit's fragment reads stay ahead of this unit's
+        // MFMAs in their own registers.  Without it the scheduler (minimising registers) read
+        // every fragment right before its MFMA into the previous unit's registers, and the
+        // lgkmcnt(0) before each use exposed the full LDS latency (gemm_bench fc1 8192 rows:
+        // 499 vs 474 fp32-eq TF/s; without LDS-DMA 630 vs 533)
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int mb = 0; mb < 2; ++mb) acc[mb][nb] = planes_mfma<2>(acc[mb][nb], as[mb], (nb & 1) ? b1 : b0);
-      pin(issue ? 1 : 0);
+        for (int mb = 0; mb < 2; ++mb) acc[mb][nb] = planes_mfma<2>(acc[mb][nb], as[mb], (nb & 1) ? b1 : b0);
+        pin(issue ? 1 : 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of stage s+1 landed
+      __builtin_amdgcn_s_barrier();                      // everyone's, and stage s fully read
+      asm volatile("" ::: "memory");
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of stage s+1 landed
-    __builtin_amdgcn_s_barrier();                      // everyone's, and stage s fully read
-    asm volatile("" ::: "memory");
+  } else {   // rows all past M: this wave's share of the pieces and the barriers only
+    for (int s = 0; s < nk; ++s) {
+      char* nbase = smem + ((s + 1) & 1) * G::STAGE;
+      const int s_next = min(s + 1, nk - 1);
+      if constexpr (!(TM & 2)) {
+#pragma unroll
+        for (int k = 0; k < G::NP; ++k) issue_piece(s_next, nbase, k);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    return;   // no stores: every row of this wave is >= M
   }
   // split-K partial epilogue: 16-row x (176 | 160)-column passes through the wave's LDS area
   char* const lds = smem + wave * FCW_EWAVE;
 #pragma unroll
   for (int mb = 0; mb < 2; ++mb) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      constexpr int NB0[2] = {0, 11};
-      const int nb0 = NB0[h], nbn = h == 0 ? 11 : 10, cols = 16 * nbn;
+    for (int h = 0; h < (NB > 11 ? 2 : 1); ++h) {
+      const int nb0 = h ? 11 : 0, nbn = NB > 11 ? (h == 0 ? 11 : NB - 11) : NB, cols = 16 * nbn;
 #pragma unroll
       for (int nb = 0; nb < 11; ++nb) {
         if (nb >= nbn) break;
@@ -1156,7 +1188,7 @@ __device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_r
           *(float*)(lds + (4 * fq + j) * FCW_EROW + (nb * 16 + fr) * 4) = acc[mb][nb0 + nb][j];
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      const int chunks = cols / 4;                      // 16-B chunks per row (44 | 40)
+      const int chunks = cols / 4;                      // 16-B chunks per row (44 | 40 | 28)
       for (int i = lane; i < 16 * chunks; i += 64) {
         const int row = i / chunks, ch = i - row * chunks;
         const long long m = m0 + wave * 32 + mb * 16 + row;
@@ -1247,9 +1279,9 @@ struct FcGroup {
 // 250): they idle for the rest of the launch (SQ busy 3.48 of 4 per cycle against 3.89 in the direct
 // FC1; FC1 13.0 -> 12.2 ms per step with rr).  Blocks past the last M tile exit.  The masked in-place
 // alt launches keep rr 0 (measured slower with rr: 1.44 -> 1.90 ms per step).
-template <int TM = 0>
+template <int TM = 0, int NB = FCW_NB>
 __global__ __launch_bounds__(512, 1) void beluga_fc_h3k(FcGroup g) {
-  __shared__ __attribute__((aligned(1024))) char smem[2 * FCW_STAGE];
+  __shared__ __attribute__((aligned(1024))) char smem[2 * FcwGeo<NB>::STAGE];
   const unsigned nblk = gridDim.x, bid = blockIdx.x;
   int k = 0, mt, nt;
   if (g.rr) {
@@ -1269,10 +1301,10 @@ __global__ __launch_bounds__(512, 1) void beluga_fc_h3k(FcGroup g) {
   }
   const FcDesc& d = g.d[k];
   if (d.mask && !(d.mask[mt] & 1u)) return;
-  const int n0 = nt * FCW_BN;
+  const int n0 = nt * 16 * NB;
   constexpr int ROW_KB = 128;
-  fc_h3w_tile<TM>(d.A, d.a_rows, d.a_off, 0, 0, d.M, d.Bp + (long long)n0 * g.kb_total * ROW_KB, g.kb_total, d.nk, d.C,
-                  g.ldc, g.n_store, (long long)mt * X6P_BM, n0, smem);
+  fc_h3w_tile<TM, NB>(d.A, d.a_rows, d.a_off, 0, 0, d.M, d.Bp + (long long)n0 * g.kb_total * ROW_KB, g.kb_total, d.nk,
+                      d.C, g.ldc, g.n_store, (long long)mt * X6P_BM, n0, smem);
 }
 
 // ---- f16x3 conv GEMM with the Toeplitz A tile staged once per channel chunk -------------
@@ -1328,11 +1360,11 @@ constexpr int h3c_lds_mb() { return 2 * SlabGeo<MB>::ASLAB + NSB * H3C_BSTAGE; }
 // column block under an n < n_store branch, right before use: 20-40 loads per tile each followed
 // by s_waitcnt vmcnt(0) -- which also waited for the epilogue's own earlier global stores --
 // i.e. 20-40 serialized memory latencies per tile (BATCH false: that form, a timing probe).
-template <bool BATCH = true>
-__device__ __forceinline__ void epi_factors(const GemmArgs& p, int n0, int fr, float (&cso)[10], float (&bo)[10]) {
-  float c[10], b[10];
+template <bool BATCH = true, int NB = 10>
+__device__ __forceinline__ void epi_factors(const GemmArgs& p, int n0, int fr, float (&cso)[NB], float (&bo)[NB]) {
+  float c[NB], b[NB];
 #pragma unroll
-  for (int nb = 0; nb < 10; ++nb) {
+  for (int nb = 0; nb < NB; ++nb) {
     const int n = n0 + nb * 16 + fr;
     if constexpr (BATCH) {
       const int nc = min(n, p.n_store - 1);
@@ -1344,7 +1376,7 @@ __device__ __forceinline__ void epi_factors(const GemmArgs& p, int n0, int fr, f
     }
   }
 #pragma unroll
-  for (int nb = 0; nb < 10; ++nb) {
+  for (int nb = 0; nb < NB; ++nb) {
     const bool in = n0 + nb * 16 + fr < p.n_store;
     // fmaxf(acc*cs + b, 0) * osc with the power-of-2 scales folded: the same value
     cso[nb] = in ? c[nb] * p.out_scale : 0.f;
@@ -1352,21 +1384,23 @@ __device__ __forceinline__ void epi_factors(const GemmArgs& p, int n0, int fr, f
   }
 }
 
-template <int MB = 4, bool BATCH = true>
-__device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const floatx4v (&acc)[MB][10], long long mw,
+template <int MB = 4, bool BATCH = true, int NB = 10>
+__device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const floatx4v (&acc)[MB][NB], long long mw,
                                                      int n0, int lane, char* lds) {
+  static_assert(NB % 2 == 0, "whole 32-column blocks");
+  constexpr int CPR = 4 * NB;                          // 16-B chunks per staged row (40 | 16)
   const int fr = lane & 15, fq = lane >> 4;
   const long long w0 = mw / p.s_in;
   const int t0 = (int)(mw - w0 * p.s_in);
-  float csov[10], bov[10];
-  epi_factors<BATCH>(p, n0, fr, csov, bov);
+  float csov[NB], bov[NB];
+  epi_factors<BATCH, NB>(p, n0, fr, csov, bov);
   // overflow: a running max per lane and ONE flag store at the end (a per-value conditional
   // store compiled to a branch and exec-mask juggling around every value: ~4 instructions each)
   float vmax = 0.f;
 #pragma unroll
   for (int half = 0; half < MB / 2; ++half) {
 #pragma unroll
-    for (int nb = 0; nb < 10; ++nb) {
+    for (int nb = 0; nb < NB; ++nb) {
       const float cso = csov[nb], bo = bov[nb];
 #pragma unroll
       for (int mh = 0; mh < 2; ++mh) {
@@ -1386,8 +1420,8 @@ __device__ __forceinline__ void epilogue_relu_h2_lds(const GemmArgs& p, const fl
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const long long ldb = p.ldc >> 5;
 #pragma unroll 4
-    for (int i = 0; i < 20; ++i) {
-      const int k = i * 64 + lane, row = k / 40, ch = k - row * 40;
+    for (int i = 0; i < CPR / 2; ++i) {
+      const int k = i * 64 + lane, row = k / CPR, ch = k - row * CPR;
       const long long m = mw + half * 32 + row;
       if (m < p.M) {
         long long w;
@@ -1856,9 +1890,28 @@ __device__ __forceinline__ void conv12_producer(const GemmArgs& p, char* smem, l
   if (!(vmax < 65504.f)) *p.ovf = 1;   // conv1 value out of fp16 range: recomputed (bf16x6)
 }
 
-template <int LAYER, int EPI, int TM, int NSB>
+// s_waitcnt vmcnt(N) for the compile-time piece counts of the conv producers
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 2)
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 5)
+    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if constexpr (N == 10)
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else
+    static_assert(N == 2, "vmcnt value");
+}
+
+template <int LAYER, int EPI, int TM, int NSB, int NB = 10>
 __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem) {
   static_assert(NSB == 3 || NSB == 4, "B ring depth");
+  // NB 16-column blocks per tile: 10 (160 columns), or 4 (64: conv5 / conv6 of small batches, 2.5x
+  // the workgroups; an output's products and k order do not depend on the tile width -- same bits)
+  static_assert(NB == 10 || (NB == 4 && EPI == EPI_RELU && (TM & H3P_FUSE_CONV1) == 0), "conv tile width");
+  constexpr int JB = NB / 2;                          // B pieces per producer wave and stage (of 2 NB)
   // PF (NSB 4): producers keep one stage less in flight, so at the end of stage s the consumers
   // can already read stage s+1's first B fragments (and, at a chunk's last tap, the next slab's
   // A fragments) and start it right after the barrier without an LDS round trip.
@@ -1874,7 +1927,7 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const long long m0 = mt * G::BM;
-  const int n0 = nt * GBN;
+  const int n0 = nt * 16 * NB;
   const int kb_total = (int)(p.ldb / GBK);
   const long long lda_kb = p.lda / GBK;
   const int nchunk = (int)lda_kb;
@@ -1903,13 +1956,14 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
       aoff[i] = (unsigned)((m - m0) * lda_kb * ROW_KB + pl * 64 + 16 * c);
     }
     const char* Bb = (const char*)p.Bp + (long long)n0 * kb_total * ROW_KB;
-    unsigned boff[5];
+    unsigned boff[5], bdst[5];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
+    for (int j = 0; j < JB; ++j) {
       const int g = pw + 4 * j;
-      const int pl = g / 10, r = 16 * (g % 10) + (lane >> 2);
+      const int pl = g / NB, r = 16 * (g % NB) + (lane >> 2);
       const int c = (lane & 3) ^ swz(r);
       boff[j] = (unsigned)((long long)r * kb_total * ROW_KB + pl * 64 + 16 * c);
+      bdst[j] = (unsigned)((pl * 10 + g % NB) * 1024);   // plane pl at X6P_B_PLANE whatever NB
     }
     const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, 0x7fffffff, 0x00020000);
@@ -1926,8 +1980,8 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
       if constexpr ((TM & (8 | 32)) != 0) s = 0;          // timing probes: B L2-hot
       char* base = bring + slot * H3C_BSTAGE;
 #pragma unroll
-      for (int j = 0; j < 5; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + (pw + 4 * j) * 1024), 16, boff[j],
+      for (int j = 0; j < JB; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + bdst[j]), 16, boff[j],
                                                  (unsigned)(s * ROW_KB), 0, 0);
     };
     issue_a(0, 0, NAP);
@@ -1936,11 +1990,11 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
     if constexpr (NSB == 4) {
       issue_b(min(2, nk - 1), 2);
       if constexpr (PF)
-        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");    // stages 0 and 1 landed
+        wait_vm<JB>();    // stages 0 and 1 landed
       else
-        asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+        wait_vm<2 * JB>();
     } else {
-      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      wait_vm<JB>();
     }
     __builtin_amdgcn_s_barrier();
     int slot = 0;
@@ -1959,9 +2013,9 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
         // (PF: all but this stage's pieces, so B(s+2) has landed at barrier s and the
         // consumers read stage s+1's first fragments before that barrier)
         if constexpr (NSB == 4 && !PF)
-          asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+          wait_vm<2 * JB>();
         else
-          asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+          wait_vm<JB>();
         __builtin_amdgcn_s_barrier();
         slot = slot + 1 == NSB ? 0 : slot + 1;
       }
@@ -1974,11 +2028,11 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
   }
 
   // ---------------- consumer: LDS reads and MFMAs ----------------
-  floatx4v acc[4][10];
+  floatx4v acc[4][NB];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-    for (int nb = 0; nb < 10; ++nb)
+    for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[mb][nb][r] = 0.f;
   const int fr = lane & 15, fq = lane >> 4;
@@ -2019,8 +2073,8 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
       const int nslot = slot + 1 == NSB ? 0 : slot + 1;
       if constexpr (!PF) read_b(base, 0, b0);
 #pragma unroll
-      for (int nb = 0; nb < 10; ++nb) {
-        if (nb + 1 < 10) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
+      for (int nb = 0; nb < NB; ++nb) {
+        if (nb + 1 < NB) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb) acc[mb][nb] = planes_mfma<2>(acc[mb][nb], as[mb], (nb & 1) ? b1 : b0);
         pin();
@@ -2044,25 +2098,25 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-      for (int nb = 0; nb < 10; ++nb) t += acc[mb][nb][0] + acc[mb][nb][1] + acc[mb][nb][2] + acc[mb][nb][3];
+      for (int nb = 0; nb < NB; ++nb) t += acc[mb][nb][0] + acc[mb][nb][1] + acc[mb][nb][2] + acc[mb][nb][3];
     p.C[(m0 + wave * 64 + lane) % p.M] = t;
     return;
   }
   if constexpr (EPI == EPI_RELU || EPI == EPI_RELU_POOL4) {
     __builtin_amdgcn_s_barrier();                     // producers drained their tail pieces
     if constexpr (EPI == EPI_RELU)
-      epilogue_relu_h2_lds<4, (TM & 8192) == 0>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
+      epilogue_relu_h2_lds<4, (TM & 8192) == 0, NB>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
     else
       epilogue_pool_h2_lds<4, LAYER == 4, (TM & 8192) == 0>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
   } else {
-    gemm_epilogue16<EPI, 2, 10, 4>(p, acc, m0 + wave * 64, n0, 0, lane);
+    if constexpr (NB == 10) gemm_epilogue16<EPI, 2, 10, 4>(p, acc, m0 + wave * 64, n0, 0, lane);
   }
 }
 
-template <int LAYER, int EPI, int TM = 0, int NSB = 3>
+template <int LAYER, int EPI, int TM = 0, int NSB = 3, int NB = 10>
 __global__ __launch_bounds__(512, 1) void beluga_conv_h3p(GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[h3c_lds<NSB>()];
-  gemm_conv_h3p_body<LAYER, EPI, TM, NSB>(p, smem);
+  gemm_conv_h3p_body<LAYER, EPI, TM, NSB, NB>(p, smem);
 }
 
 // ---- f16x3 conv GEMM as a 2 x 2 Toeplitz Karatsuba (conv3 / conv4) --------------------------

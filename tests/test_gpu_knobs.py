@@ -46,12 +46,39 @@ def _run(monkeypatch, env, fa, dg, vs, shifts, max_batch=2048, use_segments=True
                                  {"EXPECTO_FC_WIDE": "0"}, {"EXPECTO_FC_WIDE": "0", "EXPECTO_FC1_ORDER": "2"},
                                  {"EXPECTO_FC_WIDE": "0", "EXPECTO_FC1_ORDER": "0", "EXPECTO_FC1_M_ORDER_MB": "0"},
                                  {"EXPECTO_FC_WIDE": "0", "EXPECTO_FC1_M_GROUP": "3"},
-                                 {"EXPECTO_FC1K_SLICE": "700"}])
+                                 {"EXPECTO_FC1K_SLICE": "700"}, {"EXPECTO_FC1_NARROW": "1"},
+                                 {"EXPECTO_CONV_NARROW": "1"}])
 def test_same_bits_knobs(monkeypatch, env):
     fa, dg, vs, shifts = _setup()
     want = _run(monkeypatch, {}, fa, dg, vs, shifts)
     got = _run(monkeypatch, env, fa, dg, vs, shifts)
     assert torch.equal(got, want), f"{env}: max|diff| {float((got - want).abs().max())}"
+
+
+def test_tile_widths_small_batches(monkeypatch):
+    """Per-window batches take narrower N tiles where they need fewer rounds of workgroups: the
+    grouped FC1 112 instead of 336 columns (beluga.hip fc1_narrow; its part-filled M tiles' empty
+    waves skip their MFMAs), conv5 / conv6 64 instead of 160 (conv_narrow).  Batch 5 / 32 / 200 /
+    512 in FC1 roles 0, 3 and the direct FC1: the same bits as the wide tiles (EXPECTO_FC1_NARROW=0,
+    EXPECTO_CONV_NARROW=0)."""
+    from expecto_amd import beluga
+    rng = np.random.default_rng(61)
+    codes = torch.from_numpy(rng.integers(0, 5, (512, 2000)).astype(np.uint8)).cuda()
+    engs = {}
+    for v in ("0", "-1"):
+        monkeypatch.setenv("EXPECTO_FC1_NARROW", v)
+        monkeypatch.setenv("EXPECTO_CONV_NARROW", v)
+        engs[v] = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=512).cuda().engine()
+        monkeypatch.delenv("EXPECTO_FC1_NARROW")
+        monkeypatch.delenv("EXPECTO_CONV_NARROW")
+    for role in (0, 3, 4):
+        for b in (5, 32, 200, 512):
+            ys = []
+            for eng in engs.values():
+                eng.set_fc1_role(role)
+                ys.append(eng.forward_codes(codes[:b], 2).clone())
+                eng.set_fc1_role(0)
+            assert torch.equal(ys[0], ys[1]), (role, b, float((ys[0] - ys[1]).abs().max()))
 
 
 def test_fc2_without_split_k(monkeypatch):
