@@ -1569,6 +1569,7 @@ struct expecto_beluga {
   int conv_tile = 0;                  // f16x3 conv M tile: 0 = auto (conv_tile_rows), 256 or 384
   int fc1_narrow = -1;                // grouped FC1 tile width: -1 auto (fc1_narrow), 0 336, 1 112 columns
   int conv_narrow = -1;               // conv5 / conv6 tile width: -1 auto (conv_narrow), 0 160, 1 64 columns
+  bool narrow_scope = false;          // inside forward_chunk: auto narrow tiles allowed (nothing runs beside)
   int seg_chunk_windows = 0;          // segment path: windows per chunk cap (0 = none; tuning knob)
   int cus = 0;                        // compute units of the device (workgroups per round)
   bool pool_one_pass = true;          // segment path: pool2 of all phases in one pass (same bits)
@@ -1896,17 +1897,20 @@ int conv_tile_rows(const expecto_beluga* h, int l, bool pool, long long M, int n
 }
 
 // 64-column tiles for conv5 / conv6 (640 outputs: 10 N tiles instead of 4; gemm_kernel.h
-// gemm_conv_h3p_body NB 4, same bits) when they need clearly fewer rounds of the chip's workgroups
-// than the layer's 160-column choice -- the per-window forwards of small batches (batch 32: 60
-// workgroups on 256 CUs).  EXPECTO_CONV_NARROW=0 / 1 forces it (same bits either way).
+// gemm_conv_h3p_body NB 4, same bits) for launches whose 160-column form leaves most of the chip
+// idle -- the per-window forwards of small batches (batch 32: 60 workgroups on 256 CUs).  EXPECTO_CONV_NARROW=0 / 1 forces it (same bits either way).
 bool conv_narrow(const expecto_beluga* h, int l, long long M, int bm, int n_tiles) {
   if (g_precision != EXPECTO_PRECISION_F16X3 || (l != 3 && l != 4)) return false;
   if (h->conv_narrow >= 0) return h->conv_narrow != 0;
+  if (!h->narrow_scope) return false;
+  // only when the narrow launch is one round of workgroups (per column the 64-column tile runs at
+  // ~0.8 of the 160-column one: batch 32, conv5 + conv6 281 -> 138 us for 0.4 of the work per
+  // workgroup), and only for the per-window forwards (narrow_scope): the segment path's small
+  // alt-delta conv5 / conv6 launches run beside the trunk on the second stream, where more
+  // workgroups for the same work cost the trunk (conv6 11.1 -> 11.6 ms per headline step, same box)
   const long long cus = h->cus > 0 ? h->cus : 256;
-  auto cost = [&](int rows, long long tiles, int cols) {
-    return (double)(((M + rows - 1) / rows * tiles + cus - 1) / cus) * rows * cols;
-  };
-  return cost(256, kConv[l].cout / 64, 64) * 1.1 <= cost(bm, n_tiles, GBN);
+  const long long narrow = (M + 255) / 256 * (kConv[l].cout / 64), wide = (M + bm - 1) / bm * n_tiles;
+  return narrow <= cus && wide < cus;
 }
 
 template <int LAYER, int EPI>
@@ -2395,16 +2399,18 @@ int fk_reduce(expecto_beluga* h, const float* part, const int* prow, int n, floa
 
 // Tile width of a full grouped FC1 launch over mtt M tiles (256 rows each): the 336-column tile
 // (6 N tiles) unless 112-column tiles (18 N tiles, a third of the work each; gemm_kernel.h
-// fc_h3w_tile NB 7, same bits) need clearly fewer rounds of the chip's workgroups -- the per-window
-// forwards of small batches (the reference's batch 32 / 200 calls: 9 M tiles, 54 workgroups on 256
-// CUs).  EXPECTO_FC1_NARROW=0 / 1 forces the choice (same bits either way).
+// fc_h3w_tile NB 7, same bits) fit in one round of the chip's workgroups -- the per-window forwards
+// of small batches (the reference's batch 32 / 200 calls: 9 M tiles, 54 workgroups on 256 CUs;
+// FC1 525 -> ~185 us at batch 32).  EXPECTO_FC1_NARROW=0 / 1 forces the choice (same bits either way).
 constexpr int kFcNarrowNb = 7;
 static_assert(kHidLd % (16 * kFcNarrowNb) == 0 && kHidLd % FCW_BN == 0, "FC1 N tiles");
 bool fc1_narrow(const expecto_beluga* h, long long mtt) {
   if (h->fc1_narrow >= 0) return h->fc1_narrow != 0;
+  if (!h->narrow_scope) return false;
+  // only when the narrow launch is one round of workgroups (batch 512, 2 narrow rounds against 1
+  // wide: no gain measured)
   const long long cus = h->cus > 0 ? h->cus : 256;
-  const long long wide = (mtt * (kHidLd / FCW_BN) + cus - 1) / cus * 3, narrow = (mtt * (kHidLd / 112) + cus - 1) / cus;
-  return (double)narrow * 1.1 <= (double)wide;
+  return mtt * (kHidLd / (16 * kFcNarrowNb)) <= cus;
 }
 
 // One grouped launch of the Karatsuba FC1 over n windows: per product g with cnt[g] groups, its
@@ -2615,6 +2621,11 @@ int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long 
                   int mode, long long row0, int nb, float* y, hipStream_t st) {
   int rc;
   g_precision = h->precision;
+  struct Scope {
+    expecto_beluga* h;
+    ~Scope() { h->narrow_scope = false; }
+  } scope{h};
+  h->narrow_scope = true;
   const bool kmer = use_kmer(h, x);
   const bool fuse = !kmer && fuse_conv1(h, x);
   const C1Src f1{codes, code_stride, n_src, mode, row0, kLen};
