@@ -1057,9 +1057,11 @@ __device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_r
   // 16 (Q % NB) ..)
   const char* asrc[4];
   unsigned adst[4];
+  unsigned alive = 0;   // bit i: A piece i holds a row < M (a row group past M feeds only skipping waves)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int P = wave + 8 * i, g = P >> 1, pl = P & 1;
+    if (m0 + 16 * g < M) alive |= 1u << i;
     const int r = 16 * g + (lane >> 2);
     long long m = m0 + r;
     if (m > M - 1) m = M - 1;
@@ -1081,9 +1083,10 @@ __device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_r
   const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, 0x7fffffff, 0x00020000);
   auto issue_piece = [&](int s, char* base, int k) {   // piece k < NP of stage s: 0-3 A, then B
     if constexpr ((TM & 8) != 0) s = 0;
-    if (k < 4)
-      glds16(asrc[k] + (long long)((TM & 16) ? 0 : s) * ROW_KB, base + adst[k]);
-    else
+    if (k < 4) {
+      // (the narrow tiles of small batches only: the wide kernel's schedule stays branch-free)
+      if (NB == FCW_NB || ((alive >> k) & 1u)) glds16(asrc[k] + (long long)((TM & 16) ? 0 : s) * ROW_KB, base + adst[k]);
+    } else
       __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + bdst[k - 4]), 16, boff[k - 4],
                                                (unsigned)(((TM & 32) ? 0 : s) * ROW_KB), 0, 0);
   };
