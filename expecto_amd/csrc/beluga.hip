@@ -1946,7 +1946,7 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
       } else if (a.n_tile_cols == 64) {   // 64-column tiles (conv_narrow: conv5 / conv6 of small batches)
         if constexpr ((LAYER == 5 || LAYER == 6) && EPI == EPI_RELU) {
           EXPECTO_REQUIRE(bm == 256 && a.n_tiles * 64 >= a.n_store, "64-column conv tiles: 256 rows");
-          beluga_conv_h3p<LAYER, EPI, 256, 4, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
+          beluga_conv_h3p_narrow<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
         } else {
           EXPECTO_REQUIRE(false, "64-column conv tiles: conv5 / conv6 only");
         }
@@ -2402,7 +2402,7 @@ int fk_reduce(expecto_beluga* h, const float* part, const int* prow, int n, floa
 // fc_h3w_tile NB 7, same bits) fit in one round of the chip's workgroups -- the per-window forwards
 // of small batches (the reference's batch 32 / 200 calls: 9 M tiles, 54 workgroups on 256 CUs;
 // FC1 525 -> ~185 us at batch 32).  EXPECTO_FC1_NARROW=0 / 1 forces the choice (same bits either way).
-constexpr int kFcNarrowNb = 7;
+constexpr int kFcNarrowNb = 7;   // beluga_fc_h3k_narrow
 static_assert(kHidLd % (16 * kFcNarrowNb) == 0 && kHidLd % FCW_BN == 0, "FC1 N tiles");
 bool fc1_narrow(const expecto_beluga* h, long long mtt) {
   if (h->fc1_narrow >= 0) return h->fc1_narrow != 0;
@@ -2490,7 +2490,7 @@ int fk_fc1(expecto_beluga* h, const float* x, float* const* seq, const FkProduct
     }
     const long long grid = G.rr ? (mtt + 7) / 8 * 8 * G.n_tiles : mtt * G.n_tiles;
     if (narrow)
-      beluga_fc_h3k<0, kFcNarrowNb><<<dim3((unsigned)grid), dim3(512), 0, st>>>(G);
+      beluga_fc_h3k_narrow<<<dim3((unsigned)grid), dim3(512), 0, st>>>(G);
     else
       beluga_fc_h3k<0><<<dim3((unsigned)grid), dim3(512), 0, st>>>(G);
     int rc = check_launch("beluga_fc_h3k");

@@ -1282,9 +1282,8 @@ struct FcGroup {
 // 250): they idle for the rest of the launch (SQ busy 3.48 of 4 per cycle against 3.89 in the direct
 // FC1; FC1 13.0 -> 12.2 ms per step with rr).  Blocks past the last M tile exit.  The masked in-place
 // alt launches keep rr 0 (measured slower with rr: 1.44 -> 1.90 ms per step).
-template <int TM = 0, int NB = FCW_NB>
-__global__ __launch_bounds__(512, 1) void beluga_fc_h3k(FcGroup g) {
-  __shared__ __attribute__((aligned(1024))) char smem[2 * FcwGeo<NB>::STAGE];
+template <int TM, int NB>
+__device__ __forceinline__ void fc_h3k_body(const FcGroup& g, char* smem) {
   const unsigned nblk = gridDim.x, bid = blockIdx.x;
   int k = 0, mt, nt;
   if (g.rr) {
@@ -1308,6 +1307,18 @@ __global__ __launch_bounds__(512, 1) void beluga_fc_h3k(FcGroup g) {
   constexpr int ROW_KB = 128;
   fc_h3w_tile<TM, NB>(d.A, d.a_rows, d.a_off, 0, 0, d.M, d.Bp + (long long)n0 * g.kb_total * ROW_KB, g.kb_total, d.nk,
                       d.C, g.ldc, g.n_store, (long long)mt * X6P_BM, n0, smem);
+}
+
+template <int TM = 0>
+__global__ __launch_bounds__(512, 1) void beluga_fc_h3k(FcGroup g) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * FcwGeo<FCW_NB>::STAGE];
+  fc_h3k_body<TM, FCW_NB>(g, smem);
+}
+
+// the same grouped launch on 112-column tiles (per-window forwards of small batches; same bits)
+__global__ __launch_bounds__(512, 1) void beluga_fc_h3k_narrow(FcGroup g) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * FcwGeo<7>::STAGE];
+  fc_h3k_body<0, 7>(g, smem);
 }
 
 // ---- f16x3 conv GEMM with the Toeplitz A tile staged once per channel chunk -------------
@@ -2116,10 +2127,17 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
   }
 }
 
-template <int LAYER, int EPI, int TM = 0, int NSB = 3, int NB = 10>
+template <int LAYER, int EPI, int TM = 0, int NSB = 3>
 __global__ __launch_bounds__(512, 1) void beluga_conv_h3p(GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[h3c_lds<NSB>()];
-  gemm_conv_h3p_body<LAYER, EPI, TM, NSB, NB>(p, smem);
+  gemm_conv_h3p_body<LAYER, EPI, TM, NSB>(p, smem);
+}
+
+// the same kernel on 64-column tiles (conv5 / conv6 of small per-window batches; same bits)
+template <int LAYER, int EPI>
+__global__ __launch_bounds__(512, 1) void beluga_conv_h3p_narrow(GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[h3c_lds<4>()];
+  gemm_conv_h3p_body<LAYER, EPI, 256, 4, 4>(p, smem);
 }
 
 // ---- f16x3 conv GEMM as a 2 x 2 Toeplitz Karatsuba (conv3 / conv4) --------------------------
