@@ -326,8 +326,20 @@ class Beluga(nn.Module):
 
     # -- engine management: rebuilt whenever the parameters change (load_state_dict, .cuda())
     def _params(self):
-        sd = dict(self.named_parameters())
-        return [sd[k] for k in PARAM_KEYS]
+        # (owner module, name) of each parameter, resolved once: a named_parameters() walk per
+        # forward cost ~50 us of host time, 7 % of a batch-32 Beluga.forward; a parameter
+        # reassigned on its module is still seen (the owner's _parameters is read each call)
+        slots = self.__dict__.get("_param_slots")
+        if slots is None:
+            slots = []
+            for k in PARAM_KEYS:
+                *path, name = k.split(".")
+                mod = self
+                for part in path:
+                    mod = mod._modules[part]
+                slots.append((mod._parameters, name))
+            self.__dict__["_param_slots"] = slots
+        return [d[name] for d, name in slots]
 
     def _key(self, params):
         return tuple((p.data_ptr(), p._version) for p in params)

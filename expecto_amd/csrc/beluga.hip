@@ -3768,17 +3768,61 @@ int expecto_beluga_forward_onehot(expecto_beluga_t h, const float* x, int n, flo
   // when every column of x is an exact one-hot or all-zero column, the call runs as
   // forward_codes(FWD) on codes converted chunk by chunk -- conv1 + conv2 + pool1 from the k-mer
   // tables, the same bits as forward_codes -- else conv1 / conv2 stay on the MFMAs (any fp32
-  // input, like the reference).  Deciding costs one check pass over x and one stream sync.
-  bool as_codes = false;
-  if (h->onehot_as_codes && h->kmer && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
-      (h->precision == EXPECTO_PRECISION_F16X3 || h->precision == EXPECTO_PRECISION_BF16X6)) {
-    if (!h->oh_codes) {
-      float *c = nullptr, *f = nullptr;
+  // input, like the reference).  With the per-call overflow check the codes path runs at once and
+  // the conversion's flag is read with the overflow flag at the end (one sync; an input that is not
+  // one-hot reruns on the MFMA path); with the deferred check, one check pass and a sync first.
+  const bool candidate = h->onehot_as_codes && h->kmer && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+                         (h->precision == EXPECTO_PRECISION_F16X3 || h->precision == EXPECTO_PRECISION_BF16X6);
+  if (candidate && !h->oh_codes) {
+    float *c = nullptr, *f = nullptr;
+    int rc;
+    if ((rc = dalloc(h, &c, ((size_t)h->max_batch * kLen + 3) / 4)) || (rc = dalloc(h, &f, 1))) return rc;
+    h->oh_codes = reinterpret_cast<uint8_t*>(c);
+    h->oh_bad = reinterpret_cast<int*>(f);
+  }
+  // all chunks, conv1 input from codes converted per chunk (bad: also flag non-one-hot columns) or x
+  auto run = [&](bool as_codes, int* bad) {
+    for (long long r0 = 0; r0 < n; r0 += h->max_batch) {
+      const int nb = (int)std::min<long long>(h->max_batch, n - r0);
       int rc;
-      if ((rc = dalloc(h, &c, ((size_t)h->max_batch * kLen + 3) / 4)) || (rc = dalloc(h, &f, 1))) return rc;
-      h->oh_codes = reinterpret_cast<uint8_t*>(c);
-      h->oh_bad = reinterpret_cast<int*>(f);
+      if (as_codes) {
+        {
+          LayerTimer lt(h, 0, st);
+          const long long q = (long long)nb * (kLen / 4);
+          onehot_codes<<<dim3((unsigned)((q + 255) / 256)), dim3(256), 0, st>>>(x + r0 * 4 * kLen, nb, kLen,
+                                                                              h->oh_codes, bad);
+          if ((rc = check_launch("onehot_codes"))) return rc;
+        }
+        rc = forward_chunk(h, nullptr, h->oh_codes, kLen, nb, EXPECTO_STRAND_FWD, 0, nb, y + r0 * kNFeat, st);
+      } else {
+        rc = forward_chunk(h, x, nullptr, 0, 0, 0, r0, nb, y + r0 * kNFeat, st);
+      }
+      if (rc) return rc;
     }
+    return (int)EXPECTO_OK;
+  };
+  if (candidate && h->precision == EXPECTO_PRECISION_F16X3 && !h->ovf_deferred) {
+    EXPECTO_HIP_CHECK(hipMemsetAsync(h->oh_bad, 0, sizeof(int), st));
+    int rc = run(true, h->oh_bad);
+    if (rc) return rc;
+    int flags[2] = {0, 0};
+    EXPECTO_HIP_CHECK(hipMemcpyAsync(&flags[0], h->ovf, sizeof(int), hipMemcpyDeviceToHost, st));
+    EXPECTO_HIP_CHECK(hipMemcpyAsync(&flags[1], h->oh_bad, sizeof(int), hipMemcpyDeviceToHost, st));
+    EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
+    if (flags[1]) {   // not one-hot: the whole call on the MFMA path (its own overflow check)
+      EXPECTO_HIP_CHECK(hipMemsetAsync(h->ovf, 0, sizeof(int), st));
+      return run_checked(h, st, [&]() { return run(false, nullptr); });
+    }
+    if (!flags[0]) return EXPECTO_OK;
+    EXPECTO_HIP_CHECK(hipMemsetAsync(h->ovf, 0, sizeof(int), st));   // as run_checked: bf16x6 redo
+    h->fallbacks += 1;
+    h->precision = EXPECTO_PRECISION_BF16X6;
+    rc = run(true, nullptr);
+    h->precision = EXPECTO_PRECISION_F16X3;
+    return rc;
+  }
+  bool as_codes = false;
+  if (candidate) {
     int bad = 0;
     {
       LayerTimer lt(h, 0, st);
@@ -3792,26 +3836,7 @@ int expecto_beluga_forward_onehot(expecto_beluga_t h, const float* x, int n, flo
     EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
     as_codes = bad == 0;
   }
-  return run_checked(h, st, [&]() {
-    for (long long r0 = 0; r0 < n; r0 += h->max_batch) {
-      const int nb = (int)std::min<long long>(h->max_batch, n - r0);
-      int rc;
-      if (as_codes) {
-        {
-          LayerTimer lt(h, 0, st);
-          const long long q = (long long)nb * (kLen / 4);
-          onehot_codes<<<dim3((unsigned)((q + 255) / 256)), dim3(256), 0, st>>>(x + r0 * 4 * kLen, nb, kLen,
-                                                                              h->oh_codes, nullptr);
-          if ((rc = check_launch("onehot_codes"))) return rc;
-        }
-        rc = forward_chunk(h, nullptr, h->oh_codes, kLen, nb, EXPECTO_STRAND_FWD, 0, nb, y + r0 * kNFeat, st);
-      } else {
-        rc = forward_chunk(h, x, nullptr, 0, 0, 0, r0, nb, y + r0 * kNFeat, st);
-      }
-      if (rc) return rc;
-    }
-    return (int)EXPECTO_OK;
-  });
+  return run_checked(h, st, [&]() { return run(as_codes, nullptr); });
 }
 
 int expecto_beluga_forward_codes(expecto_beluga_t h, const uint8_t* codes, int n, long long code_stride,

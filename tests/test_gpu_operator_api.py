@@ -66,13 +66,20 @@ def test_onehot_forward_equals_forward_codes_bitwise(precision):
     assert_close(y[idx].cpu().numpy(), want, what=f"one-hot forward ({precision}) vs oracle")
 
 
-def test_non_onehot_input_keeps_the_mfma_path(monkeypatch):
+@pytest.mark.parametrize("deferred", [False, True])
+def test_non_onehot_input_keeps_the_mfma_path(monkeypatch, deferred):
     """A batch with one non-one-hot value (0.5, or a -0.0) runs conv1 / conv2 on the MFMAs for the
     whole call: the same bits as a handle with EXPECTO_ONEHOT_CODES=0; an exact one-hot batch
-    differs from that handle (it takes the gather)."""
+    differs from that handle (it takes the gather) and equals forward_codes.  Both overflow-check
+    modes: per call (the codes path runs first, its one-hot flag read with the overflow flag: a
+    rerun on the MFMA path) and deferred (a check pass first)."""
     m = _model()
     mm = _model(env={"EXPECTO_ONEHOT_CODES": "0"}, monkeypatch=monkeypatch)
-    x = _onehot(_codes(20, 2))
+    for e in (m.engine(), mm.engine()):
+        e.set_overflow_check(deferred=deferred)
+    codes = _codes(20, 2)
+    x = _onehot(codes)
+    assert torch.equal(m.forward(x), m.forward_codes(torch.from_numpy(codes).cuda(), 0))
     assert not torch.equal(m.forward(x), mm.forward(x))
     for bad in (0.5, -0.0):
         xb = x.clone()
