@@ -1023,6 +1023,21 @@ constexpr int FCW_STAGE = 2 * FCW_APLANE + 2 * FCW_BPLANE;   // 75,776 B
 constexpr int FCW_EROW = 176 * 4 + 16;                 // epilogue staging row stride (720 B)
 constexpr int FCW_EWAVE = 16 * FCW_EROW;               // 11,520 B per wave
 
+// s_waitcnt vmcnt(N) for compile-time piece counts (conv producers, the 3-stage FC ring)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 2)
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 5)
+    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if constexpr (N == 10)
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else
+    static_assert(N == 2, "vmcnt value");
+}
+
 // One 256 x (16 NB) split-K partial tile of the wide FC GEMM: A row m (< M) starts at element
 // (a_rows ? a_rows[m] + a_off : m * 32 * lda_kb) of A and is read for nk 32-deep K blocks from
 // K block kb0; Bb = the weight planes of column n0 at the same first K block (kb_total K blocks
@@ -1043,7 +1058,7 @@ struct FcwGeo {
   static_assert(2 * STAGE >= 8 * FCW_EWAVE, "epilogue staging inside the stage ring");
 };
 
-template <int TM, int NB = FCW_NB>
+template <int TM, int NB = FCW_NB, int NS = 2>
 __device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_rows, long long a_off, long long lda_kb,
                                             int kb0a, long long M, const char* Bb, int kb_total, int nk, float* cbase,
                                             long long ldc, int n_store, long long m0, int n0, char* smem) {
@@ -1122,10 +1137,36 @@ __device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_r
       __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
     }
   };
-  // prologue: stage 0
+  // NS stages in the ring: 2 (the wide tiles: 2 x 75,776 B), or 3 for the narrow tiles (3 x 47,104
+  // B), whose part-filled M tiles leave a stage's loads less compute to hide behind (one live wave
+  // per CU at batch 32).  Pieces of stage s + NS - 1 are issued during stage s; at its end a wave
+  // waits until only those are outstanding (npw of them: its B pieces and its A pieces of live row
+  // groups), i.e. for stage s + 1.
+  static_assert(NS == 2 || NS == 3, "FC ring depth");
+  static_assert(NS * G::STAGE <= 160 * 1024, "FC ring in LDS");
+  static_assert(NS == 2 || NB != FCW_NB, "3-stage ring: narrow tiles (A pieces of dead row groups skipped)");
+  constexpr int LOOK = NS - 1;
+  const int npw = __builtin_popcount(alive) + G::JB;   // wave-uniform
+  auto stage_end_wait = [&]() {
+    if constexpr (NS == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of stage s+1 landed
+    } else {
+      static_assert(G::JB == 2, "vmcnt cases");
+      switch (npw) {
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+      }
+    }
+  };
+  // prologue: stages 0 .. LOOK-1
 #pragma unroll
-  for (int k = 0; k < G::NP; ++k) issue_piece(0, smem, k);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int st = 0; st < LOOK; ++st)
+#pragma unroll
+    for (int k = 0; k < G::NP; ++k) issue_piece(min(st, nk - 1), smem + st * G::STAGE, k);
+  stage_end_wait();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   bf16x8 as[2][3];
@@ -1133,12 +1174,12 @@ __device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_r
   const bool live = m0 + 32 * wave < M;   // wave-uniform: some of this wave's rows are real
   if (live) {
     for (int s = 0; s < nk; ++s) {
-      const char* base = smem + (s & 1) * G::STAGE;
-      char* nbase = smem + ((s + 1) & 1) * G::STAGE;
-      // the next stage's pieces are issued unconditionally (the last stage re-fetches its own K
+      const char* base = smem + (s % NS) * G::STAGE;
+      char* nbase = smem + ((s + LOOK) % NS) * G::STAGE;
+      // the next stage's pieces are issued unconditionally (the last stages re-fetch the last K
       // block into the free buffer, drained before the epilogue): a runtime `more` test compiled to
       // a branch around every piece, and the block boundaries made the LDS-read waits lgkmcnt(0)
-      const int s_next = min(s + 1, nk - 1);
+      const int s_next = min(s + LOOK, nk - 1);
       constexpr bool more = !(TM & 2);
       read_b(base, 0, b0);
       read_a(base, as);
@@ -1158,24 +1199,29 @@ __device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_r
         for (int mb = 0; mb < 2; ++mb) acc[mb][nb] = planes_mfma<2>(acc[mb][nb], as[mb], (nb & 1) ? b1 : b0);
         pin(issue ? 1 : 0);
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of stage s+1 landed
+      stage_end_wait();
       __builtin_amdgcn_s_barrier();                      // everyone's, and stage s fully read
       asm volatile("" ::: "memory");
     }
   } else {   // rows all past M: this wave's share of the pieces and the barriers only
     for (int s = 0; s < nk; ++s) {
-      char* nbase = smem + ((s + 1) & 1) * G::STAGE;
-      const int s_next = min(s + 1, nk - 1);
+      char* nbase = smem + ((s + LOOK) % NS) * G::STAGE;
+      const int s_next = min(s + LOOK, nk - 1);
       if constexpr (!(TM & 2)) {
 #pragma unroll
         for (int k = 0; k < G::NP; ++k) issue_piece(s_next, nbase, k);
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      stage_end_wait();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
-    return;   // no stores: every row of this wave is >= M
   }
+  if constexpr (NS > 2) {   // the last re-fetches still in flight: drained before the LDS is reused
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  if (!live) return;   // no stores: every row of this wave is >= M
   // split-K partial epilogue: 16-row x (176 | 160)-column passes through the wave's LDS area
   char* const lds = smem + wave * FCW_EWAVE;
 #pragma unroll
@@ -1282,7 +1328,7 @@ struct FcGroup {
 // 250): they idle for the rest of the launch (SQ busy 3.48 of 4 per cycle against 3.89 in the direct
 // FC1; FC1 13.0 -> 12.2 ms per step with rr).  Blocks past the last M tile exit.  The masked in-place
 // alt launches keep rr 0 (measured slower with rr: 1.44 -> 1.90 ms per step).
-template <int TM, int NB>
+template <int TM, int NB, int NS = 2>
 __device__ __forceinline__ void fc_h3k_body(const FcGroup& g, char* smem) {
   const unsigned nblk = gridDim.x, bid = blockIdx.x;
   int k = 0, mt, nt;
@@ -1305,8 +1351,8 @@ __device__ __forceinline__ void fc_h3k_body(const FcGroup& g, char* smem) {
   if (d.mask && !(d.mask[mt] & 1u)) return;
   const int n0 = nt * 16 * NB;
   constexpr int ROW_KB = 128;
-  fc_h3w_tile<TM, NB>(d.A, d.a_rows, d.a_off, 0, 0, d.M, d.Bp + (long long)n0 * g.kb_total * ROW_KB, g.kb_total, d.nk,
-                      d.C, g.ldc, g.n_store, (long long)mt * X6P_BM, n0, smem);
+  fc_h3w_tile<TM, NB, NS>(d.A, d.a_rows, d.a_off, 0, 0, d.M, d.Bp + (long long)n0 * g.kb_total * ROW_KB, g.kb_total,
+                          d.nk, d.C, g.ldc, g.n_store, (long long)mt * X6P_BM, n0, smem);
 }
 
 template <int TM = 0>
@@ -1317,8 +1363,8 @@ __global__ __launch_bounds__(512, 1) void beluga_fc_h3k(FcGroup g) {
 
 // the same grouped launch on 112-column tiles (per-window forwards of small batches; same bits)
 __global__ __launch_bounds__(512, 1) void beluga_fc_h3k_narrow(FcGroup g) {
-  __shared__ __attribute__((aligned(1024))) char smem[2 * FcwGeo<7>::STAGE];
-  fc_h3k_body<0, 7>(g, smem);
+  __shared__ __attribute__((aligned(1024))) char smem[3 * FcwGeo<7>::STAGE];
+  fc_h3k_body<0, 7, 3>(g, smem);
 }
 
 // ---- f16x3 conv GEMM with the Toeplitz A tile staged once per channel chunk -------------
@@ -1902,21 +1948,6 @@ __device__ __forceinline__ void conv12_producer(const GemmArgs& p, char* smem, l
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (!(vmax < 65504.f)) *p.ovf = 1;   // conv1 value out of fp16 range: recomputed (bf16x6)
-}
-
-// s_waitcnt vmcnt(N) for the compile-time piece counts of the conv producers
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  if constexpr (N == 2)
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else if constexpr (N == 4)
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 5)
-    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-  else if constexpr (N == 10)
-    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-  else
-    static_assert(N == 2, "vmcnt value");
 }
 
 template <int LAYER, int EPI, int TM, int NSB, int NB = 10>
