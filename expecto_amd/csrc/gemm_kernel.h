@@ -1100,7 +1100,8 @@ __device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_r
     if constexpr ((TM & 8) != 0) s = 0;
     if (k < 4) {
       // (the narrow tiles of small batches only: the wide kernel's schedule stays branch-free)
-      if (NB == FCW_NB || ((alive >> k) & 1u)) glds16(asrc[k] + (long long)((TM & 16) ? 0 : s) * ROW_KB, base + adst[k]);
+      if (NB == FCW_NB || ((alive >> k) & 1u))
+        glds16(asrc[k] + (long long)((TM & 16) ? 0 : s) * ROW_KB, base + adst[k]);
     } else
       __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + bdst[k - 4]), 16, boff[k - 4],
                                                (unsigned)(((TM & 32) ? 0 : s) * ROW_KB), 0, 0);
