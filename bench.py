@@ -83,12 +83,6 @@ def conv2_table_on(precision: str = "f16x3") -> bool:
     return precision in ("f16x3", "bf16x6") and os.environ.get("EXPECTO_CONV2_TABLE", "1") != "0"
 
 
-def conv_karatsuba_on(precision: str = "f16x3") -> bool:
-    """conv3 / conv4 as pair Karatsuba GEMMs (f16x3, opt-in EXPECTO_CONV_KARATSUBA=1; the default runs
-    them direct): 13 instead of 16 K blocks per output pair (beluga_conv_h3k)."""
-    return precision == "f16x3" and os.environ.get("EXPECTO_CONV_KARATSUBA", "0") == "1"
-
-
 def fc1_karatsuba_on(precision: str = "f16x3") -> bool:
     """FC1 as the block-Karatsuba convolution (the library default for f16x3; EXPECTO_FC1_KARATSUBA=0
     runs the direct split-K FC1): 9 block products per 4 windows instead of 16 on the headline."""
@@ -133,8 +127,6 @@ def kernel_name(layer: str, precision: str, segments: bool = True) -> str:
             return "beluga_fc_h3k"                         # FC1 products + tail: one grouped launch
         if l in (7, 8):   # split-K FC GEMMs on 336-column tiles (beluga_fc_h3w)
             return f"beluga_fc_h3w<{l}, {e}, 0>"
-        if layer in ("conv3", "conv4") and conv_karatsuba_on(precision):
-            return f"beluga_conv_h3k<{l}, {e}>"             # pair Karatsuba, 128-pair x 160 tiles
         if layer == "conv2" and os.environ.get("EXPECTO_FUSE_CONV1", "1") != "0":
             return f"beluga_conv_h3p<{l}, {e}, 16640, 4>"   # conv1 fused into the producers (256 | 16384)
         return f"beluga_conv_h3p<{l}, {e}, 256, 4>"   # producer / consumer 256-row tiles (every conv layer)
@@ -401,20 +393,42 @@ def products_and_peak(precision):
     return 1, FP32_MFMA_PEAK_TFLOPS
 
 
-def roofline(layers, precision, segments=True):
+CONV_LAYERS = ("conv2", "conv3", "conv4", "conv5", "conv6")
+
+
+def main_launches(eng):
+    """{conv layer: (rows, ms, launches, MACs)} of its full-size GEMM launches alone, timed while
+    profiling (include/expecto_hip.h expecto_beluga_main_launches)."""
+    return {k: eng.main_launches(k) for k in CONV_LAYERS}
+
+
+def roofline(layers, precision, segments=True, main=None):
     """MFMA roofline of the dominant GEMM kernel from executed work per launch (library counts)
-    and its average launch duration (HIP events on the launch stream)."""
+    over its average launch duration (HIP events on the launch stream).  For a conv layer the
+    figure is taken over its FULL-SIZE launches alone (`main`: the GEMM launch without the pool2
+    pass that shares conv4's slot, nor the small alt-delta launches; the rocprofv3 launch_groups.csv
+    row of the largest grid times the same launches); the slot's all-launch figure stands beside it."""
     gemm = [k for k in GEMM_LAYER_EPI if not (k == "conv2" and conv2_table_on(precision))]
     dom = max(gemm, key=lambda k: layers[k][0])   # (the f16x3 conv2 is a gather: conv2_table_roofline)
     ms, calls, macs = layers[dom]
+    mult, peak = products_and_peak(precision)
+    all_tflops = 2.0 * macs / calls / (ms / calls / 1e3) / 1e12
+    all_launches = {"avg_launch_ms": ms / calls, "launches": calls, "fp32_tflops": all_tflops,
+                    "frac": mult * all_tflops / peak,
+                    "what": "every launch of the layer slot, HIP events around the layer (conv4: + its pool2 pass)"}
+    rows = 0
+    if main and dom in main and main[dom][2] > 0:
+        rows, ms, calls, macs = main[dom]
     fp32_flops_launch = 2.0 * macs / calls
     fp32_tflops = fp32_flops_launch / (ms / calls / 1e3) / 1e12
-    mult, peak = products_and_peak(precision)
     achieved = mult * fp32_tflops
     return {"bound": "mfma", "kernel": kernel_name(dom, precision, segments), "layer": dom, "achieved": achieved,
             "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
-            "avg_launch_ms": ms / calls, "launches": calls, "mfma_flops_per_launch": mult * fp32_flops_launch,
-            "fp32_flops_per_launch": fp32_flops_launch, "fp32_tflops": fp32_tflops, "precision": precision}
+            "avg_launch_ms": ms / calls, "launches": calls, "rows_per_launch": rows or None,
+            "timed": "full-size launches alone" if rows else "every launch of the slot",
+            "mfma_flops_per_launch": mult * fp32_flops_launch,
+            "fp32_flops_per_launch": fp32_flops_launch, "fp32_tflops": fp32_tflops, "precision": precision,
+            "all_launches": all_launches}
 
 
 def profile_key(n=None, precision="f16x3"):
@@ -422,8 +436,7 @@ def profile_key(n=None, precision="f16x3"):
     its PMC numbers to be attached to this bench line."""
     return {"workload": "sed200", "variants": N200 if n is None else n, "precision": precision,
             "max_batch": MAX_BATCH, "genome": "repeat-rich",
-            "fc1": "karatsuba" if fc1_karatsuba_on(precision) else "direct",
-            **({"conv34": "karatsuba"} if conv_karatsuba_on(precision) else {})}
+            "fc1": "karatsuba" if fc1_karatsuba_on(precision) else "direct"}
 
 
 def pmc_traffic(key, kernel):
@@ -489,9 +502,10 @@ def measure(step, eng, n_units, steps, warmup, world, dev, prof_steps=2, segment
     """(units/s, ms/step, fallbacks, layers, roofline, executed MACs per step)."""
     el, fb = time_steps(step, eng, steps, warmup, world, dev)
     layers = profile_layers(step, eng, prof_steps)
+    main = main_launches(eng)
     exec_macs = sum(m for _, _, m in layers.values()) / prof_steps
     return {"units_per_s": world * n_units * steps / el, "ms_per_step": el / steps * 1e3, "fallbacks": fb,
-            "layers": layers, "roofline": roofline(layers, eng.precision, segments), "exec_macs_step": exec_macs,
+            "layers": layers, "roofline": roofline(layers, eng.precision, segments, main), "exec_macs_step": exec_macs,
             "prof_steps": prof_steps}
 
 

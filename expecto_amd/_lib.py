@@ -31,7 +31,6 @@ SIGNATURES = {
     "expecto_beluga_device_bytes": (ctypes.c_size_t, [c_vp]),
     "expecto_beluga_conv2_table_active": (ctypes.c_int, [c_vp, c_i32p]),
     "expecto_beluga_set_fc1_role": (ctypes.c_int, [c_vp, ctypes.c_int]),
-    "expecto_beluga_set_conv_role": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "expecto_beluga_forward_onehot": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, c_vp, c_vp]),
     "expecto_beluga_forward_codes": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_longlong, ctypes.c_int,
                                                     c_vp, c_vp]),
@@ -54,6 +53,7 @@ SIGNATURES = {
     "expecto_beluga_count_fallback": (ctypes.c_int, [c_vp]),
     "expecto_beluga_set_profiling": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "expecto_beluga_layer_times": (ctypes.c_int, [c_vp, c_f64p, c_i64p, c_f64p, ctypes.c_int]),
+    "expecto_beluga_main_launches": (ctypes.c_int, [c_vp, ctypes.c_int, c_i64p, c_f64p, c_i64p, c_f64p]),
     "expecto_variant_windows": (ctypes.c_int, [c_vp, ctypes.c_longlong, c_vp, c_vp, c_vp, ctypes.c_int, c_vp,
                                                ctypes.c_int, c_vp, c_vp]),
     "expecto_indel_windows": (ctypes.c_int, [c_vp, ctypes.c_longlong, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,

@@ -74,16 +74,11 @@ class BelugaEngine:
         self.precision = precision
 
     def set_fc1_role(self, role: int):
-        """Block-Karatsuba FC1 role (0..3) of this engine's per-window forwards (include/expecto_hip.h
-        expecto_beluga_set_fc1_role): a segment-path window of role r equals a per-window forward
-        in role r bit for bit (pipeline.fc1_role gives a segment window's role)."""
+        """FC1 role of this engine's per-window forwards (include/expecto_hip.h
+        expecto_beluga_set_fc1_role): 4 = the direct FC1 (default, the form of +-800 sweeps), 0..3 =
+        block-Karatsuba roles; a segment-path window of role r equals a per-window forward in role r
+        bit for bit (pipeline.fc1_role / sweep_roles give a segment window's role)."""
         _lib.check(self.lib.expecto_beluga_set_fc1_role(self.handle, int(role)), "set_fc1_role")
-
-    def set_conv_role(self, role: int):
-        """conv3 / conv4 form of this engine's per-window forwards (include/expecto_hip.h
-        expecto_beluga_set_conv_role): 0 pair Karatsuba (default), 1 direct.  A forward_segments
-        call equals per-window forwards in role pipeline.conv_role(...) bit for bit."""
-        _lib.check(self.lib.expecto_beluga_set_conv_role(self.handle, int(role)), "set_conv_role")
 
     def set_f16_target(self, target_log2: int):
         """f16x3 calibration target: the largest calibration activation maps to 2^target_log2."""
@@ -278,6 +273,16 @@ class BelugaEngine:
         if n < 0:
             _lib.check(n, "layer_times")
         return {_lib.LAYER_NAMES[i]: (ms[i], calls[i], macs[i]) for i in range(_lib.N_LAYERS)}
+
+    def main_launches(self, layer: str):
+        """(rows, device ms, launches, executed multiply-adds) of the layer's full-size conv GEMM
+        launches alone (include/expecto_hip.h expecto_beluga_main_launches), accumulated while
+        profiling; rows 0 if none ran."""
+        rows, ms, calls, macs = ctypes.c_longlong(), ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double()
+        _lib.check(self.lib.expecto_beluga_main_launches(self.handle, _lib.LAYER_NAMES.index(layer), ctypes.byref(rows),
+                                                         ctypes.byref(ms), ctypes.byref(calls), ctypes.byref(macs)),
+                   "main_launches")
+        return rows.value, ms.value, calls.value, macs.value
 
     def device_bytes(self) -> int:
         """Device bytes of the handle; shared k-mer tables count only for their first holder."""

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -482,18 +483,14 @@ __global__ void seg_a_rows(const int* __restrict__ win_seg, const int* __restric
 //   layer    changed rows (from the previous run)          W     input rows (A patch)
 //   conv1    [p-7, p]                                      8     15 codes
 //   conv2+p  pooled [floor((r1-7)/4), floor((r1+7)/4)]     5     4*5+7 -> 28
-//   conv3    [r2-7, r2+5] in [r3, r3+14), r3 even          14    22
-//   conv4+p  pooled [floor((r3-7)/4), floor((r3+13)/4)]    6     4*6+7 -> 32
+//   conv3    [r2-7, r2+4]                                  12    19
+//   conv4+p  pooled [floor((r3-7)/4), floor((r3+11)/4)]    6     4*6+7 -> 32
 //   conv5    [r4-7, r4+5]                                  13    20
 //   conv6    [r5-7, r5+12]                                 20    27
 // Each start is clamped to [0, T_l - W_l] (T_l = valid rows of layer l), which keeps the run
-// inside the layer and still covers every changed row.  conv3 / conv4 run as pair Karatsuba GEMMs
-// (beluga_conv_h3k): a patch's output pairs (2p, 2p+1) must be the full run's pairs (runs start on
-// even rows, patches hold an even row count), and the odd output of a pair also depends, through
-// rounding, on the pair's even input row (its S and U products hold w_0 x[2p] with opposite signs),
-// so a changed even input row r changes outputs [r-7, r+1]: conv3's run covers r2+5 too (14 rows).
-constexpr int kDW[7] = {0, 8, 5, 14, 6, 13, 20};         // W_l, l = 1..6
-constexpr int kDA[7] = {0, 15, 28, 22, 32, 20, 27};      // input rows of the layer-l patch
+// inside the layer and still covers every changed row.
+constexpr int kDW[7] = {0, 8, 5, 12, 6, 13, 20};         // W_l, l = 1..6
+constexpr int kDA[7] = {0, 15, 28, 19, 32, 20, 27};      // input rows of the layer-l patch
 constexpr int kDT[7] = {0, 1993, 496, 489, 120, 113, 106};
 constexpr int kDC[7] = {4, 320, 320, 480, 480, 640, 640};  // channels of layer l's output
 
@@ -504,14 +501,13 @@ struct DeltaRows {
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 __device__ __forceinline__ int floor4(int v) { return v >= 0 ? v >> 2 : -((3 - v) >> 2); }
-__device__ __forceinline__ int floor2(int v) { return v & ~1; }   // even, <= v (two's complement)
 
 __device__ __forceinline__ DeltaRows delta_rows(int p) {
   DeltaRows d;
   d.r[0] = p;
   d.r[1] = clampi(p - 7, 0, kDT[1] - kDW[1]);
   d.r[2] = clampi(floor4(d.r[1] - 7), 0, kDT[2] - kDW[2]);
-  d.r[3] = clampi(floor2(d.r[2] - 7), 0, (kDT[3] - kDW[3] + 1) & ~1);   // 476: rows up to 489
+  d.r[3] = clampi(d.r[2] - 7, 0, kDT[3] - kDW[3]);
   d.r[4] = clampi(floor4(d.r[3] - 7), 0, kDT[4] - kDW[4]);
   d.r[5] = clampi(d.r[4] - 7, 0, kDT[5] - kDW[5]);
   d.r[6] = clampi(d.r[5] - 7, 0, kDT[6] - kDW[6]);
@@ -616,12 +612,10 @@ __global__ __launch_bounds__(256) void pair_patch_apply(const float* __restrict_
 // above; conv4 is unpooled on the segment path, so its run is the 19 rows [r4u, r4u+19); each
 // pool2 phase p then changes <= 6 pooled rows [r4p, r4p+6) and conv5 / conv6 runs follow per
 // (segment, phase) block.  Starts are clamped with the phase-0 (longest) geometry, like the
-// ref blocks; rows past a phase's valid length are never read by any window.  conv3's and conv4's
-// runs start on even rows (pair Karatsuba GEMMs); their upper clamps round up to even, so a run
-// may compute one row past the layer's valid rows (from the rows the padded strides P1s / T3s hold).
+// ref blocks; rows past a phase's valid length are never read by any window.
 // Per-segment table (kSegTab ints): q', r1, r2, r3, r4u, r4p[4], r5[4], r6[4].
 constexpr int kSegTab = 20;
-constexpr int kW4u = 22, kA4u = 30;   // conv4 run [floor2(r3 - 7), +22) covers [r3 - 7, r3 + 14)
+constexpr int kW4u = 19, kA4u = 26;   // conv4 run [r3 - 7, r3 + 12): the 12 changed conv3 rows' reach
 struct SegDims {
   int L, T1, P1, T3, T4, S5, T5, T6;
 };
@@ -635,8 +629,8 @@ __global__ void seg_delta_table(const int* __restrict__ var_pos, int s0, int ns,
   int* t = tab + m * kSegTab;
   const int r1 = clampi(q - 7, 0, g.T1 - kDW[1]);
   const int r2 = clampi(floor4(r1 - 7), 0, g.P1 - kDW[2]);
-  const int r3 = clampi(floor2(r2 - 7), 0, (g.T3 - kDW[3] + 1) & ~1);
-  const int r4 = clampi(floor2(r3 - 7), 0, (g.T4 - kW4u + 1) & ~1);
+  const int r3 = clampi(r2 - 7, 0, g.T3 - kDW[3]);
+  const int r4 = clampi(r3 - 7, 0, g.T4 - kW4u);
   t[0] = q;
   t[1] = r1;
   t[2] = r2;
@@ -644,9 +638,8 @@ __global__ void seg_delta_table(const int* __restrict__ var_pos, int s0, int ns,
   t[4] = r4;
   for (int i = 0; i < n_ph; ++i) {
     const int p = i == 0 ? ph.x : i == 1 ? ph.y : i == 2 ? ph.z : ph.w;
-    // pooled rows g of phase p read conv4 rows p+4g .. p+4g+3; the changed conv4 rows lie in
-    // [r3 - 7, r3 + 13] (inside the run [r4, r4 + 22)): 6 pooled rows of any phase
-    const int r4p = clampi(floor4(r3 - 7 - p), 0, g.S5 - kDW[4]);
+    // pooled rows g of phase p read conv4 rows p+4g .. p+4g+3: the changed ones meet [r4, r4+19)
+    const int r4p = clampi(floor4(r4 - p), 0, g.S5 - kDW[4]);
     const int r5 = clampi(r4p - 7, 0, g.T5 - kDW[5]);
     t[5 + i] = r4p;
     t[9 + i] = r5;
@@ -911,9 +904,25 @@ __global__ __launch_bounds__(320) void fk_seq_h2(const float* __restrict__ x, in
       h[e] = a;
       l[e] = b;
     }
-    char* d = reinterpret_cast<char*>(dst) + base + row * rb;
-    *reinterpret_cast<halfx8*>(d) = h;
-    *reinterpret_cast<halfx8*>(d + 64) = l;
+    // Full-line stores: the 8 lanes of a lane octet (c8 = 8m .. 8m+7, one row) own channel groups
+    // 2m' and 2m'+1 (4 eight-channel quarters each).  Each keeps one plane and trades the other with
+    // its mirror lane j <-> 7 - j (DPP row_half_mirror): the low half keeps hi, the high half keeps
+    // lo.  Then one store instruction writes group 2m' as whole 128-B lines [hi q0..q3 | lo q0..q3]
+    // and the next group 2m'+1 -- instead of two half-line stores per group (the same bytes).
+    const int j = c8 & 7;
+    const bool low = j < 4;
+    u32x4 send = __builtin_bit_cast(u32x4, low ? l : h), recv;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) recv[w] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)send[w], 0x141, 0xf, 0xf, false);
+    const u32x4 keep = __builtin_bit_cast(u32x4, low ? h : l);
+    char* d = reinterpret_cast<char*>(dst) + blk * s * rb + row * rb + (c8 >> 3) * 256;
+    if (low) {   // hi quarter j of group 2m' (own), hi quarter 3 - j of group 2m'+1 (mirror's)
+      *reinterpret_cast<u32x4*>(d + j * 16) = keep;
+      *reinterpret_cast<u32x4*>(d + 128 + (3 - j) * 16) = recv;
+    } else {     // lo quarter 7 - j of group 2m' (mirror's), lo quarter j - 4 of group 2m'+1 (own)
+      *reinterpret_cast<u32x4*>(d + 64 + (7 - j) * 16) = recv;
+      *reinterpret_cast<u32x4*>(d + 128 + 64 + (j - 4) * 16) = keep;
+    }
   };
   float v0[8], v1[8], v2[8] = {}, v3[8] = {};
   ld(r, v0);
@@ -1076,30 +1085,6 @@ __global__ void repack_conv(const float* __restrict__ W, int cout, int cin, int 
   const int k = (int)(i % K);  // kernel K order [ci/32][tap][ci%32] (cin is a multiple of 32)
   const int chunk = k / (8 * GBK), tap = (k / GBK) % 8, ci = chunk * GBK + k % GBK;
   Wt[i] = n < cout ? W[((long long)n * cin + ci) * 8 + tap] : 0.f;
-}
-
-// Weights of the pair Karatsuba conv (gemm_kernel.h beluga_conv_h3k) from the repacked conv weights
-// Wt [npad][8 Cin] (K order [ci/32][tap][ci%32]), in the kernel's step order: S (chunk, i < 4) w_2i,
-// U (chunk, i < 5) w_2i-1 - w_2i, V (chunk, i < 4) w_2i+1 - w_2i (w_-1 = w_8 = 0); K = 13 Cin.
-// Sums in fp64, rounded once.
-__global__ void ck_weights(const float* __restrict__ Wt, long long rows, int cin, float* __restrict__ out) {
-  const int nch = cin / 32, K = 13 * cin;
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= rows * K) return;
-  const long long n = i / K;
-  const int k = (int)(i - n * K), kb = k >> 5, j = k & 31;
-  int c, t, ph;
-  if (kb < 4 * nch) {
-    ph = 0, c = kb >> 2, t = kb & 3;
-  } else if (kb < 9 * nch) {
-    ph = 1, c = (kb - 4 * nch) / 5, t = (kb - 4 * nch) % 5;
-  } else {
-    ph = 2, c = (kb - 9 * nch) >> 2, t = (kb - 9 * nch) & 3;
-  }
-  const float* w = Wt + n * 8 * cin + (long long)c * 256 + j;
-  auto tap = [&](int q) { return q < 0 || q > 7 ? 0.0 : (double)w[q * 32]; };
-  const double v = ph == 0 ? tap(2 * t) : ph == 1 ? tap(2 * t - 1) - tap(2 * t) : tap(2 * t + 1) - tap(2 * t);
-  out[i] = (float)v;
 }
 
 __global__ void repack_conv1(const float* __restrict__ w1, float* __restrict__ out) {
@@ -1580,7 +1565,7 @@ struct expecto_beluga {
   bool kmer_quad = true;              //   conv2 rows from the quad tables (EXPECTO_KMER_QUAD=0: pair tables only)
   int kmer_state = 1;                 //   0 held, 1 off (EXPECTO_CONV2_TABLE=0), 2 no room (conv2_table_active)
   bool fk_on = true;                  // f16x3 FC1 as a block-Karatsuba convolution (EXPECTO_FC1_KARATSUBA)
-  int fk_role = 0;                    //   role of per-window forwards (EXPECTO_FC1_ROLE, 0..3; 4 = direct FC1)
+  int fk_role = 4;                    //   role of per-window forwards (EXPECTO_FC1_ROLE; 4 = direct FC1, the default; 0..3 Karatsuba)
   float* fkw = nullptr;               //   the 9 products' + tail weight planes [npad][kFkKbTotal][2][32] fp16
   int* fk_sw = nullptr;               //   their per-row scale exponents
   float* fk_cs = nullptr;             //   column unscale 2^-(sx[5] + fk_sw[n])
@@ -1605,13 +1590,6 @@ struct expecto_beluga {
   int* fk_aprow = nullptr;
   int* fk_aperm = nullptr;
   unsigned* fk_smask = nullptr;
-  bool ck_on = false;                 // f16x3 conv3 / conv4 as pair Karatsuba GEMMs (EXPECTO_CONV_KARATSUBA=1; parity;
-                                      //   off by default: measured slower, DESIGN.md "conv3 / conv4 as pair Karatsuba")
-  int ck_role = 0;                    //   per-window forwards: 0 pairs, 1 direct (expecto_beluga_set_conv_role)
-  bool ck_call_direct = false;        //   this forward_segments call has windows on odd pool1 rows: direct
-  float* ckw[5] = {};                 //   weight planes in step order [npad][13 Cin/32][2][32] (conv3, conv4)
-  int* ck_sw[5] = {};                 //   their per-row exponents and column unscales 2^-(sx[l] + ck_sw[n])
-  float* ck_cs[5] = {};
   bool onehot_as_codes = true;        // forward_onehot: exact one-hot input through the k-mer gather (EXPECTO_ONEHOT_CODES)
   uint8_t* oh_codes = nullptr;        //   its codes, max_batch x 2000 (allocated on first use)
   int* oh_bad = nullptr;              //   its check flag
@@ -1625,6 +1603,16 @@ struct expecto_beluga {
   double ms[2 * kNumLayers] = {};
   long long calls[2 * kNumLayers] = {};
   double macs[2 * kNumLayers] = {};  // executed multiply-adds per slot while profiling (host-side count)
+  // the conv GEMM launches alone (no pool2 pass in the slot), per (layer slot, rows): bench.py's
+  // roofline takes the group with the most rows, i.e. the full-size launches
+  struct LaunchRec {
+    int layer;
+    long long rows;
+    int idx;
+    double macs;
+  };
+  std::vector<LaunchRec> pending_launch;
+  std::map<std::pair<int, long long>, std::array<double, 3>> launch_stats;   // ms, calls, macs
 };
 
 namespace {
@@ -1826,9 +1814,40 @@ int resolve_events(expecto_beluga* h) {
     h->calls[pr.first] += 1;
   }
   h->pending.clear();
+  for (auto& r : h->pending_launch) {
+    EXPECTO_HIP_CHECK(hipEventSynchronize(h->ev_pool[r.idx + 1]));
+    float ms = 0.f;
+    EXPECTO_HIP_CHECK(hipEventElapsedTime(&ms, h->ev_pool[r.idx], h->ev_pool[r.idx + 1]));
+    auto& a = h->launch_stats[{r.layer, r.rows}];
+    a[0] += ms;
+    a[1] += 1;
+    a[2] += r.macs;
+  }
+  h->pending_launch.clear();
   h->ev_next = 0;
   return EXPECTO_OK;
 }
+
+// Times ONE GEMM launch (its own event pair, beside the layer slot's) for the per-launch log.
+struct LaunchTimer {
+  expecto_beluga* h;
+  int idx = -1;
+  hipStream_t st;
+  expecto_beluga::LaunchRec rec;
+  LaunchTimer(expecto_beluga* hh, int layer, long long rows, double macs, hipStream_t s) : h(hh), st(s) {
+    if (!h->profiling) return;
+    if (h->ev_next + 2 > h->ev_pool.size()) resolve_events(h);
+    idx = (int)h->ev_next;
+    h->ev_next += 2;
+    rec = {h->timer_base + layer, rows, idx, macs};
+    (void)hipEventRecord(h->ev_pool[idx], st);
+  }
+  ~LaunchTimer() {
+    if (idx < 0) return;
+    (void)hipEventRecord(h->ev_pool[idx + 1], st);
+    h->pending_launch.push_back(rec);
+  }
+};
 
 struct LayerTimer {
   expecto_beluga* h;
@@ -2025,60 +2044,11 @@ int run_conv2_kmer(expecto_beluga* h, const C1Src& f, long long n_win, int rows,
   return check_launch("conv2_kmer_pool");
 }
 
-// conv3 (l 1) / conv4 (l 2) as pair Karatsuba GEMMs (f16x3): 13 instead of 16 K blocks per output
-// pair, gemm_kernel.h beluga_conv_h3k.  Output pairs are rows (2p, 2p+1) of a launch's flattened
-// rows, so every caller keeps s_in even and a window's rows on the same parity in every path
-// (per-window: row 0; segments: the window's pool1 row offset, even unless ck_call_direct).
-bool ck_use(const expecto_beluga* h, int l) {
-  return (l == 1 || l == 2) && h->ckw[l] && h->ck_on && h->ck_role == 0 && !h->ck_call_direct &&
-         g_precision == EXPECTO_PRECISION_F16X3;
-}
-
-template <int LAYER, int EPI>
-int launch_conv_k(const GemmArgs& a, hipStream_t st) {
-  const long long nblk = a.m_tiles * a.n_tiles;
-  EXPECTO_REQUIRE(nblk > 0 && nblk < (1LL << 31), "conv grid out of range");
-  EXPECTO_REQUIRE(a.lda % GBK == 0 && a.ldb == 13 * a.lda && a.Bp && a.col_scale, "Karatsuba conv operands");
-  EXPECTO_REQUIRE(a.M % 2 == 0 && a.s_in % 2 == 0 && a.m_tiles * CK_PAIRS * 2 >= a.M, "Karatsuba conv pairs");
-  beluga_conv_h3k<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
-  return check_launch("beluga_conv_h3k");
-}
-
 // conv layer l (0 = conv2 .. 4 = conv6) over `groups` row groups of s_in rows each.  f1 (conv2
 // only): compute conv1 from these codes inside the conv2 launch instead of reading src.
 int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long groups, int s_in, int t_valid,
              int s_out, bool pool, hipStream_t st, const C1Src* f1 = nullptr) {
   const ConvGeo& g = kConv[l];
-  if (!f1 && ck_use(h, l)) {
-    EXPECTO_REQUIRE(s_in % 2 == 0, "pair Karatsuba conv: rows per group must be even");
-    GemmArgs a{};
-    a.A = src;
-    a.lda = g.cin;
-    a.M = groups * s_in;
-    a.Bp = h->ckw[l];
-    a.col_scale = h->ck_cs[l];
-    a.out_scale = exp2i(h->sx[l + 1]);
-    a.ovf = h->ovf;
-    a.ldb = 13LL * g.cin;
-    a.kper = (int)a.ldb;
-    a.taps = 8;
-    a.n_tiles = npad_of(g.cout) / GBN;
-    a.m_tiles = (a.M / 2 + CK_PAIRS - 1) / CK_PAIRS;
-    a.bias = h->bt[l];
-    a.C = dst;
-    a.ldc = g.cout;
-    a.n_store = g.cout;
-    a.s_in = s_in;
-    a.t_valid = t_valid;
-    a.s_out = s_out;
-    LayerTimer lt(h, l + 1, st);
-    if (h->profiling) h->macs[h->timer_base + l + 1] += (double)(a.M / 2) * g.cout * a.ldb;   // executed MACs
-    if (pool) {
-      EXPECTO_REQUIRE(s_in % 4 == 0 && l == 2, "pool epilogue needs 4-aligned row groups");
-      return launch_conv_k<4, EPI_RELU_POOL4>(a, st);
-    }
-    return l == 1 ? launch_conv_k<3, EPI_RELU>(a, st) : launch_conv_k<4, EPI_RELU>(a, st);
-  }
   GemmArgs a{};
   a.A = src;
   a.lda = g.cin;
@@ -2127,6 +2097,7 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
   }
   LayerTimer lt(h, l + 1, st);
   if (h->profiling) h->macs[h->timer_base + l + 1] += (double)a.M * g.cout * a.kper;
+  LaunchTimer lrec(h, l + 1, a.M, (double)a.M * g.cout * a.kper, st);
   if (pool) {
     EXPECTO_REQUIRE(s_in % 4 == 0, "pool epilogue needs 4-aligned row groups");
     return l == 0 ? launch_gemm<2, EPI_RELU_POOL4>(a, 1, st, bm) : launch_gemm<4, EPI_RELU_POOL4>(a, 1, st, bm);
@@ -2676,7 +2647,6 @@ int ensure_delta(expecto_beluga* h) {
 // and K order as the per-window path, so results are bit-identical to it.
 struct SegGeo {
   int L, T1, S1, P1, T3, T4, S5, T5, T6;
-  int P1s, T3s;   // row strides of pool1 / conv3 per segment: even (conv3 / conv4 pair GEMMs), >= one spare row
   size_t p_rows_floats, q_rows_floats;  // per segment, given n_ph phases
 };
 
@@ -2691,11 +2661,9 @@ SegGeo seg_geo(int L, int n_ph) {
   g.S5 = g.T4 / 4;        // rows of the phase-0 pool2 block (the longest)
   g.T5 = g.S5 - 7;
   g.T6 = g.T5 - 7;
-  g.P1s = (g.P1 + 2) & ~1;
-  g.T3s = (g.T3 + 2) & ~1;
-  const size_t p_conv1 = (size_t)g.S1 * 320, p_conv3 = (size_t)g.T3s * 480, p_pool2 = (size_t)n_ph * g.S5 * 480,
+  const size_t p_conv1 = (size_t)g.S1 * 320, p_conv3 = (size_t)g.T3 * 480, p_pool2 = (size_t)n_ph * g.S5 * 480,
                p_conv6 = (size_t)n_ph * g.T6 * 640;
-  const size_t q_pool1 = (size_t)g.P1s * 320, q_conv4 = (size_t)g.T4 * 480, q_conv5 = (size_t)n_ph * g.T5 * 640;
+  const size_t q_pool1 = (size_t)g.P1 * 320, q_conv4 = (size_t)g.T4 * 480, q_conv5 = (size_t)n_ph * g.T5 * 640;
   g.p_rows_floats = std::max(std::max(p_conv1, p_conv3), std::max(p_pool2, p_conv6));
   g.q_rows_floats = std::max(q_pool1, std::max(q_conv4, q_conv5));
   return g;
@@ -2736,14 +2704,6 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
       ph_idx[p] = n_ph;
       ph[n_ph++] = p;
     }
-  // conv3 / conv4 output pairs are (even, odd) pool1 rows of the segment: a window on an odd pool1
-  // row (phase 1 or 3) would see the other pairing than its per-window forward, so such a call
-  // runs conv3 / conv4 direct (the per-window forwards' conv role 1: pipeline.conv_role).
-  struct CallDirect {
-    bool& f;
-    CallDirect(bool& ff, bool v) : f(ff) { f = v; }
-    ~CallDirect() { f = false; }
-  } ck_direct(h->ck_call_direct, present[1] || present[3]);
   const SegGeo g = seg_geo(L, std::max(n_ph, 1));
   const size_t p_cap = p_floats(h->max_batch) - 16 * 640, q_cap = q_floats(h->max_batch) - 16 * 640;
   const int seg_cap = (int)std::min<size_t>(p_cap / g.p_rows_floats, q_cap / g.q_rows_floats);
@@ -2978,9 +2938,9 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
       if (pr && !kmer && !fuse && (rc = alt_asm(0, h->P, g.S1, h->D0, kDW[1], 1, 2, 4, 1, kDA[2], h->pev[1], h->pev[2])))
         return rc;
       if (kmer)
-        rc = run_conv2_kmer(h, f1, ns, g.P1, g.P1s, h->Q, st);
+        rc = run_conv2_kmer(h, f1, ns, g.P1, g.P1, h->Q, st);
       else
-        rc = run_conv(h, 0, h->P, h->Q, ns, g.S1, g.P1, g.P1s, true, st, fuse ? &f1 : nullptr);
+        rc = run_conv(h, 0, h->P, h->Q, ns, g.S1, g.P1, g.P1, true, st, fuse ? &f1 : nullptr);
       if (rc) return rc;
       if (pr && kmer) {   // alt pooled conv2 rows [r2, r2 + kDW[2]) of each segment into D1
         DeltaScope ds(h);
@@ -2989,11 +2949,11 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
       } else if (pr && ((!fuse && (rc = st_wait(h->pev[2]))) || (rc = alt_gemm(0, 1, kDA[2], kDW[2], true, h->D1)))) {
         return rc;
       }
-      if (pr && (rc = alt_asm(1, h->Q, g.P1s, h->D1, kDW[2], 1, 3, 1, 2, kDA[3], h->pev[3], h->pev[4]))) return rc;
-      if ((rc = run_conv(h, 1, h->Q, h->P, ns, g.P1s, g.T3, g.T3s, false, st))) return rc;
+      if (pr && (rc = alt_asm(1, h->Q, g.P1, h->D1, kDW[2], 1, 3, 1, 2, kDA[3], h->pev[3], h->pev[4]))) return rc;
+      if ((rc = run_conv(h, 1, h->Q, h->P, ns, g.P1, g.T3, g.T3, false, st))) return rc;
       if (pr && ((rc = st_wait(h->pev[4])) || (rc = alt_gemm(1, 1, kDA[3], kDW[3], false, h->D0)))) return rc;
-      if (pr && (rc = alt_asm(2, h->P, g.T3s, h->D0, kDW[3], 1, 4, 1, 3, kA4u, h->pev[5], h->pev[6]))) return rc;
-      if ((rc = run_conv(h, 2, h->P, h->Q, ns, g.T3s, g.T4, g.T4, false, st))) return rc;
+      if (pr && (rc = alt_asm(2, h->P, g.T3, h->D0, kDW[3], 1, 4, 1, 3, kA4u, h->pev[5], h->pev[6]))) return rc;
+      if ((rc = run_conv(h, 2, h->P, h->Q, ns, g.T3, g.T4, g.T4, false, st))) return rc;
       if (pr && ((rc = st_wait(h->pev[6])) || (rc = alt_gemm(2, 1, kA4u, kW4u, false, h->D1)))) return rc;
       {  // pool2 phases (Q -> P)
         LayerTimer lt(h, 3, st);
@@ -3402,12 +3362,6 @@ int f16_col_scales(expecto_beluga* h, hipStream_t st) {
     int rc = check_launch("col_scales");
     if (rc) return rc;
   }
-  for (int g = 1; g <= 2; ++g)   // the pair Karatsuba conv3 / conv4 weights: the layer's input scale
-    if (h->ckw[g]) {
-      col_scales<<<dim3((np[g] + 255) / 256), dim3(256), 0, st>>>(h->ck_sw[g], np[g], h->sx[g], h->ck_cs[g]);
-      int rc = check_launch("col_scales (conv Karatsuba)");
-      if (rc) return rc;
-    }
   if (h->fkw) {   // the Karatsuba FC1 weights: FC1's input scale, their own row exponents
     col_scales<<<dim3((np[5] + 255) / 256), dim3(256), 0, st>>>(h->fk_sw, np[5], h->sx[5], h->fk_cs);
     return check_launch("col_scales (FC1 Karatsuba)");
@@ -3510,25 +3464,6 @@ int f16_prepare(expecto_beluga* h, hipStream_t st) {
                                                     reinterpret_cast<_Float16*>(h->w1h));
     col_scales<<<dim3(2), dim3(256), 0, st>>>(reinterpret_cast<int*>(sw1), 320, 0, h->cs1);
     if ((rc = check_launch("conv1 planes"))) return rc;
-  }
-  if (h->ck_on) {   // conv3 / conv4 pair Karatsuba: S / U / V weights, one exponent per row over all of them
-    for (int g = 1; g <= 2; ++g) {
-      const int np = layers[g].rows, cin = (int)(layers[g].K / 8);
-      const long long tot = (long long)np * 13 * cin;
-      float *wk = nullptr, *swf = nullptr;
-      if ((rc = dalloc(h, &swf, np)) || (rc = dalloc(h, &h->ck_cs[g], np)) || (rc = dalloc(h, &h->ckw[g], (size_t)tot)))
-        return rc;
-      EXPECTO_HIP_CHECK(hipMalloc(&wk, (size_t)tot * sizeof(float)));
-      h->ck_sw[g] = reinterpret_cast<int*>(swf);
-      ck_weights<<<dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st>>>(layers[g].w, np, cin, wk);
-      row_scale_exp<<<dim3(np), dim3(256), 0, st>>>(wk, 13 * cin, h->ck_sw[g]);
-      split_planes_h2<<<dim3((unsigned)((tot / 4 + 255) / 256)), dim3(256), 0, st>>>(
-          wk, np, 13 * cin, h->ck_sw[g], reinterpret_cast<_Float16*>(h->ckw[g]));
-      rc = check_launch("conv Karatsuba weights");
-      (void)hipStreamSynchronize(st);
-      (void)hipFree(wk);
-      if (rc) return rc;
-    }
   }
   if (h->fk_on) {   // FC1 block Karatsuba: the 9 products' weights + the tail, fp64 sums rounded once,
     const int np1 = npad_of(kFc1Out);   // one exponent per row over all of them (a shared column unscale)
@@ -3648,12 +3583,6 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   if (const char* e = getenv("EXPECTO_ONEHOT_CODES")) h->onehot_as_codes = atoi(e) != 0;   // parity, not bits
   if (const char* e = getenv("EXPECTO_FC1_KARATSUBA")) h->fk_on = atoi(e) != 0;       // parity, not bits
   if (const char* e = getenv("EXPECTO_FC1K_SLICE")) h->fk_slice = std::max(1, atoi(e));  // same bits either way
-  if (const char* e = getenv("EXPECTO_CONV_KARATSUBA")) h->ck_on = atoi(e) != 0;      // parity, not bits
-  if (const char* e = getenv("EXPECTO_CONV_ROLE")) {   // per-window forwards' conv3 / conv4 form (tests)
-    const int v = atoi(e);
-    EXPECTO_REQUIRE(v == 0 || v == 1, "EXPECTO_CONV_ROLE must be 0 (pairs) or 1 (direct)");
-    h->ck_role = v;
-  }
   if (const char* e = getenv("EXPECTO_FC1_ROLE")) {    // per-window forwards' Karatsuba role (tests)
     const int v = atoi(e);
     EXPECTO_REQUIRE(v >= 0 && v <= 4, "EXPECTO_FC1_ROLE must be 0..4");
@@ -3747,13 +3676,6 @@ int expecto_beluga_set_fc1_role(expecto_beluga_t h, int role) {
   EXPECTO_REQUIRE(h != nullptr, "null handle");
   EXPECTO_REQUIRE(role >= 0 && role <= 4, "FC1 role must be 0..4");
   h->fk_role = role;
-  return EXPECTO_OK;
-}
-
-int expecto_beluga_set_conv_role(expecto_beluga_t h, int role) {
-  EXPECTO_REQUIRE(h != nullptr, "null handle");
-  EXPECTO_REQUIRE(role == 0 || role == 1, "conv role must be 0 (pairs) or 1 (direct)");
-  h->ck_role = role;
   return EXPECTO_OK;
 }
 
@@ -3972,7 +3894,25 @@ int expecto_beluga_set_profiling(expecto_beluga_t h, int on) {
     std::fill(h->ms, h->ms + 2 * kNumLayers, 0.0);
     std::fill(h->calls, h->calls + 2 * kNumLayers, 0LL);
     std::fill(h->macs, h->macs + 2 * kNumLayers, 0.0);
+    h->launch_stats.clear();
   }
+  return EXPECTO_OK;
+}
+
+int expecto_beluga_main_launches(expecto_beluga_t h, int slot, long long* rows, double* ms, long long* calls,
+                                 double* macs) {
+  EXPECTO_REQUIRE(h != nullptr && rows && ms && calls && macs, "null argument");
+  EXPECTO_REQUIRE(slot >= 0 && slot < 2 * kNumLayers, "slot out of range");
+  int rc = resolve_events(h);
+  if (rc) return rc;
+  *rows = 0, *ms = 0.0, *calls = 0, *macs = 0.0;
+  for (auto& kv : h->launch_stats)
+    if (kv.first.first == slot && kv.first.second > *rows) {
+      *rows = kv.first.second;
+      *ms = kv.second[0];
+      *calls = (long long)kv.second[1];
+      *macs = kv.second[2];
+    }
   return EXPECTO_OK;
 }
 

@@ -53,20 +53,6 @@ def sweep_roles(shifts, pairs: bool = True) -> np.ndarray:
     return np.array([[fc1_role(s - lo, L, rc) for s in shifts] for rc in (False, True)], np.int64)
 
 
-def conv_role(offsets, seg_len: int, strands: str = "both") -> int:
-    """conv3 / conv4 role (include/expecto_hip.h expecto_beluga_set_conv_role) that per-window
-    forwards need to equal a forward_segments call over windows at bp `offsets` of segments of
-    `seg_len` bp bit for bit: 1 (direct) when a window starts on an odd pool1 row (offset / 4 odd)
-    of a computed strand ("fwd", "rc" or "both"; rc offsets are seg_len - 2000 - offset), else 0."""
-    for o in offsets:
-        o = int(o)
-        if strands != "rc" and (o >> 2) & 1:
-            return 1
-        if strands != "fwd" and ((seg_len - 2000 - o) >> 2) & 1:
-            return 1
-    return 0
-
-
 def _allele_code(a: str) -> int:
     c = int(_LUT[ord(a)]) if len(a) == 1 and ord(a) < 256 else 255
     if c == 255:

@@ -119,17 +119,6 @@ int expecto_beluga_conv2_table_active(expecto_beluga_t h, int* reason);
  * on every path; other roles agree to the parity bar.  Sets the per-window role (0..4). */
 int expecto_beluga_set_fc1_role(expecto_beluga_t h, int role);
 
-/* With EXPECTO_CONV_KARATSUBA=1 at handle creation (opt-in: measured slower than the direct kernel,
- * DESIGN.md "conv3 / conv4 as pair Karatsuba GEMMs"), F16X3 computes conv3 and conv4 (Beluga.py:29-32)
- * in output pairs (y[2p], y[2p+1]) as a 2 x 2 Toeplitz Karatsuba: 13 instead of 16 (32-channel, tap)
- * K blocks per pair.  Pairs are (even, odd) rows
- * of a window's rows on every per-window path, and of the segment's pool1 rows on the segment
- * path: a forward_segments call holding a window on an odd pool1 row (offset / 4 odd, in the
- * computed strand's coordinates) runs conv3 / conv4 direct for every window.  ROLE of per-window
- * forwards: 0 pairs (default), 1 direct; the same role gives the same bits on every path, the
- * other agrees to the parity bar. */
-int expecto_beluga_set_conv_role(expecto_beluga_t h, int role);
-
 /* y[n,2002] = Beluga.forward(x[n,4,1,2000]) (x contiguous fp32, any values).  When the handle
  * holds the k-mer tables, runs F16X3 or BF16X6, x is 16-byte aligned and every column of x is an
  * exact one-hot column (one 1.0f, three +0.0f) or all zeros, as encodeSeqs writes them
@@ -237,6 +226,14 @@ int expecto_beluga_count_fallback(expecto_beluga_t h);
  * Fills min(max_layers, 18) entries and returns 18. */
 int expecto_beluga_set_profiling(expecto_beluga_t h, int on);
 int expecto_beluga_layer_times(expecto_beluga_t h, double* ms, long long* calls, double* macs, int max_layers);
+
+/* While profiling, every conv GEMM launch (conv2-6) is also timed alone -- its own HIP event pair on
+ * the launch stream, without the pool2 pass that shares the conv4 slot -- and logged by (slot, rows).
+ * Returns the group of slot `slot` (layer_times numbering) with the most rows: the full-size
+ * launches, *rows each, *calls of them, their summed *ms and executed *macs.  bench.py's roofline
+ * reads this (the rocprofv3 launch_groups.csv of the same command lists the same launches). */
+int expecto_beluga_main_launches(expecto_beluga_t h, int slot, long long* rows, double* ms, long long* calls,
+                                 double* macs);
 
 /* SNV windows from a device-resident genome (uint8 codes as above).  For variant v and
  * shift s the 2000-code window is genome[off_v + shift - 999 + i], i = 0..1999, with the

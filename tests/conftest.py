@@ -50,20 +50,17 @@ def assert_close(got, want, rtol=RTOL, atol=ATOL, what=""):
         assert err.max() / np.abs(want).max() <= rtol, f"{what}: max err ratio {err.max() / np.abs(want).max():.3g}"
 
 
-def run_in_roles(eng, fn, conv=0):
+def run_in_roles(eng, fn):
     """{role: fn()} with the engine's per-window forwards in each block-Karatsuba FC1 role 0..3 and
-    the direct FC1 (role 4; include/expecto_hip.h expecto_beluga_set_fc1_role), conv3 / conv4 in
-    conv role `conv` (0 pairs, 1 direct: pipeline.conv_role of the segment call compared with);
-    both reset to 0 after."""
+    the direct FC1 (role 4, the default; include/expecto_hip.h expecto_beluga_set_fc1_role); reset
+    to 4 after."""
     ys = {}
     try:
-        eng.set_conv_role(conv)
         for r in range(5):
             eng.set_fc1_role(r)
             ys[r] = fn().clone()
     finally:
-        eng.set_fc1_role(0)
-        eng.set_conv_role(0)
+        eng.set_fc1_role(4)
     return ys
 
 

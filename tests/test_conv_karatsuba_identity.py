@@ -1,9 +1,10 @@
 """CPU (float64): conv3 / conv4 (Beluga.py:29-32, an 8-tap correlation over all input channels)
-equals the pair Karatsuba form the f16x3 library runs (gemm_kernel.h beluga_conv_h3k): per output
+equals the pair Karatsuba form of the round-5 probe kernel (tools/ck_karatsuba.h beluga_conv_h3k,
+measured slower than the direct kernel and kept out of the library): per output
 pair (y[2p], y[2p+1]), S + V and S + U with S over the pair sums s[q] = x[2q] + x[2q+1] (4 taps),
 V over the odd rows (4 taps) and U over the even rows (5 taps) -- 13 K blocks per pair instead of
 16 -- with the weights in the kernel's step order (S, U, V; chunk-major, tap-minor) as ck_weights
-builds them.  Channels shrunk so the check runs in milliseconds."""
+built them.  Channels shrunk so the check runs in milliseconds."""
 import numpy as np
 
 CIN, COUT, CH = 64, 5, 32          # two 32-channel chunks
@@ -61,13 +62,3 @@ def test_pair_karatsuba_equals_the_direct_correlation():
 def test_thirteen_k_blocks_per_pair():
     W = np.zeros((COUT, CIN, 8))
     assert _step_weights(W).shape[1] == 13 * CIN             # vs 16 * CIN for two direct outputs
-
-
-def test_conv_role_rule():
-    """pipeline.conv_role: direct (1) when a window starts on an odd pool1 row of a computed strand."""
-    from expecto_amd.pipeline import conv_role
-    L = 2000 + 1600
-    assert conv_role(range(0, 1601, 200), L) == 0             # 200-bp sweeps: rows 50 k, both strands
-    assert conv_role([0, 8, 16], L) == 0
-    assert conv_role([4], L) == 1                             # fwd row 1
-    assert conv_role([8], L + 4, "fwd") == 0 and conv_role([8], L + 4, "rc") == 1   # rc row (1596 - 8) / 4

@@ -59,7 +59,7 @@ def test_segment_windows_equal_per_window_forwards_in_their_role():
     """forward_segments over 200-bp offsets (full groups of 4, a trailing incomplete group, both
     strands) and over scattered 4-aligned offsets: every window equals forward_codes of its own
     2000 codes in its role (pipeline.fc1_role) bit for bit."""
-    from expecto_amd.pipeline import conv_role, fc1_role
+    from expecto_amd.pipeline import fc1_role
     rng = np.random.default_rng(32)
     m = _model(max_batch=256)
     eng = m.engine()
@@ -72,8 +72,7 @@ def test_segment_windows_equal_per_window_forwards_in_their_role():
         win_seg, win_off = v_i.ravel().astype(np.int32), offs[j_i.ravel()].astype(np.int32)
         y = eng.forward_segments(seg, L, win_seg, win_off, None, 2).view(2, ns, offs.size, 2002)
         wins = torch.stack([seg[v, o:o + 2000] for v, o in zip(win_seg, win_off)]).contiguous()
-        by_role = run_in_roles(eng, lambda: eng.forward_codes(wins, 2).view(2, ns, offs.size, 2002),
-                               conv=conv_role(offs, L))
+        by_role = run_in_roles(eng, lambda: eng.forward_codes(wins, 2).view(2, ns, offs.size, 2002))
         for sd in range(2):
             for j, o in enumerate(offs):
                 want = by_role[fc1_role(int(o), L, sd == 1)][sd, :, j]
@@ -99,7 +98,7 @@ def test_pair_path_masked_alt_fc1_equals_full_forward_in_every_role():
         eng.forward_pairs(ref, alt, pos, yv[0:], yv[n:], 2 * n, 2)
         assert torch.equal(y[:, 0].reshape(2 * n, 2002), eng.forward_codes(ref, 2)), role
         assert torch.equal(y[:, 1].reshape(2 * n, 2002), eng.forward_codes(alt, 2)), role
-    eng.set_fc1_role(0)
+    eng.set_fc1_role(4)
 
 
 def test_headline_segment_pairs_equal_per_window_in_role():

@@ -77,7 +77,7 @@ def test_tile_widths_small_batches(monkeypatch):
             for eng in engs.values():
                 eng.set_fc1_role(role)
                 ys.append(eng.forward_codes(codes[:b], 2).clone())
-                eng.set_fc1_role(0)
+                eng.set_fc1_role(4)
             assert torch.equal(ys[0], ys[1]), (role, b, float((ys[0] - ys[1]).abs().max()))
 
 

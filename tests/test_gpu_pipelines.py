@@ -227,12 +227,10 @@ def test_segment_pairs_alt_runs_are_bitwise_equal(precision, max_batch):
     yf = y.view(4 * S * n, 2002)
     eng.forward_segment_pairs(ref, L, q, alt_code, win_seg, win_off, win_row, yf[0:],
                               yf[S * n:], 2 * S * n)
-    from expecto_amd.pipeline import conv_role, fc1_role
-    cr = conv_role(offs, L)            # offsets 4, 796, 1596: odd pool1 rows -> conv3 / conv4 direct
-    assert cr == 1
+    from expecto_amd.pipeline import fc1_role
     for a, src in enumerate((ref, alt)):
         wins = torch.stack([src[:, o:o + 2000] for o in offs], 0).reshape(S * n, 2000).contiguous()  # row j*n + v
-        by_role = run_in_roles(eng, lambda: eng.forward_codes(wins, 2).view(2, S, n, 2002), conv=cr)
+        by_role = run_in_roles(eng, lambda: eng.forward_codes(wins, 2).view(2, S, n, 2002))
         # each window in its FC1 role; the direct FC1 (role 4) when > 1/3 of the windows hold the SNV
         n_alt = int(sum(((o <= q) & (q < o + 2000)).sum() for o in offs))
         role = (lambda o, sd: 4) if 3 * n_alt > S * n else (lambda o, sd: fc1_role(int(o), L, sd == 1))
@@ -561,3 +559,40 @@ def test_indel_windows_device_equal_host_splice():
                 want[ai, j, k, :cc.size] = cc
     bad = np.argwhere((got != want).any(-1))
     assert bad.size == 0, f"(allele, shift, item) rows differ: {bad[:8].tolist()}"
+
+
+def test_chromatin_cli_shift0_rows_equal_across_maxshift(workdir):
+    """The reference's two sweep modes (chromatin.py:243: --maxshift 0 and the default 800) write
+    the same shift-0 `.diff.h5` byte for byte: per-window forwards and the +-800 segment pairs both
+    run the direct FC1 (role 4, include/expecto_hip.h expecto_beluga_set_fc1_role).  And the
+    operator API on those windows -- Beluga.forward of encodeSeqs' one-hot [fwd; rc] rows
+    (chromatin.py:266-279) -- returns the same bits as the +-800 file's `ref` and `alt` rows
+    (VERDICT r05 item 2).  SNVs, a ref mismatch, an insertion and a deletion (the golden VCF)."""
+    import math
+    import torch
+    from expecto_amd import beluga, chromatin, h5
+    from expecto_amd.encode import encodeSeqs
+    from expecto_amd.genome import Fasta
+    from expecto_amd.pipeline import fetch_window
+    vcf = workdir / "in_modes.vcf"
+    with open(vcf, "w") as f:
+        f.write("##fileformat=VCFv4.1\n")
+        f.write(open(os.path.join(GOLDEN, "chromatin_vcf.txt")).read())
+    common = ["--genome", str(workdir / "hg19.fa"), "--synthetic-weights", "0", "--max-batch", "40"]
+    files = {}
+    for ms in (0, 800):
+        d = workdir / f"modes_{ms}"
+        chromatin.main([str(vcf), "--maxshift", str(ms), "--output_dir", str(d)] + common)
+        files[ms] = d / "snps.shift_0.diff.h5"
+    assert open(files[0], "rb").read() == open(files[800], "rb").read()
+    got = h5.read(str(files[800]))
+    vs = chromatin.read_variants(chromatin.build_parser().parse_args([str(vcf), "--output_dir", str(workdir)]
+                                                                     + common), write_side_files=False)
+    fa = Fasta(str(workdir / "hg19.fa"))
+    m = beluga.seeded(0, gain=math.sqrt(6.0), max_batch=40).cuda()
+    for k, alleles in (("ref", vs.ref), ("alt", vs.alt)):
+        seqs = [fetch_window(fa, c, int(p), r, a, 0) for c, p, r, a in zip(vs.chrom, vs.pos, vs.ref, alleles)]
+        x = torch.from_numpy(encodeSeqs(seqs).astype(np.float32)).unsqueeze(2).cuda()
+        y = torch.cat([m(x[i:i + 32]) for i in range(0, x.shape[0], 32)]).cpu().numpy()   # batchSize 32
+        assert y.shape == got[k].shape
+        assert np.array_equal(y.view(np.uint32), got[k].view(np.uint32)), k

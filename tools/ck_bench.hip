@@ -2,7 +2,7 @@
 // (beluga_conv_h3p<.., 256, 4>) against the pair Karatsuba kernel (beluga_conv_h3k) and its timing
 // probes (PROBE bits, wrong results).  Random ReLU-like activation planes, unit scales.
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/ck_bench.hip -o tools/ck_bench
-// Run:   tools/ck_bench [windows=2000] [rounds=5] [conv3|conv4]
+// Run:   tools/ck_bench [windows=2000] [rounds=5] [conv3|conv4|conv5|conv6]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -12,7 +12,7 @@
 #include <string>
 #include <vector>
 
-#include "../expecto_amd/csrc/gemm_kernel.h"
+#include "ck_karatsuba.h"
 
 using namespace expecto;
 
@@ -65,11 +65,36 @@ Variant mkp(const char* name) {
   return {name, 256, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3p<L, EPI_RELU, TM, 4><<<nblk, 512>>>(a); }};
 }
 
+template <int L>
+Variant mkr(const char* name) {
+  return {name, 384, [](const GemmArgs& a, unsigned nblk) { beluga_conv_h3r<L, EPI_RELU, 0><<<nblk, 256>>>(a); }};
+}
+
+// stamp build: per-wave cycle sums (gemm_kernel.h H3P_STAMP), summarised as shares of the loop
+static void stamp_report(const unsigned long long* d, long long nblk, int nk) {
+  double cl = 0, cb = 0, ce = 0, pl = 0, pb = 0, pv = 0;
+  for (long long b = 0; b < nblk; ++b)
+    for (int w = 0; w < 8; ++w) {
+      const unsigned long long* e = d + (b * 8 + w) * 4;
+      if (w < 4) { cl += e[0]; cb += e[1]; ce += e[3]; }
+      else { pl += e[0]; pb += e[1]; pv += e[2]; }
+    }
+  const double nw = 4.0 * nblk;
+  printf("stamp: %d stages per tile; consumer loop %.0f cycles/tile (%.0f per stage; 120 MFMAs = 1920 at 16 each), "
+         "barrier wait %.3f of the loop, epilogue %.0f cycles (%.3f of loop)\n",
+         nk, cl / nw, cl / nw / nk, cb / cl, ce / nw, ce / cl);
+  printf("stamp: producer loop %.0f cycles/tile, vmcnt wait %.3f, barrier wait %.3f of its loop\n", pl / nw, pv / pl, pb / pl);
+}
+
 int main(int argc, char** argv) {
   const int nb = argc > 1 ? atoi(argv[1]) : 2000;
   const int rounds = argc > 2 ? atoi(argv[2]) : 5;
-  const bool c4 = argc > 3 && !strcmp(argv[3], "conv4");
-  const int cin = c4 ? 480 : 320, cout = 480, s_in = c4 ? 492 : 496, t_valid = c4 ? 482 : 489, s_out = c4 ? 482 : 492;
+  const char* layer = argc > 3 ? argv[3] : "conv3";
+  const bool c4 = !strcmp(layer, "conv4"), c5 = !strcmp(layer, "conv5"), c6 = !strcmp(layer, "conv6");
+  // conv5 / conv6: the per-window shapes (Q4 120 rows -> 113; conv5 113 rows -> 106)
+  const int cin = c6 ? 640 : (c4 || c5) ? 480 : 320, cout = (c5 || c6) ? 640 : 480;
+  const int s_in = c6 ? 113 : c5 ? 120 : c4 ? 492 : 496, t_valid = c6 ? 106 : c5 ? 113 : c4 ? 482 : 489;
+  const int s_out = c6 ? 106 : c5 ? 113 : c4 ? 482 : 492;
   const long long M = (long long)nb * s_in;
   const int npad = (cout + GBN - 1) / GBN * GBN;
   _Float16 *X, *Bd, *Bk;
@@ -94,8 +119,35 @@ int main(int argc, char** argv) {
   CK(hipMemset(ovf, 0, 4));
   CK(hipDeviceSynchronize());
   std::vector<Variant> vs;
-  if (c4) {
+  if (c5) {
+    vs.push_back(mkp<5>("direct_h3p"));
+    vs.push_back(mkp<5, 256 | H3P_STAMP>("direct_stamp"));
+    vs.push_back(mkp<5, 256 | 2048>("direct_noepi"));
+    vs.push_back(mkp<5, 256 | 512>("direct_nostore"));
+    vs.push_back(mkp<5, 256 | 2>("direct_noload"));
+    vs.push_back(mkp<5, 256 | H3P_STAMP | 8>("direct_stamp_hotAB"));
+    vs.push_back(mkp<5, 256 | H3P_STAMP | 2>("direct_stamp_noload"));
+    vs.push_back(mkr<5>("h3r_384"));
+    vs.push_back(mkp<5, 256 | 8>("direct_hotAB"));
+  } else if (c6) {
+    vs.push_back(mkp<6>("direct_h3p"));
+    vs.push_back(mkp<6, 256 | H3P_STAMP>("direct_stamp"));
+    vs.push_back(mkp<6, 256 | 2048>("direct_noepi"));
+    vs.push_back(mkp<6, 256 | 512>("direct_nostore"));
+    vs.push_back(mkp<6, 256 | 2>("direct_noload"));
+    vs.push_back(mkp<6, 256 | H3P_STAMP | 8>("direct_stamp_hotAB"));
+    vs.push_back(mkp<6, 256 | H3P_STAMP | 2>("direct_stamp_noload"));
+    vs.push_back(mkr<6>("h3r_384"));
+    vs.push_back(mkp<6, 256 | 8>("direct_hotAB"));
+  } else if (c4) {
     vs.push_back(mkp<4>("direct_h3p"));
+    vs.push_back(mkp<4, 256 | H3P_STAMP>("direct_stamp"));
+    vs.push_back(mkp<4, 256 | 2048>("direct_noepi"));
+    vs.push_back(mkp<4, 256 | 512>("direct_nostore"));
+    vs.push_back(mkp<4, 256 | 2>("direct_noload"));
+    vs.push_back(mkp<4, 256 | H3P_STAMP | 8>("direct_stamp_hotAB"));
+    vs.push_back(mkp<4, 256 | H3P_STAMP | 2>("direct_stamp_noload"));
+    vs.push_back(mkr<4>("h3r_384"));
     vs.push_back(mkp<4, 256 | 8>("direct_hotAB"));
     vs.push_back(mkp<4, 256 | 16>("direct_hotA"));
     vs.push_back(mkp<4, 256 | 32>("direct_hotB"));
@@ -108,6 +160,13 @@ int main(int argc, char** argv) {
     vs.push_back(mkk<4, 16>("k_s_valu_only"));
   } else {
     vs.push_back(mkp<3>("direct_h3p"));
+    vs.push_back(mkp<3, 256 | H3P_STAMP>("direct_stamp"));
+    vs.push_back(mkp<3, 256 | 2048>("direct_noepi"));
+    vs.push_back(mkp<3, 256 | 512>("direct_nostore"));
+    vs.push_back(mkp<3, 256 | 2>("direct_noload"));
+    vs.push_back(mkp<3, 256 | H3P_STAMP | 8>("direct_stamp_hotAB"));
+    vs.push_back(mkp<3, 256 | H3P_STAMP | 2>("direct_stamp_noload"));
+    vs.push_back(mkr<3>("h3r_384"));
     vs.push_back(mkp<3, 256 | 8>("direct_hotAB"));
     vs.push_back(mkp<3, 256 | 16>("direct_hotA"));
     vs.push_back(mkp<3, 256 | 32>("direct_hotB"));
@@ -132,7 +191,7 @@ int main(int argc, char** argv) {
   std::vector<double> best(vs.size(), 1e30), sum(vs.size(), 0.0);
   for (int r = 0; r < rounds; ++r)
     for (size_t v = 0; v < vs.size(); ++v) {
-      const bool kar = vs[v].name.rfind("direct", 0) != 0;
+      const bool kar = vs[v].name.rfind("k", 0) == 0;   // karatsuba, k_*
       GemmArgs a{};
       a.A = reinterpret_cast<const float*>(X);
       a.lda = cin;
@@ -142,7 +201,7 @@ int main(int argc, char** argv) {
       a.kper = (int)a.ldb;
       a.taps = 8;
       a.n_tiles = npad / GBN;
-      a.m_tiles = kar ? (M / 2 + CK_PAIRS - 1) / CK_PAIRS : (M + 255) / 256;
+      a.m_tiles = kar ? (M / 2 + CK_PAIRS - 1) / CK_PAIRS : (M + vs[v].rows_per_tile - 1) / vs[v].rows_per_tile;
       a.bias = bias;
       a.col_scale = cs;
       a.out_scale = 1.f;
@@ -154,6 +213,11 @@ int main(int argc, char** argv) {
       a.t_valid = t_valid;
       a.s_out = s_out;
       const unsigned nblk = (unsigned)(a.m_tiles * a.n_tiles);
+      const bool stamp = vs[v].name.rfind("direct_stamp", 0) == 0;
+      if (stamp) {
+        CK(hipMalloc(&a.stamps, (size_t)nblk * 8 * 4 * 8));
+        CK(hipMemset(a.stamps, 0, (size_t)nblk * 8 * 4 * 8));
+      }
       vs[v].launch(a, nblk);   // warm
       CK(hipEventRecord(e0));
       for (int i = 0; i < 3; ++i) vs[v].launch(a, nblk);
@@ -162,11 +226,20 @@ int main(int argc, char** argv) {
       float ms;
       CK(hipEventElapsedTime(&ms, e0, e1));
       ms /= 3;
+      if (stamp) {
+        std::vector<unsigned long long> h((size_t)nblk * 8 * 4);
+        CK(hipMemcpy(h.data(), a.stamps, h.size() * 8, hipMemcpyDeviceToHost));
+        if (r == rounds - 1) {
+          printf("%s ", vs[v].name.c_str());
+          stamp_report(h.data(), nblk, (int)(cin / 32 * 8));
+        }
+        CK(hipFree(a.stamps));
+      }
       best[v] = std::min(best[v], (double)ms);
       sum[v] += ms;
     }
   const double alg = 2.0 * M * cout * 8.0 * cin;   // direct fp32-equivalent flops
-  printf("%s, %d windows, M %lld rows\n", c4 ? "conv4 (unpooled)" : "conv3", nb, M);
+  printf("%s, %d windows, M %lld rows\n", c4 ? "conv4 (unpooled)" : layer, nb, M);
   for (size_t v = 0; v < vs.size(); ++v)
     printf("%-14s mean %.3f ms  best %.3f ms  dense-equivalent %.1f TF/s  (%.3fx direct)\n", vs[v].name.c_str(),
            sum[v] / rounds, best[v], alg / (sum[v] / rounds * 1e-3) / 1e12, vs.empty() ? 0.0 : sum[0] / sum[v]);

@@ -9,6 +9,8 @@
 #   power    rocm-smi power / clock samples during 200 headline steps       -> gpurun_out/power.log
 #   gb       tools/gemm_bench $GB_ARGS (e.g. "8192 5 fc1 8")                -> gpurun_out/gb.log
 #   gbpmc    SQ stall counter sets of gemm_bench $GB_ARGS, VARIANT=$V
+#   ckstamp  tools/ck_bench per conv layer with the stamp build (barrier / vmcnt / epilogue shares) -> ck_<layer>.log
+#   convpmc  SQ stall counter sets of the headline's conv kernels (beluga_conv_h3p only)  -> convpmc_<i>_$TAG/
 #   writes   tools/write_probe.py, 8 writers at configs[3]'s full size: plain, staggered, staggered with 4 threads
 #
 #   STEPS=tests,bench TAG=r04 /usr/local/graft/bin/gpurun -- bash tools/gpu_session.sh
@@ -64,6 +66,22 @@ if has gbpmc; then
     i=$((i+1))
     run gbpmc_$i 180 rocprofv3 --pmc $ctrs --kernel-trace --output-format csv -d $OUT/gbpmc_$i -o run -- \
       tools/gemm_bench ${GB_ARGS:-1000 2 conv2}
+  done
+fi
+if has ckstamp; then
+  run ck_conv3 200 tools/ck_bench 2000 3 conv3
+  run ck_conv4 200 tools/ck_bench 2000 3 conv4
+  run ck_conv5 200 tools/ck_bench 16000 3 conv5
+  run ck_conv6 200 tools/ck_bench 16000 3 conv6
+fi
+if has convpmc; then
+  i=0
+  for ctrs in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM GRBM_GUI_ACTIVE" \
+              "SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE" \
+              "SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_VMEM SQ_WAVES GRBM_GUI_ACTIVE"; do
+    i=$((i+1))
+    run convpmc_${i}_$TAG 300 rocprofv3 --pmc $ctrs --kernel-include-regex beluga_conv_h3p --kernel-trace \
+      --output-format csv -d $OUT/convpmc_${i}_$TAG -o run -- $B --steps 1 --warmup 1
   done
 fi
 if has writes; then
