@@ -332,19 +332,31 @@ class Beluga(nn.Module):
     # -- engine management: rebuilt whenever the parameters change (load_state_dict, .cuda())
     def _params(self):
         # (owner module, name) of each parameter, resolved once: a named_parameters() walk per
-        # forward cost ~50 us of host time, 7 % of a batch-32 Beluga.forward; a parameter
-        # reassigned on its module is still seen (the owner's _parameters is read each call)
-        slots = self.__dict__.get("_param_slots")
-        if slots is None:
-            slots = []
+        # forward cost ~50 us of host time, 7 % of a batch-32 Beluga.forward.  A parameter
+        # reassigned on its module is still seen (the owner's _parameters is read each call), and
+        # the cached module links are checked by identity each call, so a replaced submodule
+        # (model.model[0] = nn.Conv2d(...)) or a copy whose module dicts are its own (DataParallel
+        # replicas copy __dict__) resolves again instead of reading stale parameters.
+        cache = self.__dict__.get("_param_slots")
+        if cache is not None:
+            root, checks, slots = cache
+            if root is not self._modules or any(parent.get(part) is not child for parent, part, child in checks):
+                cache = None
+        if cache is None:
+            slots, seen, checks = [], set(), []
             for k in PARAM_KEYS:
                 *path, name = k.split(".")
                 mod = self
                 for part in path:
-                    mod = mod._modules[part]
+                    child = mod._modules[part]
+                    if id(child) not in seen:          # each module link once (13 identity checks)
+                        seen.add(id(child))
+                        checks.append((mod._modules, part, child))
+                    mod = child
                 slots.append((mod._parameters, name))
-            self.__dict__["_param_slots"] = slots
-        return [d[name] for d, name in slots]
+            cache = (self._modules, checks, slots)
+            self.__dict__["_param_slots"] = cache
+        return [d[name] for d, name in cache[2]]
 
     def _key(self, params):
         return tuple((p.data_ptr(), p._version) for p in params)

@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <array>
+#include <cassert>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -588,10 +589,11 @@ __global__ void fc1_slab_mask(const int* __restrict__ var_pos, int nv, int v0, i
 
 // profiling: executed MACs of a masked FC1 = set slab bits x MACs per (tile, slab), summed into
 // acc on the device (one wave; the host reads acc when the layer times are collected)
+// (waves: the Karatsuba FC1 masks, whose bits 1..8 are the tile's computing 32-row waves)
 __global__ __launch_bounds__(64) void slab_macs(const unsigned* __restrict__ mask, int tiles, double per_bit,
-                                                double* __restrict__ acc) {
+                                                double* __restrict__ acc, int waves = 0) {
   int bits = 0;
-  for (int i = threadIdx.x; i < tiles; i += 64) bits += __popc(mask[i]);
+  for (int i = threadIdx.x; i < tiles; i += 64) bits += __popc(waves ? (mask[i] >> 1) & 0xffu : mask[i]);
   for (int o = 32; o > 0; o >>= 1) bits += __shfl_down(bits, o);
   if (threadIdx.x == 0) atomicAdd(acc, bits * per_bit);
 }
@@ -1016,7 +1018,13 @@ __global__ void fk_window_tables(int M, int rstride, int role, long long* __rest
 // ref rows only in [r6, r6 + 20) (window rows), so partial (product j, slab s) -- sequence rows
 // 25 (blk - role) + [13 s - (s ? 1 : 0), 13 s + 12] with their lags -- and the tail (rows 100..105)
 // are recomputed only where a dependency row falls in that run: bit 0 of mask[d * tiles + m / 256]
-// for descriptor d = 2j + s (8 = the tail).  Unset descriptors keep the ref partials in place.
+// for descriptor d = 2j + s (8 = the tail), and bit 1 + w for the tile's 32-row wave w holding m
+// (fk_wave_bits: the other waves of the tile skip their MFMAs and keep their ref partials).  Unset
+// descriptors keep the ref partials in place.
+// mask word bits of partial row i of a masked FC1 descriptor: bit 0 = its 256-row M tile runs, bit
+// 1 + w = the tile's wave w (rows 32 w .. 32 w + 31, gemm_kernel.h fc_h3w_tile) computes
+__device__ __forceinline__ unsigned fk_wave_bits(int i) { return 1u | (2u << ((i & 255) >> 5)); }
+
 __global__ void fk_window_mask(const int* __restrict__ var_pos, int nv, int v0, int R, int role, int tiles,
                                unsigned* __restrict__ mask) {
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1034,10 +1042,10 @@ __global__ void fk_window_mask(const int* __restrict__ var_pos, int nv, int v0, 
         const int lag = l == 0 ? 0 : (nl == 2 ? lag1 : 25 * l);
         hit |= i0 + lag < r6e && i1 + lag >= r6;
       }
-      if (hit) atomicOr(mask + (2 * j + s) * tiles + m / 256, 1u);
+      if (hit) atomicOr(mask + (2 * j + s) * tiles + m / 256, fk_wave_bits(m));
     }
   }
-  if (100 < r6e && 105 >= r6) atomicOr(mask + 8 * tiles + m / 256, 1u);
+  if (100 < r6e && 105 >= r6) atomicOr(mask + 8 * tiles + m / 256, fk_wave_bits(m));
 }
 
 // Alt masks of the segment path's in-place alt FC1 (segment pairs): descriptor slot d of the ref
@@ -1059,7 +1067,7 @@ __global__ void fk_seg_mask(FkMaskDesc md, const int* __restrict__ rgrp, const i
   if (d == md.n) {   // the tail
     if (i >= md.nw) return;
     const int r6 = r6_of(winfo[2 * i]), o = winfo[2 * i + 1];
-    if (o + 100 < r6 + kDW[6] && o + 105 >= r6) atomicOr(mask + (size_t)d * tiles + i / 256, 1u);
+    if (o + 100 < r6 + kDW[6] && o + 105 >= r6) atomicOr(mask + (size_t)d * tiles + i / 256, fk_wave_bits(i));
     return;
   }
   if (i >= md.cnt[d]) return;
@@ -1073,7 +1081,7 @@ __global__ void fk_seg_mask(FkMaskDesc md, const int* __restrict__ rgrp, const i
     const int lag = l == 0 ? 0 : (nl == 2 ? lag1 : 25 * l);
     hit |= i0 + lag < r6e && i1 + lag >= r6;
   }
-  if (hit) atomicOr(mask + (size_t)d * tiles + i / 256, 1u);
+  if (hit) atomicOr(mask + (size_t)d * tiles + i / 256, fk_wave_bits(i));
 }
 
 // ---- weight repacking (reference layouts -> kernel layouts) --------------------------
@@ -1593,6 +1601,8 @@ struct expecto_beluga {
   bool onehot_as_codes = true;        // forward_onehot: exact one-hot input through the k-mer gather (EXPECTO_ONEHOT_CODES)
   uint8_t* oh_codes = nullptr;        //   its codes, max_batch x 2000 (allocated on first use)
   int* oh_bad = nullptr;              //   its check flag
+  bool oh_hint_bad = false;           //   the last input was not one-hot: check first instead of a speculative run
+  int* hflags = nullptr;              // pinned host words the per-call checks read their device flags into
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, int>> pending;  // (layer, event index of start)
@@ -1729,7 +1739,9 @@ void kmer_release(expecto_beluga* h) {
   for (size_t i = 0; i < g_kmer.size(); ++i)
     if (g_kmer[i].T == h->kmer) {
       auto& hs = g_kmer[i].holders;
-      hs.erase(std::find(hs.begin(), hs.end(), h));
+      const auto it = std::find(hs.begin(), hs.end(), h);
+      assert(it != hs.end() && "k-mer table held by an unregistered handle");
+      if (it != hs.end()) hs.erase(it);   // (never erase end(): a handle not in the list is left alone)
       if (hs.empty()) {
         (void)hipFree(g_kmer[i].T);
         g_kmer.erase(g_kmer.begin() + (long)i);
@@ -1918,8 +1930,12 @@ int conv_tile_rows(const expecto_beluga* h, int l, bool pool, long long M, int n
 // 64-column tiles for conv5 / conv6 (640 outputs: 10 N tiles instead of 4; gemm_kernel.h
 // gemm_conv_h3p_body NB 4, same bits) for launches whose 160-column form leaves most of the chip
 // idle -- the per-window forwards of small batches (batch 32: 60 workgroups on 256 CUs).  EXPECTO_CONV_NARROW=0 / 1 forces it (same bits either way).
+// Round 6: conv3 / conv4 (480 outputs) of such batches on 128-column tiles (4 N tiles instead of 3;
+// the weight planes carry 32 zero rows): batch 32 is 62 M tiles, 186 workgroups on 256 CUs at 160
+// columns, 248 at 128 -- one round either way, 0.8 of the work per workgroup.
+int conv_narrow_cols(int l) { return l == 1 || l == 2 ? 128 : 64; }
 bool conv_narrow(const expecto_beluga* h, int l, long long M, int bm, int n_tiles) {
-  if (g_precision != EXPECTO_PRECISION_F16X3 || (l != 3 && l != 4)) return false;
+  if (g_precision != EXPECTO_PRECISION_F16X3 || l < 1 || l > 4) return false;
   if (h->conv_narrow >= 0) return h->conv_narrow != 0;
   if (!h->narrow_scope) return false;
   // only when the narrow launch is one round of workgroups (per column the 64-column tile runs at
@@ -1928,7 +1944,8 @@ bool conv_narrow(const expecto_beluga* h, int l, long long M, int bm, int n_tile
   // alt-delta conv5 / conv6 launches run beside the trunk on the second stream, where more
   // workgroups for the same work cost the trunk (conv6 11.1 -> 11.6 ms per headline step, same box)
   const long long cus = h->cus > 0 ? h->cus : 256;
-  const long long narrow = (M + 255) / 256 * (kConv[l].cout / 64), wide = (M + bm - 1) / bm * n_tiles;
+  const int nc = conv_narrow_cols(l);
+  const long long narrow = (M + 255) / 256 * ((kConv[l].cout + nc - 1) / nc), wide = (M + bm - 1) / bm * n_tiles;
   return narrow <= cus && wide < cus;
 }
 
@@ -1969,6 +1986,13 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
         } else {
           EXPECTO_REQUIRE(false, "64-column conv tiles: conv5 / conv6 only");
         }
+      } else if (a.n_tile_cols == 128) {   // 128-column tiles (conv_narrow: conv3 / conv4 of small batches)
+        if constexpr (LAYER == 3 || LAYER == 4) {
+          EXPECTO_REQUIRE(bm == 256 && a.n_tiles == 4 && a.n_store == 480, "128-column conv tiles: conv3 / conv4");
+          beluga_conv_h3p_narrow<LAYER, EPI, 8><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
+        } else {
+          EXPECTO_REQUIRE(false, "128-column conv tiles: conv3 / conv4 only");
+        }
       } else if (bm == 384)
         beluga_conv_h3r<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
       else   // 4-deep B ring, next-stage fragments read before the stage barrier (TM 256)
@@ -1977,11 +2001,14 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
       // FC split-K partials: 336-column tiles on 8 MFMA waves when the caller tiled N that way
       // (n_tile_cols, set from fc_wide_tiles), else 160-column producer / consumer tiles (same
       // bits either way)
-      EXPECTO_REQUIRE(a.n_tile_cols == 0 || a.n_tile_cols == FCW_BN, "FC tile width: 0 (160) or 336 columns");
+      EXPECTO_REQUIRE(a.n_tile_cols == 0 || a.n_tile_cols == FCW_BN || a.n_tile_cols == 112,
+                      "FC tile width: 0 (160), 336 or 112 columns");
       EXPECTO_REQUIRE((long long)a.n_tiles * (a.n_tile_cols ? a.n_tile_cols : GBN) >= a.n_store,
                       "FC N tiles do not cover the stored columns");
       if (a.n_tile_cols == FCW_BN)
         beluga_fc_h3w<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
+      else if (a.n_tile_cols == 112)
+        beluga_fc_h3w_narrow<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
       else
         beluga_fc_h3p<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
     } else {   // FC layers: producer / consumer waves, both operands through an LDS ring (same bits)
@@ -2063,10 +2090,10 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
   a.taps = 8;
   a.n_tiles = npad_of(g.cout) / GBN;
   int bm = f1 ? 256 : conv_tile_rows(h, l, pool, a.M, (int)a.n_tiles);
-  if (!f1 && !pool && conv_narrow(h, l, a.M, bm, (int)a.n_tiles)) {
+  if (!f1 && (!pool || l == 2) && conv_narrow(h, l, a.M, bm, (int)a.n_tiles)) {
     bm = 256;
-    a.n_tile_cols = 64;
-    a.n_tiles = g.cout / 64;
+    a.n_tile_cols = conv_narrow_cols(l);
+    a.n_tiles = (g.cout + a.n_tile_cols - 1) / a.n_tile_cols;
   }
   a.m_tiles = (a.M + bm - 1) / bm;
   a.m_fastest = 0;
@@ -2125,6 +2152,8 @@ float* h1_rows(expecto_beluga* h, long long rows) { return h->h1 + rows * kHidLd
 // tile share its A rows, ~5.3 M tiles per XCD share a weight tile.
 bool fc_wide_tiles(const expecto_beluga* h) { return h->fc_wide && g_precision == EXPECTO_PRECISION_F16X3; }
 
+bool fc1_narrow(const expecto_beluga* h, long long mtt);
+
 // FC1 (split-K slabs into `part`) + fc1_reduce (bias, ReLU, activation planes) into h1.
 int run_fc1(expecto_beluga* h, const float* act, const long long* a_rows, int nb, float* h1, hipStream_t st,
             const unsigned* ks_mask = nullptr, double slab_frac = 1.0, long long part_rows = 0) {
@@ -2170,6 +2199,10 @@ int run_fc1(expecto_beluga* h, const float* act, const long long* a_rows, int nb
       a.m_fastest = 0;
       a.linear_order = 0;
       a.n_tile_cols = FCW_BN;
+      if (!ks_mask && fc1_narrow(h, m_tiles * splits)) {   // small per-window batches: 112 columns
+        a.n_tile_cols = 112;
+        a.n_tiles = kHidLd / 112;
+      }
     }
     a.C = h->part;
     a.ldc = kHidLd;
@@ -2221,6 +2254,10 @@ int run_fc2(expecto_beluga* h, const float* h1, int nb, float* y, hipStream_t st
     if (wide) {
       a.m_fastest = 0;
       a.n_tile_cols = FCW_BN;
+      if (fc1_narrow(h, m_tiles * h->fc2_splits)) {   // small per-window batches: 112 columns
+        a.n_tile_cols = 112;
+        a.n_tiles = (kNFeat + 111) / 112;
+      }
     }
     a.C = h->part2;
     a.ldc = kHidLd;
@@ -2583,7 +2620,7 @@ int count_desc_macs(expecto_beluga* h, const unsigned* mask, int tiles, double p
     h->macs_d = reinterpret_cast<double*>(f);
     EXPECTO_HIP_CHECK(hipMemsetAsync(h->macs_d, 0, 2 * kNumLayers * sizeof(double), st));
   }
-  slab_macs<<<dim3(1), dim3(64), 0, st>>>(mask, tiles, per_tile, h->macs_d + h->timer_base + 6);
+  slab_macs<<<dim3(1), dim3(64), 0, st>>>(mask, tiles, per_tile / 8, h->macs_d + h->timer_base + 6, 1);
   return check_launch("slab_macs");
 }
 
@@ -3016,9 +3053,11 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
         if (nb > h->fk_gres_cap) {
           if (h->fk_gres) EXPECTO_HIP_CHECK(hipFree(h->fk_gres));
           h->fk_gres = nullptr;
+          h->bytes -= (size_t)h->fk_gres_cap * sizeof(int);
           h->fk_gres_cap = 0;
           EXPECTO_HIP_CHECK(hipMalloc(&h->fk_gres, (size_t)nb * sizeof(int)));
           h->fk_gres_cap = nb;
+          h->bytes += (size_t)nb * sizeof(int);
         }
         if ((rc = stage_copies(h, {{h->fk_gres, gres.data(), gres.size() * sizeof(int)}}, st)) || (rc = fk_tables(h)) ||
             (rc = fk_seg_buffers(h)) || (rc = fk_sequences(h, h->P, nb, g.T6, g.T6, nullptr, n_ph, st, h->fk_gres)))
@@ -3442,8 +3481,10 @@ int f16_prepare(expecto_beluga* h, hipStream_t st) {
   for (int g = 0; g < 7; ++g) {
     const L& y = layers[g];
     float* swf = nullptr;
+    // conv3 / conv4: 32 zero rows past the 480 (4 N tiles of 128 columns for small batches, conv_narrow)
+    const int zrows = (g == 1 || g == 2) ? 4 * 128 - y.rows : 0;
     if ((rc = dalloc(h, &swf, y.rows)) || (rc = dalloc(h, &h->cs[g], y.rows)) ||
-        (rc = dalloc(h, &h->wh[g], (size_t)y.rows * y.K)))
+        (rc = dalloc(h, &h->wh[g], (size_t)(y.rows + zrows) * y.K)))
       return rc;
     h->swd[g] = reinterpret_cast<int*>(swf);
     row_scale_exp<<<dim3(y.rows), dim3(256), 0, st>>>(y.w, (int)y.K, h->swd[g]);
@@ -3499,10 +3540,10 @@ int run_checked(expecto_beluga* h, hipStream_t st, F&& fn) {
   if (h->precision != EXPECTO_PRECISION_F16X3 || h->ovf_deferred) return fn();
   int rc = fn();
   if (rc) return rc;
-  int flag = 0;
-  EXPECTO_HIP_CHECK(hipMemcpyAsync(&flag, h->ovf, sizeof(int), hipMemcpyDeviceToHost, st));
+  int* flag = h->hflags;   // pinned: the copy is one DMA, no staging through a driver bounce buffer
+  EXPECTO_HIP_CHECK(hipMemcpyAsync(flag, h->ovf, sizeof(int), hipMemcpyDeviceToHost, st));
   EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
-  if (!flag) return EXPECTO_OK;
+  if (!*flag) return EXPECTO_OK;
   EXPECTO_HIP_CHECK(hipMemsetAsync(h->ovf, 0, sizeof(int), st));
   h->fallbacks += 1;
   h->precision = EXPECTO_PRECISION_BF16X6;
@@ -3531,6 +3572,10 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
     return code;
   };
   if ((rc = dalloc(h, &h->w1, 320 * 32)) || (rc = dalloc(h, &h->b1, 320))) return fail(rc);
+  if (hipHostMalloc(&h->hflags, 4 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+    set_error("hipHostMalloc (flag words)");
+    return fail(EXPECTO_ENOMEM);
+  }
   EXPECTO_HIP_CHECK(hipMemcpyAsync(h->w1, params[0], 320 * 32 * sizeof(float), hipMemcpyDeviceToDevice, st));
   EXPECTO_HIP_CHECK(hipMemcpyAsync(h->b1, params[1], 320 * sizeof(float), hipMemcpyDeviceToDevice, st));
   for (int l = 0; l < 5; ++l) {
@@ -3659,6 +3704,7 @@ void expecto_beluga_destroy(expecto_beluga_t h) {
     if (h->stage_buf[s]) (void)hipHostFree(h->stage_buf[s]);
     if (h->stage_ev[s]) (void)hipEventDestroy(h->stage_ev[s]);
   }
+  if (h->hflags) (void)hipHostFree(h->hflags);
   delete h;
 }
 
@@ -3692,7 +3738,10 @@ int expecto_beluga_forward_onehot(expecto_beluga_t h, const float* x, int n, flo
   // tables, the same bits as forward_codes -- else conv1 / conv2 stay on the MFMAs (any fp32
   // input, like the reference).  With the per-call overflow check the codes path runs at once and
   // the conversion's flag is read with the overflow flag at the end (one sync; an input that is not
-  // one-hot reruns on the MFMA path); with the deferred check, one check pass and a sync first.
+  // one-hot reruns on the MFMA path, and the handle then checks its next inputs first until one is
+  // one-hot again, so a stream of soft inputs costs one check pass each, not a second forward);
+  // with the deferred check, one check pass and a sync first (include/expecto_hip.h).  Either way
+  // an input's path -- and so its bits -- depends only on the input.
   const bool candidate = h->onehot_as_codes && h->kmer && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
                          (h->precision == EXPECTO_PRECISION_F16X3 || h->precision == EXPECTO_PRECISION_BF16X6);
   if (candidate && !h->oh_codes) {
@@ -3723,15 +3772,16 @@ int expecto_beluga_forward_onehot(expecto_beluga_t h, const float* x, int n, flo
     }
     return (int)EXPECTO_OK;
   };
-  if (candidate && h->precision == EXPECTO_PRECISION_F16X3 && !h->ovf_deferred) {
+  if (candidate && h->precision == EXPECTO_PRECISION_F16X3 && !h->ovf_deferred && !h->oh_hint_bad) {
     EXPECTO_HIP_CHECK(hipMemsetAsync(h->oh_bad, 0, sizeof(int), st));
     int rc = run(true, h->oh_bad);
     if (rc) return rc;
-    int flags[2] = {0, 0};
+    int* flags = h->hflags;   // pinned host words
     EXPECTO_HIP_CHECK(hipMemcpyAsync(&flags[0], h->ovf, sizeof(int), hipMemcpyDeviceToHost, st));
     EXPECTO_HIP_CHECK(hipMemcpyAsync(&flags[1], h->oh_bad, sizeof(int), hipMemcpyDeviceToHost, st));
     EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
     if (flags[1]) {   // not one-hot: the whole call on the MFMA path (its own overflow check)
+      h->oh_hint_bad = true;
       EXPECTO_HIP_CHECK(hipMemsetAsync(h->ovf, 0, sizeof(int), st));
       return run_checked(h, st, [&]() { return run(false, nullptr); });
     }
@@ -3754,9 +3804,11 @@ int expecto_beluga_forward_onehot(expecto_beluga_t h, const float* x, int n, flo
       int rc = check_launch("onehot_codes check");
       if (rc) return rc;
     }
-    EXPECTO_HIP_CHECK(hipMemcpyAsync(&bad, h->oh_bad, sizeof(int), hipMemcpyDeviceToHost, st));
+    EXPECTO_HIP_CHECK(hipMemcpyAsync(h->hflags + 2, h->oh_bad, sizeof(int), hipMemcpyDeviceToHost, st));
     EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
+    bad = h->hflags[2];
     as_codes = bad == 0;
+    h->oh_hint_bad = !as_codes;
   }
   return run_checked(h, st, [&]() { return run(as_codes, nullptr); });
 }

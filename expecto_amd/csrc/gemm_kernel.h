@@ -1070,10 +1070,13 @@ struct FcwGeo {
   static_assert(2 * STAGE >= 8 * FCW_EWAVE, "epilogue staging inside the stage ring");
 };
 
+// wlive: bit w = wave w (rows 32 w ..) computes; a masked in-place alt launch clears the bits of
+// the waves none of whose rows it must recompute (they skip MFMAs, reads and stores, as waves past M)
 template <int TM, int NB = FCW_NB, int NS = 2>
 __device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_rows, long long a_off, long long lda_kb,
                                             int kb0a, long long M, const char* Bb, int kb_total, int nk, float* cbase,
-                                            long long ldc, int n_store, long long m0, int n0, char* smem) {
+                                            long long ldc, int n_store, long long m0, int n0, char* smem,
+                                            unsigned wlive = 0xffu) {
   using G = FcwGeo<NB>;
   constexpr int ROW_KB = 128;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1184,7 +1187,7 @@ __device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_r
   asm volatile("" ::: "memory");
   bf16x8 as[2][3];
   bf16x8 b0[3], b1[3];
-  const bool live = m0 + 32 * wave < M;   // wave-uniform: some of this wave's rows are real
+  const bool live = m0 + 32 * wave < M && ((wlive >> wave) & 1u);   // wave-uniform: some rows to compute
   if (live) {
     for (int s = 0; s < nk; ++s) {
       const char* base = smem + (s % NS) * G::STAGE;
@@ -1263,7 +1266,7 @@ __device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_r
   }
 }
 
-template <int LAYER, int EPI, int TM>
+template <int LAYER, int EPI, int TM, int NB = FCW_NB, int NS = 2>
 __device__ __forceinline__ void gemm_fc_h3w_body(const GemmArgs& p, char* smem) {
   static_assert(EPI == EPI_PARTIAL, "split-K partial slabs only");
   const unsigned nblk = gridDim.x, bid = blockIdx.x;
@@ -1294,11 +1297,11 @@ __device__ __forceinline__ void gemm_fc_h3w_body(const GemmArgs& p, char* smem) 
   }
   if (p.ks_mask && !((p.ks_mask[mt] >> ks) & 1u)) return;   // slab unchanged: partials already in C
   const long long m0 = mt * X6P_BM;
-  const int n0 = nt * FCW_BN;
+  const int n0 = nt * 16 * NB;
   const int kb_total = (int)(p.ldb / GBK);
   const int gs0 = ks * (p.kper / GBK);
   constexpr int ROW_KB = 128;
-  fc_h3w_tile<TM>(p.A, p.a_rows, 0, p.lda / GBK, gs0, p.M, (const char*)p.Bp + ((long long)n0 * kb_total + gs0) * ROW_KB,
+  fc_h3w_tile<TM, NB, NS>(p.A, p.a_rows, 0, p.lda / GBK, gs0, p.M, (const char*)p.Bp + ((long long)n0 * kb_total + gs0) * ROW_KB,
                   kb_total, p.kper / GBK, p.C + (long long)ks * p.split_stride, p.ldc, p.n_store, m0, n0, smem);
 }
 
@@ -1306,6 +1309,15 @@ template <int LAYER, int EPI, int TM = 0>
 __global__ __launch_bounds__(512, 1) void beluga_fc_h3w(GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * FCW_STAGE];
   gemm_fc_h3w_body<LAYER, EPI, TM>(p, smem);
+}
+
+// the same split-K GEMM on 112-column tiles and a 3-stage ring (the direct FC1 / FC2 of small
+// per-window batches: 3x the workgroups at a third of the work each; an output's products and k
+// order do not depend on the tile width, so the same bits)
+template <int LAYER, int EPI>
+__global__ __launch_bounds__(512, 1) void beluga_fc_h3w_narrow(GemmArgs p) {
+  __shared__ __attribute__((aligned(1024))) char smem[3 * FcwGeo<7>::STAGE];
+  gemm_fc_h3w_body<LAYER, EPI, 0, 7, 3>(p, smem);
 }
 
 // ---- grouped wide FC GEMM: several split-K partial GEMMs in one launch ----------------------
@@ -1361,11 +1373,12 @@ __device__ __forceinline__ void fc_h3k_body(const FcGroup& g, char* smem) {
     mt = r / g.n_tiles;
   }
   const FcDesc& d = g.d[k];
-  if (d.mask && !(d.mask[mt] & 1u)) return;
+  const unsigned mw = d.mask ? d.mask[mt] : 0x1ffu;   // bit 0 the tile, bits 1..8 its waves
+  if (!(mw & 1u)) return;
   const int n0 = nt * 16 * NB;
   constexpr int ROW_KB = 128;
   fc_h3w_tile<TM, NB, NS>(d.A, d.a_rows, d.a_off, 0, 0, d.M, d.Bp + (long long)n0 * g.kb_total * ROW_KB, g.kb_total,
-                          d.nk, d.C, g.ldc, g.n_store, (long long)mt * X6P_BM, n0, smem);
+                          d.nk, d.C, g.ldc, g.n_store, (long long)mt * X6P_BM, n0, smem, (mw >> 1) & 0xffu);
 }
 
 template <int TM = 0>
@@ -1536,16 +1549,18 @@ __device__ __forceinline__ int conv_swz(int r) {
 // The wave's 4*MB pooled rows x 160 columns are split into its private LDS area in the planes
 // layout, then stored as 16-B chunks (one contiguous 640-B run per pooled row) instead of two
 // 2-byte stores per value.  Same values as gemm_epilogue16<EPI_RELU_POOL4, 2>.
-template <int MB, bool CANON = false, bool BATCH = true>
-__device__ __forceinline__ void epilogue_pool_h2_lds(const GemmArgs& p, const floatx4v (&acc)[MB][10], long long mw,
+template <int MB, bool CANON = false, bool BATCH = true, int NB = 10>
+__device__ __forceinline__ void epilogue_pool_h2_lds(const GemmArgs& p, const floatx4v (&acc)[MB][NB], long long mw,
                                                      int n0, int lane, char* lds) {
   static_assert(4 * MB <= 32, "pooled rows per wave exceed the LDS area");
+  static_assert(NB % 2 == 0, "whole 32-column blocks");
+  constexpr int CPR = 4 * NB;                          // 16-B chunks per staged row (40 | 32 | 16)
   const int fr = lane & 15, fq = lane >> 4;
-  float csov[10], bov[10];
-  epi_factors<BATCH>(p, n0, fr, csov, bov);
+  float csov[NB], bov[NB];
+  epi_factors<BATCH, NB>(p, n0, fr, csov, bov);
   float vmax = 0.f;   // overflow: running max, one flag store at the end
 #pragma unroll
-  for (int nb = 0; nb < 10; ++nb) {
+  for (int nb = 0; nb < NB; ++nb) {
     const float cso = csov[nb], bo = bov[nb];
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
@@ -1567,8 +1582,8 @@ __device__ __forceinline__ void epilogue_pool_h2_lds(const GemmArgs& p, const fl
   const long long w0 = mw / p.s_in;
   const int t0 = (int)(mw - w0 * p.s_in);
 #pragma unroll 5
-  for (int i = 0; i < (4 * MB * 40) / 64; ++i) {
-    const int k = i * 64 + lane, row = k / 40, ch = k - row * 40;
+  for (int i = 0; i < (4 * MB * CPR) / 64; ++i) {
+    const int k = i * 64 + lane, row = k / CPR, ch = k - row * CPR;
     const long long m4 = mw + 4 * row;                  // first conv row of pooled row `row`
     if (m4 < p.M) {
       long long w;
@@ -1971,9 +1986,12 @@ __device__ __forceinline__ void conv12_producer(const GemmArgs& p, char* smem, l
 template <int LAYER, int EPI, int TM, int NSB, int NB = 10>
 __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem) {
   static_assert(NSB == 3 || NSB == 4, "B ring depth");
-  // NB 16-column blocks per tile: 10 (160 columns), or 4 (64: conv5 / conv6 of small batches, 2.5x
-  // the workgroups; an output's products and k order do not depend on the tile width -- same bits)
-  static_assert(NB == 10 || (NB == 4 && EPI == EPI_RELU && (TM & H3P_FUSE_CONV1) == 0), "conv tile width");
+  // NB 16-column blocks per tile: 10 (160 columns), 8 (128: conv3 / conv4 of small batches, 4 N
+  // tiles of 480 outputs -- the weight planes carry 32 zero rows -- so 62 M tiles x 4 fit one round
+  // of 256 CUs at batch 32 where 3 N tiles left 70 idle) or 4 (64: conv5 / conv6 of small batches,
+  // 2.5x the workgroups); an output's products and k order do not depend on the tile width: same bits
+  static_assert(NB == 10 || ((NB == 4 || NB == 8) && (TM & H3P_FUSE_CONV1) == 0 &&
+                             (EPI == EPI_RELU || EPI == EPI_RELU_POOL4)), "conv tile width");
   constexpr int JB = NB / 2;                          // B pieces per producer wave and stage (of 2 NB)
   // PF (NSB 4): producers keep one stage less in flight, so at the end of stage s the consumers
   // can already read stage s+1's first B fragments (and, at a chunk's last tap, the next slab's
@@ -2199,7 +2217,8 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
       epilogue_relu_h2_lds<4, (TM & 8192) == 0, NB, (TM & 512) != 0>(p, acc, m0 + wave * 64, n0, lane,
                                                                     smem + wave * H3E_WAVE);
     else
-      epilogue_pool_h2_lds<4, LAYER == 4, (TM & 8192) == 0>(p, acc, m0 + wave * 64, n0, lane, smem + wave * H3E_WAVE);
+      epilogue_pool_h2_lds<4, LAYER == 4, (TM & 8192) == 0, NB>(p, acc, m0 + wave * 64, n0, lane,
+                                                                 smem + wave * H3E_WAVE);
     if constexpr (ST) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned long long t = h3p_stamp();
@@ -2222,11 +2241,12 @@ __global__ __launch_bounds__(512, 1) void beluga_conv_h3p(GemmArgs p) {
   gemm_conv_h3p_body<LAYER, EPI, TM, NSB>(p, smem);
 }
 
-// the same kernel on 64-column tiles (conv5 / conv6 of small per-window batches; same bits)
-template <int LAYER, int EPI>
+// the same kernel on 64-column (NB 4: conv5 / conv6) or 128-column (NB 8: conv3 / conv4) tiles for
+// small per-window batches (same bits)
+template <int LAYER, int EPI, int NB = 4>
 __global__ __launch_bounds__(512, 1) void beluga_conv_h3p_narrow(GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[h3c_lds<4>()];
-  gemm_conv_h3p_body<LAYER, EPI, 256, 4, 4>(p, smem);
+  gemm_conv_h3p_body<LAYER, EPI, 256, 4, NB>(p, smem);
 }
 
 // B planes for beluga_gemm_x6q from a K-contiguous fp32 B [rows][K] (K % 32 == 0).

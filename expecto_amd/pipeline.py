@@ -358,7 +358,8 @@ class VariantPipeline:
         batch-times for a flagged fraction f, against 2 for the whole batch.  If no slice flags
         again, the whole batch is recomputed in bf16x6 (counted once).  Returns the number of
         bf16x6 recomputations, as the engine's fallback counter counts them: one per flagged
-        slice, or 1 when the whole batch was recomputed."""
+        slice, or 1 when the whole batch was recomputed; ``self.last_recomputed_slices`` holds the
+        number of slices whose rows were recomputed (all `parts` slices in the second case)."""
         eng = self.engine
         n = len(vs)
         if n == 0:
@@ -390,7 +391,9 @@ class VariantPipeline:
             with eng.precision_override("bf16x6"):
                 self.predict(self.prepare(vs, shifts, rows), out=out)
             eng.count_fallback()
-            redone = 1
+            self.last_recomputed_slices = k
+            return 1
+        self.last_recomputed_slices = redone
         return redone
 
     def sed_features(self, y: torch.Tensor, weights: torch.Tensor, out: torch.Tensor | None = None,

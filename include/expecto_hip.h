@@ -204,7 +204,10 @@ long long expecto_beluga_f16_fallbacks(expecto_beluga_t h, int* sx);
  * the device until expecto_beluga_overflow_pending() is called at the caller's release point
  * (before outputs are copied out), which syncs `stream`, returns 1 if any call since the last
  * check overflowed (and clears the flag; the caller then recomputes those calls with BF16X6),
- * else 0 (< 0 on error). */
+ * else 0 (< 0 on error).  One exception to "no host sync": expecto_beluga_forward_onehot on a
+ * handle that holds the k-mer tables runs a one-hot check pass over x and syncs once per call to
+ * pick its path (codes through the tables, or the MFMA conv1 / conv2 for other floats) before it
+ * enqueues the forward; EXPECTO_ONEHOT_CODES=0 (always the MFMA path) or forward_codes avoid it. */
 int expecto_beluga_set_overflow_check(expecto_beluga_t h, int deferred);
 int expecto_beluga_overflow_pending(expecto_beluga_t h, void* stream);
 /* Deferred mode, streamed batches: enqueue on `stream` a copy of the flag into *dst (pinned host

@@ -160,3 +160,25 @@ def test_variant_tables_and_decay_table_follow_predict_py():
     assert tab.shape[1] == int(fl.max()) + 1
     for k, c in enumerate(DECAY):
         np.testing.assert_array_equal(tab[k][fl.astype(int)], np.exp(-c * fl))
+
+
+def test_beluga_parameter_slots_follow_replaced_modules():
+    """Beluga._params caches each parameter's owner module once (host time per forward) and checks
+    the cached module links by identity: a replaced submodule, a reassigned parameter and a replica
+    with its own module dicts (DataParallel's _replicate_for_data_parallel) all resolve to the
+    parameters the module holds now."""
+    import torch
+    from expecto_amd.beluga import Beluga
+    m = Beluga()
+    p0 = m._params()
+    assert p0[0] is m.model[0][0].weight and p0[-1] is m.model[1][4][1].bias
+    m.model[0][0] = torch.nn.Conv2d(4, 320, (1, 8))
+    assert m._params()[0] is m.model[0][0].weight and m._params()[0] is not p0[0]
+    m.model[0][2].bias = torch.nn.Parameter(torch.zeros(320))
+    assert m._params()[3] is m.model[0][2].bias
+    r = m._replicate_for_data_parallel()
+    r._modules["model"] = m.model._replicate_for_data_parallel()
+    r.model._modules["0"] = torch.nn.Sequential(*[c for c in m.model[0]])
+    r.model[0]._modules["0"] = torch.nn.Conv2d(4, 320, (1, 8))
+    assert r._params()[0] is r.model[0][0].weight and r._params()[0] is not m._params()[0]
+    assert m._params()[0] is m.model[0][0].weight

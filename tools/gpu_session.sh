@@ -11,6 +11,8 @@
 #   gbpmc    SQ stall counter sets of gemm_bench $GB_ARGS, VARIANT=$V
 #   ckstamp  tools/ck_bench per conv layer with the stamp build (barrier / vmcnt / epilogue shares) -> ck_<layer>.log
 #   convpmc  SQ stall counter sets of the headline's conv kernels (beluga_conv_h3p only)  -> convpmc_<i>_$TAG/
+#   sb       tools/small_batch_probe.py: batch 32 / 200 / 512 Beluga.forward, device-resident and the
+#            reference's H2D + forward + D2H pattern; then a kernel trace of it -> sb.log, sbt/
 #   writes   tools/write_probe.py, 8 writers at configs[3]'s full size: plain, staggered, staggered with 4 threads
 #
 #   STEPS=tests,bench TAG=r04 /usr/local/graft/bin/gpurun -- bash tools/gpu_session.sh
@@ -83,6 +85,10 @@ if has convpmc; then
     run convpmc_${i}_$TAG 300 rocprofv3 --pmc $ctrs --kernel-include-regex beluga_conv_h3p --kernel-trace \
       --output-format csv -d $OUT/convpmc_${i}_$TAG -o run -- $B --steps 1 --warmup 1
   done
+fi
+if has sb; then
+  run sb 300 python -u tools/small_batch_probe.py
+  run sbt 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/sbt -o run -- python3 $REPO/tools/small_batch_probe.py --trace
 fi
 if has writes; then
   run writes_plain 600 python -u tools/write_probe.py --ranks 8 --variants 100000 --dir /tmp/wp
