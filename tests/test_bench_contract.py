@@ -11,8 +11,11 @@ sys.path.insert(0, ROOT)
 
 
 def _latest_profile():
-    tags = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")))
-    assert tags, "no profiles/<round> directory"
+    """The newest profiles/<round> holding a headline kernel trace (a round's directory may hold
+    probe summaries before its trace is taken)."""
+    tags = sorted(t for t in glob.glob(os.path.join(ROOT, "profiles", "r*"))
+                  if os.path.exists(os.path.join(t, "kernel_stats.csv")))
+    assert tags, "no profiles/<round> directory with kernel_stats.csv"
     return tags[-1]
 
 
