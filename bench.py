@@ -127,9 +127,10 @@ def kernel_name(layer: str, precision: str, segments: bool = True) -> str:
             return "beluga_fc_h3k"                         # FC1 products + tail: one grouped launch
         if l in (7, 8):   # split-K FC GEMMs on 336-column tiles (beluga_fc_h3w)
             return f"beluga_fc_h3w<{l}, {e}, 0>"
+        ea = 64 if os.environ.get("EXPECTO_CONV_EA", "1") != "0" else 0   # early next-stage reads (TM bit 64)
         if layer == "conv2" and os.environ.get("EXPECTO_FUSE_CONV1", "1") != "0":
-            return f"beluga_conv_h3p<{l}, {e}, 16640, 4>"   # conv1 fused into the producers (256 | 16384)
-        return f"beluga_conv_h3p<{l}, {e}, 256, 4>"   # producer / consumer 256-row tiles (every conv layer)
+            return f"beluga_conv_h3p<{l}, {e}, {16640 + ea}, 4>"   # conv1 fused into the producers (256 | 16384)
+        return f"beluga_conv_h3p<{l}, {e}, {256 + ea}, 4>"   # producer / consumer 256-row tiles (every conv layer)
     return f"beluga_gemm<{l}, {e}, 4, 2, 32, 1>"
 
 

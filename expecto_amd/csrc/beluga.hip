@@ -1560,6 +1560,7 @@ struct expecto_beluga {
   int fc1_m_group = 8;                // order 3: M tiles per group (EXPECTO_FC1_M_GROUP)
   bool fc_wide = true;                // f16x3 FC split-K GEMMs on 336-column tiles (EXPECTO_FC_WIDE; same bits)
   int conv_tile = 0;                  // f16x3 conv M tile: 0 = auto (conv_tile_rows), 256 or 384
+  bool conv_ea = true;                // f16x3 conv consumers' early next-stage reads (EXPECTO_CONV_EA)
   int fc1_narrow = -1;                // grouped FC1 tile width: -1 auto (fc1_narrow), 0 336, 1 112 columns
   int conv_narrow = -1;               // conv5 / conv6 tile width: -1 auto (conv_narrow), 0 160, 1 64 columns
   bool narrow_scope = false;          // inside forward_chunk: auto narrow tiles allowed (nothing runs beside)
@@ -1890,6 +1891,10 @@ struct DeltaScope {
 // Arithmetic of the MFMA GEMMs: exact fp32 (v_mfma_f32_32x32x2_f32), the fp32-faithful 3-way
 // bf16 split (bf16x6) or the scaled 2-way fp16 split (f16x3), gemm_kernel.h.
 thread_local int g_precision = EXPECTO_PRECISION_BF16X6;
+// f16x3 conv consumers read the next stage's operands inside the stage's last unit (gemm_kernel.h
+// gemm_conv_h3p_body EA, TM bit 64; EXPECTO_CONV_EA=0 restores the reads after the last MFMA; same
+// bits either way), set from the handle with g_precision
+thread_local bool g_conv_ea = true;
 
 // activation storage format (gemm_kernel.h): 1 bf16 planes (bf16x6), 2 scaled fp16 planes
 // (f16x3), 0 fp32 rows; bytes per element 6 / 4 / 4
@@ -1975,14 +1980,17 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
       if (a.c1_codes) {   // conv2 with conv1 fused into the producers (A slabs from base codes)
         if constexpr (LAYER == 2 && EPI == EPI_RELU_POOL4) {
           EXPECTO_REQUIRE(bm == 256 && a.c1_w && a.c1_cs && a.c1_b, "fused conv1: 256-row tiles, conv1 planes");
-          beluga_conv_h3p<LAYER, EPI, 256 | H3P_FUSE_CONV1, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
+          if (g_conv_ea)
+            beluga_conv_h3p<LAYER, EPI, 256 | 64 | H3P_FUSE_CONV1, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
+          else
+            beluga_conv_h3p<LAYER, EPI, 256 | H3P_FUSE_CONV1, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
         } else {
           EXPECTO_REQUIRE(false, "fused conv1: conv2 + pool1 only");
         }
       } else if (a.n_tile_cols == 64) {   // 64-column tiles (conv_narrow: conv5 / conv6 of small batches)
         if constexpr ((LAYER == 5 || LAYER == 6) && EPI == EPI_RELU) {
           EXPECTO_REQUIRE(bm == 256 && a.n_tiles * 64 >= a.n_store, "64-column conv tiles: 256 rows");
-          beluga_conv_h3p_narrow<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
+          beluga_conv_h3p_narrow<LAYER, EPI, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
         } else {
           EXPECTO_REQUIRE(false, "64-column conv tiles: conv5 / conv6 only");
         }
@@ -1995,6 +2003,8 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
         }
       } else if (bm == 384)
         beluga_conv_h3r<LAYER, EPI><<<dim3((unsigned)nblk), dim3(256), 0, st>>>(a);
+      else if (g_conv_ea)   // 4-deep B ring, next-stage fragments read inside the stage's last unit (TM 256 | 64)
+        beluga_conv_h3p<LAYER, EPI, 256 | 64, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
       else   // 4-deep B ring, next-stage fragments read before the stage barrier (TM 256)
         beluga_conv_h3p<LAYER, EPI, 256, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
     } else if constexpr (EPI == EPI_PARTIAL) {
@@ -2629,6 +2639,7 @@ int forward_chunk(expecto_beluga* h, const float* x, const uint8_t* codes, long 
                   int mode, long long row0, int nb, float* y, hipStream_t st) {
   int rc;
   g_precision = h->precision;
+  g_conv_ea = h->conv_ea;
   struct Scope {
     expecto_beluga* h;
     ~Scope() { h->narrow_scope = false; }
@@ -2722,6 +2733,7 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
                      hipStream_t st, const SegPairs* pr = nullptr) {
   EXPECTO_REQUIRE(L >= kLen && L % 4 == 0, "segment length must be >= 2000 and a multiple of 4");
   g_precision = h->precision;
+  g_conv_ea = h->conv_ea;
   int rc;
   if (pr && (rc = ensure_delta(h))) return rc;
   // phases present (fwd and, for BOTH, the mirrored rc offsets)
@@ -3279,6 +3291,7 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
 int forward_pairs(expecto_beluga* h, const uint8_t* ref, const uint8_t* alt, int n, long long stride,
                   const int* var_pos, int mode, float* y_ref, float* y_alt, long long strand_stride, hipStream_t st) {
   g_precision = h->precision;
+  g_conv_ea = h->conv_ea;
   const int strands = mode == EXPECTO_STRAND_BOTH ? 2 : 1;
   int rc;
   if ((rc = ensure_delta(h))) return rc;
@@ -3644,6 +3657,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
     EXPECTO_REQUIRE(v >= -1 && v <= 1, "EXPECTO_FC1_NARROW must be -1 (auto), 0 or 1");
     h->fc1_narrow = v;
   }
+  if (const char* e = getenv("EXPECTO_CONV_EA")) h->conv_ea = atoi(e) != 0;   // same bits either way
   if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)
     const int v = atoi(e);
     EXPECTO_REQUIRE(v == 0 || v == 256 || v == 384, "EXPECTO_CONV_TILE must be 0 (auto), 256 or 384");

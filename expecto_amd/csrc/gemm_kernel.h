@@ -2160,6 +2160,29 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
       __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
     }
   };
+  // EA (TM & 64, PF only): the next stage's operands are read INSIDE the stage's last unit -- B
+  // fragment 0 of stage s+1 first (b0 is free there: the last unit, NB - 1 odd, runs on b1), then
+  // row block mb's A fragments of the next tap right after mb's 3 MFMAs -- instead of all 10 reads
+  // after the last MFMA, where the 4 waves' 40 KB of LDS reads met the next stage's first MFMAs
+  // across the barrier (tools/ck_bench stamp build: 2,210 cycles per 1,920-cycle stage, unchanged
+  // with no loads at all).  The reads go to the same registers, branch-free (past the tile's last
+  // stage they re-read resident LDS into registers nothing uses); same MFMAs in the same order.
+  constexpr bool EA = PF && (TM & 64) != 0;
+  static_assert(!EA || (NB % 2) == 0, "EA: the last unit runs on b1");
+  auto read_a1 = [&](const char* slab, int t, int mb, bf16x8 (&a)[3]) {
+    const int rr2 = fr + t;
+    const int off = (wave * 64 + rr2) * 64 + 16 * (fq ^ swz(rr2));
+    a[0] = *(const bf16x8*)(slab + off + mb * 1024);
+    a[1] = *(const bf16x8*)(slab + off + mb * 1024 + G::APLANE);
+  };
+  auto pin_last = [&]() {
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // next stage's b0
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);   // row block mb's 3 products
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // its next-tap A fragments
+    }
+  };
   __builtin_amdgcn_s_barrier();                       // slab 0 and B stage 0 landed
   asm volatile("" ::: "memory");
   bf16x8 as[4][3];
@@ -2179,16 +2202,31 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
         if (nb + 1 < NB) read_b(base, nb + 1, (nb & 1) ? b0 : b1);
+        if (EA && nb == NB - 1) {
+          // next tap of this slab, or tap 0 of the next chunk's slab (landed by tap 6's barrier)
+          const char* nsl = t < 7 ? slab : aslab + ((c + 1) & 1) * G::ASLAB;
+          const int ntap = t < 7 ? t + 1 : 0;
+          read_b(bring + nslot * H3C_BSTAGE, 0, b0);   // stage s+1 landed at barrier s-1
+#pragma unroll
+          for (int mb = 0; mb < 4; ++mb) {
+            acc[mb][nb] = planes_mfma<2>(acc[mb][nb], as[mb], b1);
+            read_a1(nsl, ntap, mb, as[mb]);
+          }
+          pin_last();
+          continue;
+        }
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb) acc[mb][nb] = planes_mfma<2>(acc[mb][nb], as[mb], (nb & 1) ? b1 : b0);
         pin();
       }
-      if (t < 7)
-        read_a(slab, t + 1, as);   // slab reads stay in flight across the barrier
-      else if (PF && c + 1 < nchunk)
-        read_a(aslab + ((c + 1) & 1) * G::ASLAB, 0, as);   // next slab landed by tap 6's barrier
-      if constexpr (PF) {
-        if (c * 8 + t + 1 < nk) read_b(bring + nslot * H3C_BSTAGE, 0, b0);   // stage s+1 landed at barrier s-1
+      if constexpr (!EA) {
+        if (t < 7)
+          read_a(slab, t + 1, as);   // slab reads stay in flight across the barrier
+        else if (PF && c + 1 < nchunk)
+          read_a(aslab + ((c + 1) & 1) * G::ASLAB, 0, as);   // next slab landed by tap 6's barrier
+        if constexpr (PF) {
+          if (c * 8 + t + 1 < nk) read_b(bring + nslot * H3C_BSTAGE, 0, b0);   // stage s+1 landed at barrier s-1
+        }
       }
       unsigned long long t1 = 0;
       if constexpr (ST) t1 = h3p_stamp();
@@ -2246,7 +2284,7 @@ __global__ __launch_bounds__(512, 1) void beluga_conv_h3p(GemmArgs p) {
 template <int LAYER, int EPI, int NB = 4>
 __global__ __launch_bounds__(512, 1) void beluga_conv_h3p_narrow(GemmArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[h3c_lds<4>()];
-  gemm_conv_h3p_body<LAYER, EPI, 256, 4, NB>(p, smem);
+  gemm_conv_h3p_body<LAYER, EPI, 256 | 64, 4, NB>(p, smem);   // early next-stage reads (EA)
 }
 
 // B planes for beluga_gemm_x6q from a K-contiguous fp32 B [rows][K] (K % 32 == 0).

@@ -47,7 +47,8 @@ def _run(monkeypatch, env, fa, dg, vs, shifts, max_batch=2048, use_segments=True
                                  {"EXPECTO_FC_WIDE": "0", "EXPECTO_FC1_ORDER": "0", "EXPECTO_FC1_M_ORDER_MB": "0"},
                                  {"EXPECTO_FC_WIDE": "0", "EXPECTO_FC1_M_GROUP": "3"},
                                  {"EXPECTO_FC1K_SLICE": "700"}, {"EXPECTO_FC1_NARROW": "1"},
-                                 {"EXPECTO_CONV_NARROW": "1"}])
+                                 {"EXPECTO_CONV_NARROW": "1"}, {"EXPECTO_CONV_EA": "0"},
+                                 {"EXPECTO_CONV_EA": "0", "EXPECTO_CONV2_TABLE": "0"}])
 def test_same_bits_knobs(monkeypatch, env):
     fa, dg, vs, shifts = _setup()
     want = _run(monkeypatch, {}, fa, dg, vs, shifts)
@@ -57,10 +58,10 @@ def test_same_bits_knobs(monkeypatch, env):
 
 def test_tile_widths_small_batches(monkeypatch):
     """Per-window batches take narrower N tiles where they need fewer rounds of workgroups: the
-    grouped FC1 112 instead of 336 columns (beluga.hip fc1_narrow; its part-filled M tiles' empty
-    waves skip their MFMAs), conv5 / conv6 64 instead of 160 (conv_narrow).  Batch 5 / 32 / 200 /
-    512 in FC1 roles 0, 3 and the direct FC1: the same bits as the wide tiles (EXPECTO_FC1_NARROW=0,
-    EXPECTO_CONV_NARROW=0)."""
+    grouped FC1, the direct FC1 and FC2 112 instead of 336 columns (beluga.hip fc1_narrow; part-filled
+    M tiles' empty waves skip their MFMAs), conv3 / conv4 128 and conv5 / conv6 64 instead of 160
+    (conv_narrow).  Batch 5 / 32 / 200 / 512 in FC1 roles 0, 3 and the direct FC1: the same bits as
+    the wide tiles (EXPECTO_FC1_NARROW=0, EXPECTO_CONV_NARROW=0)."""
     from expecto_amd import beluga
     rng = np.random.default_rng(61)
     codes = torch.from_numpy(rng.integers(0, 5, (512, 2000)).astype(np.uint8)).cuda()

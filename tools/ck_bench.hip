@@ -123,6 +123,8 @@ int main(int argc, char** argv) {
     vs.push_back(mkp<5>("direct_h3p"));
     vs.push_back(mkp<5, 256 | H3P_STAMP>("direct_stamp"));
     vs.push_back(mkp<5, 256 | 2048>("direct_noepi"));
+    vs.push_back(mkp<5, 256 | 64>("direct_ea"));
+    vs.push_back(mkp<5, 256 | 64 | H3P_STAMP>("direct_stamp_ea"));
     vs.push_back(mkp<5, 256 | 512>("direct_nostore"));
     vs.push_back(mkp<5, 256 | 2>("direct_noload"));
     vs.push_back(mkp<5, 256 | H3P_STAMP | 8>("direct_stamp_hotAB"));
@@ -133,6 +135,8 @@ int main(int argc, char** argv) {
     vs.push_back(mkp<6>("direct_h3p"));
     vs.push_back(mkp<6, 256 | H3P_STAMP>("direct_stamp"));
     vs.push_back(mkp<6, 256 | 2048>("direct_noepi"));
+    vs.push_back(mkp<6, 256 | 64>("direct_ea"));
+    vs.push_back(mkp<6, 256 | 64 | H3P_STAMP>("direct_stamp_ea"));
     vs.push_back(mkp<6, 256 | 512>("direct_nostore"));
     vs.push_back(mkp<6, 256 | 2>("direct_noload"));
     vs.push_back(mkp<6, 256 | H3P_STAMP | 8>("direct_stamp_hotAB"));
@@ -143,6 +147,8 @@ int main(int argc, char** argv) {
     vs.push_back(mkp<4>("direct_h3p"));
     vs.push_back(mkp<4, 256 | H3P_STAMP>("direct_stamp"));
     vs.push_back(mkp<4, 256 | 2048>("direct_noepi"));
+    vs.push_back(mkp<4, 256 | 64>("direct_ea"));
+    vs.push_back(mkp<4, 256 | 64 | H3P_STAMP>("direct_stamp_ea"));
     vs.push_back(mkp<4, 256 | 512>("direct_nostore"));
     vs.push_back(mkp<4, 256 | 2>("direct_noload"));
     vs.push_back(mkp<4, 256 | H3P_STAMP | 8>("direct_stamp_hotAB"));
@@ -162,6 +168,8 @@ int main(int argc, char** argv) {
     vs.push_back(mkp<3>("direct_h3p"));
     vs.push_back(mkp<3, 256 | H3P_STAMP>("direct_stamp"));
     vs.push_back(mkp<3, 256 | 2048>("direct_noepi"));
+    vs.push_back(mkp<3, 256 | 64>("direct_ea"));
+    vs.push_back(mkp<3, 256 | 64 | H3P_STAMP>("direct_stamp_ea"));
     vs.push_back(mkp<3, 256 | 512>("direct_nostore"));
     vs.push_back(mkp<3, 256 | 2>("direct_noload"));
     vs.push_back(mkp<3, 256 | H3P_STAMP | 8>("direct_stamp_hotAB"));
@@ -238,6 +246,44 @@ int main(int argc, char** argv) {
       best[v] = std::min(best[v], (double)ms);
       sum[v] += ms;
     }
+  // same bits: the early-read variant against the direct kernel (one launch each, output compared)
+  {
+    int iref = -1, iea = -1;
+    for (size_t v = 0; v < vs.size(); ++v) {
+      if (vs[v].name == "direct_h3p") iref = (int)v;
+      if (vs[v].name == "direct_ea") iea = (int)v;
+    }
+    if (iref >= 0 && iea >= 0) {
+      const size_t cb = (size_t)nb * s_out * cout * 4;
+      std::vector<char> h0(cb), h1(cb);
+      for (int k = 0; k < 2; ++k) {
+        GemmArgs a{};
+        a.A = reinterpret_cast<const float*>(X);
+        a.lda = cin;
+        a.M = M;
+        a.Bp = Bd;
+        a.ldb = 8 * cin;
+        a.kper = (int)a.ldb;
+        a.taps = 8;
+        a.n_tiles = npad / GBN;
+        a.m_tiles = (M + 255) / 256;
+        a.bias = bias;
+        a.col_scale = cs;
+        a.out_scale = 1.f;
+        a.ovf = ovf;
+        a.C = C;
+        a.ldc = cout;
+        a.n_store = cout;
+        a.s_in = s_in;
+        a.t_valid = t_valid;
+        a.s_out = s_out;
+        CK(hipMemset(C, 0, cb));
+        vs[k ? iea : iref].launch(a, (unsigned)(a.m_tiles * a.n_tiles));
+        CK(hipMemcpy(k ? h1.data() : h0.data(), C, cb, hipMemcpyDeviceToHost));
+      }
+      printf("direct_ea output bitwise equal to direct_h3p: %s\n", memcmp(h0.data(), h1.data(), cb) ? "NO" : "yes");
+    }
+  }
   const double alg = 2.0 * M * cout * 8.0 * cin;   // direct fp32-equivalent flops
   printf("%s, %d windows, M %lld rows\n", c4 ? "conv4 (unpooled)" : layer, nb, M);
   for (size_t v = 0; v < vs.size(); ++v)
