@@ -1603,7 +1603,8 @@ struct expecto_beluga {
   uint8_t* oh_codes = nullptr;        //   its codes, max_batch x 2000 (allocated on first use)
   int* oh_bad = nullptr;              //   its check flag
   bool oh_hint_bad = false;           //   the last input was not one-hot: check first instead of a speculative run
-  int* hflags = nullptr;              // pinned host words the per-call checks read their device flags into
+  int* hflags = nullptr;              // pinned, device-mapped host words the per-call checks read their flags into
+  int* hflags_d = nullptr;            //   their device address (take_flags writes them: no blit kernels per call)
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, int>> pending;  // (layer, event index of start)
@@ -3548,13 +3549,28 @@ int f16_prepare(expecto_beluga* h, hipStream_t st) {
 // Run one public call; on the f16x3 path check the overflow flag afterwards and, if an
 // activation did not fit fp16, recompute the whole call with bf16x6.  In deferred mode the
 // flag stays on the device for expecto_beluga_overflow_pending (the caller's release point).
+// The per-call checks' flag words into pinned, device-mapped host memory (out[0] the f16x3 overflow
+// flag, out[1] the one-hot check flag, which is reset for the next call): one tiny kernel on the
+// call's stream instead of a copy-engine blit per flag plus a memset; visible to the host after the
+// stream sync that follows.
+__global__ void take_flags(const int* __restrict__ ovf, int* __restrict__ bad, int* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  // agent-scope loads: vector loads past the CU's caches (the flags were stored by earlier kernels)
+  if (ovf) out[0] = __hip_atomic_load(ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (bad) {
+    out[1] = __hip_atomic_load(bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *bad = 0;
+  }
+}
+
 template <class F>
 int run_checked(expecto_beluga* h, hipStream_t st, F&& fn) {
   if (h->precision != EXPECTO_PRECISION_F16X3 || h->ovf_deferred) return fn();
   int rc = fn();
   if (rc) return rc;
-  int* flag = h->hflags;   // pinned: the copy is one DMA, no staging through a driver bounce buffer
-  EXPECTO_HIP_CHECK(hipMemcpyAsync(flag, h->ovf, sizeof(int), hipMemcpyDeviceToHost, st));
+  int* flag = h->hflags;   // pinned, device-mapped: one tiny kernel writes it (no copy-engine blit)
+  take_flags<<<1, 64, 0, st>>>(h->ovf, nullptr, h->hflags_d);
+  EXPECTO_HIP_CHECK(hipGetLastError());
   EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
   if (!*flag) return EXPECTO_OK;
   EXPECTO_HIP_CHECK(hipMemsetAsync(h->ovf, 0, sizeof(int), st));
@@ -3585,7 +3601,8 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
     return code;
   };
   if ((rc = dalloc(h, &h->w1, 320 * 32)) || (rc = dalloc(h, &h->b1, 320))) return fail(rc);
-  if (hipHostMalloc(&h->hflags, 4 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+  if (hipHostMalloc(&h->hflags, 4 * sizeof(int), hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hflags_d), h->hflags, 0) != hipSuccess) {
     set_error("hipHostMalloc (flag words)");
     return fail(EXPECTO_ENOMEM);
   }
@@ -3787,12 +3804,12 @@ int expecto_beluga_forward_onehot(expecto_beluga_t h, const float* x, int n, flo
     return (int)EXPECTO_OK;
   };
   if (candidate && h->precision == EXPECTO_PRECISION_F16X3 && !h->ovf_deferred && !h->oh_hint_bad) {
-    EXPECTO_HIP_CHECK(hipMemsetAsync(h->oh_bad, 0, sizeof(int), st));
+    // (oh_bad is 0 here: zeroed at allocation, and every path that sets it resets it in take_flags)
     int rc = run(true, h->oh_bad);
     if (rc) return rc;
-    int* flags = h->hflags;   // pinned host words
-    EXPECTO_HIP_CHECK(hipMemcpyAsync(&flags[0], h->ovf, sizeof(int), hipMemcpyDeviceToHost, st));
-    EXPECTO_HIP_CHECK(hipMemcpyAsync(&flags[1], h->oh_bad, sizeof(int), hipMemcpyDeviceToHost, st));
+    int* flags = h->hflags;   // pinned, device-mapped host words: ovf, oh_bad (then reset on the device)
+    take_flags<<<1, 64, 0, st>>>(h->ovf, h->oh_bad, h->hflags_d);
+    EXPECTO_HIP_CHECK(hipGetLastError());
     EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
     if (flags[1]) {   // not one-hot: the whole call on the MFMA path (its own overflow check)
       h->oh_hint_bad = true;
@@ -3818,9 +3835,10 @@ int expecto_beluga_forward_onehot(expecto_beluga_t h, const float* x, int n, flo
       int rc = check_launch("onehot_codes check");
       if (rc) return rc;
     }
-    EXPECTO_HIP_CHECK(hipMemcpyAsync(h->hflags + 2, h->oh_bad, sizeof(int), hipMemcpyDeviceToHost, st));
+    take_flags<<<1, 64, 0, st>>>(nullptr, h->oh_bad, h->hflags_d);   // (resets oh_bad)
+    EXPECTO_HIP_CHECK(hipGetLastError());
     EXPECTO_HIP_CHECK(hipStreamSynchronize(st));
-    bad = h->hflags[2];
+    bad = h->hflags[1];
     as_codes = bad == 0;
     h->oh_hint_bad = !as_codes;
   }

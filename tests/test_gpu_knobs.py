@@ -47,13 +47,22 @@ def _run(monkeypatch, env, fa, dg, vs, shifts, max_batch=2048, use_segments=True
                                  {"EXPECTO_FC_WIDE": "0", "EXPECTO_FC1_ORDER": "0", "EXPECTO_FC1_M_ORDER_MB": "0"},
                                  {"EXPECTO_FC_WIDE": "0", "EXPECTO_FC1_M_GROUP": "3"},
                                  {"EXPECTO_FC1K_SLICE": "700"}, {"EXPECTO_FC1_NARROW": "1"},
-                                 {"EXPECTO_CONV_NARROW": "1"}, {"EXPECTO_CONV_EA": "0"},
-                                 {"EXPECTO_CONV_EA": "0", "EXPECTO_CONV2_TABLE": "0"}])
+                                 {"EXPECTO_CONV_NARROW": "1"}, {"EXPECTO_CONV_EA": "0"}])
 def test_same_bits_knobs(monkeypatch, env):
     fa, dg, vs, shifts = _setup()
     want = _run(monkeypatch, {}, fa, dg, vs, shifts)
     got = _run(monkeypatch, env, fa, dg, vs, shifts)
     assert torch.equal(got, want), f"{env}: max|diff| {float((got - want).abs().max())}"
+
+
+def test_conv_early_reads_same_bits_with_fused_conv1(monkeypatch):
+    """The conv consumers' early next-stage reads (EXPECTO_CONV_EA) on the MFMA conv2 with conv1 fused
+    into its producers (EXPECTO_CONV2_TABLE=0, which itself changes conv2's sums): the same bits on
+    and off."""
+    fa, dg, vs, shifts = _setup()
+    want = _run(monkeypatch, {"EXPECTO_CONV2_TABLE": "0"}, fa, dg, vs, shifts)
+    got = _run(monkeypatch, {"EXPECTO_CONV2_TABLE": "0", "EXPECTO_CONV_EA": "0"}, fa, dg, vs, shifts)
+    assert torch.equal(got, want), f"max|diff| {float((got - want).abs().max())}"
 
 
 def test_tile_widths_small_batches(monkeypatch):

@@ -5,8 +5,8 @@ import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-rows = [r for r in rows if "rocclr" not in r["Kernel_Name"]]
-starts = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("expecto::onehot_codes")]
+rows = [r for r in rows]   # (the blit kernels of hipMemsetAsync / hipMemcpyAsync included)
+starts = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("onehot_codes") or "::onehot_codes(" in r["Kernel_Name"]]
 # forwards in order: 23 per batch (onehot_codes opens every forward of exact one-hot input)
 for b, B in enumerate((32, 200, 512)):
     k = 23 * b + 22
