@@ -589,11 +589,10 @@ __global__ void fc1_slab_mask(const int* __restrict__ var_pos, int nv, int v0, i
 
 // profiling: executed MACs of a masked FC1 = set slab bits x MACs per (tile, slab), summed into
 // acc on the device (one wave; the host reads acc when the layer times are collected)
-// (waves: the Karatsuba FC1 masks, whose bits 1..8 are the tile's computing 32-row waves)
 __global__ __launch_bounds__(64) void slab_macs(const unsigned* __restrict__ mask, int tiles, double per_bit,
-                                                double* __restrict__ acc, int waves = 0) {
+                                                double* __restrict__ acc) {
   int bits = 0;
-  for (int i = threadIdx.x; i < tiles; i += 64) bits += __popc(waves ? (mask[i] >> 1) & 0xffu : mask[i]);
+  for (int i = threadIdx.x; i < tiles; i += 64) bits += __popc(mask[i]);
   for (int o = 32; o > 0; o >>= 1) bits += __shfl_down(bits, o);
   if (threadIdx.x == 0) atomicAdd(acc, bits * per_bit);
 }
@@ -862,6 +861,7 @@ __global__ void fk_weights(const float* __restrict__ w1, long long rows, float* 
 // planes are consumed as stored), the overflow flag as any f16x3 store.  [lo, hi) = [0, T), or
 // with `tab` (segment pairs: the alt blocks seg_alt_blocks filled, n_ph blocks per segment) the
 // rows that alt block holds.  320 threads = 4 rows x 80 eight-channel pieces (16 B of hi + 16 B of lo).
+template <bool NT>
 __global__ __launch_bounds__(320) void fk_seq_h2(const float* __restrict__ x, int T, int s, const int* __restrict__ tab,
                                                  int n_ph, const int* __restrict__ gres, float* __restrict__ d1,
                                                  float* __restrict__ d2, float* __restrict__ dd, int* __restrict__ ovf) {
@@ -918,12 +918,20 @@ __global__ __launch_bounds__(320) void fk_seq_h2(const float* __restrict__ x, in
     for (int w = 0; w < 4; ++w) recv[w] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)send[w], 0x141, 0xf, 0xf, false);
     const u32x4 keep = __builtin_bit_cast(u32x4, low ? h : l);
     char* d = reinterpret_cast<char*>(dst) + blk * s * rb + row * rb + (c8 >> 3) * 256;
+    // NT: streaming stores (the 1.3 GB of sequences are read back by the next FC1 launch, far
+    // beyond L2 / MALL reuse distance)
+    auto st = [](char* p, const u32x4& v) {
+      if constexpr (NT)
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+      else
+        *reinterpret_cast<u32x4*>(p) = v;
+    };
     if (low) {   // hi quarter j of group 2m' (own), hi quarter 3 - j of group 2m'+1 (mirror's)
-      *reinterpret_cast<u32x4*>(d + j * 16) = keep;
-      *reinterpret_cast<u32x4*>(d + 128 + (3 - j) * 16) = recv;
+      st(d + j * 16, keep);
+      st(d + 128 + (3 - j) * 16, recv);
     } else {     // lo quarter 7 - j of group 2m' (mirror's), lo quarter j - 4 of group 2m'+1 (own)
-      *reinterpret_cast<u32x4*>(d + 64 + (7 - j) * 16) = recv;
-      *reinterpret_cast<u32x4*>(d + 128 + 64 + (j - 4) * 16) = keep;
+      st(d + 64 + (7 - j) * 16, recv);
+      st(d + 128 + 64 + (j - 4) * 16, keep);
     }
   };
   float v0[8], v1[8], v2[8] = {}, v3[8] = {};
@@ -1018,13 +1026,7 @@ __global__ void fk_window_tables(int M, int rstride, int role, long long* __rest
 // ref rows only in [r6, r6 + 20) (window rows), so partial (product j, slab s) -- sequence rows
 // 25 (blk - role) + [13 s - (s ? 1 : 0), 13 s + 12] with their lags -- and the tail (rows 100..105)
 // are recomputed only where a dependency row falls in that run: bit 0 of mask[d * tiles + m / 256]
-// for descriptor d = 2j + s (8 = the tail), and bit 1 + w for the tile's 32-row wave w holding m
-// (fk_wave_bits: the other waves of the tile skip their MFMAs and keep their ref partials).  Unset
-// descriptors keep the ref partials in place.
-// mask word bits of partial row i of a masked FC1 descriptor: bit 0 = its 256-row M tile runs, bit
-// 1 + w = the tile's wave w (rows 32 w .. 32 w + 31, gemm_kernel.h fc_h3w_tile) computes
-__device__ __forceinline__ unsigned fk_wave_bits(int i) { return 1u | (2u << ((i & 255) >> 5)); }
-
+// for descriptor d = 2j + s (8 = the tail).  Unset descriptors keep the ref partials in place.
 __global__ void fk_window_mask(const int* __restrict__ var_pos, int nv, int v0, int R, int role, int tiles,
                                unsigned* __restrict__ mask) {
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1042,10 +1044,10 @@ __global__ void fk_window_mask(const int* __restrict__ var_pos, int nv, int v0, 
         const int lag = l == 0 ? 0 : (nl == 2 ? lag1 : 25 * l);
         hit |= i0 + lag < r6e && i1 + lag >= r6;
       }
-      if (hit) atomicOr(mask + (2 * j + s) * tiles + m / 256, fk_wave_bits(m));
+      if (hit) atomicOr(mask + (2 * j + s) * tiles + m / 256, 1u);
     }
   }
-  if (100 < r6e && 105 >= r6) atomicOr(mask + 8 * tiles + m / 256, fk_wave_bits(m));
+  if (100 < r6e && 105 >= r6) atomicOr(mask + 8 * tiles + m / 256, 1u);
 }
 
 // Alt masks of the segment path's in-place alt FC1 (segment pairs): descriptor slot d of the ref
@@ -1067,7 +1069,7 @@ __global__ void fk_seg_mask(FkMaskDesc md, const int* __restrict__ rgrp, const i
   if (d == md.n) {   // the tail
     if (i >= md.nw) return;
     const int r6 = r6_of(winfo[2 * i]), o = winfo[2 * i + 1];
-    if (o + 100 < r6 + kDW[6] && o + 105 >= r6) atomicOr(mask + (size_t)d * tiles + i / 256, fk_wave_bits(i));
+    if (o + 100 < r6 + kDW[6] && o + 105 >= r6) atomicOr(mask + (size_t)d * tiles + i / 256, 1u);
     return;
   }
   if (i >= md.cnt[d]) return;
@@ -1081,7 +1083,7 @@ __global__ void fk_seg_mask(FkMaskDesc md, const int* __restrict__ rgrp, const i
     const int lag = l == 0 ? 0 : (nl == 2 ? lag1 : 25 * l);
     hit |= i0 + lag < r6e && i1 + lag >= r6;
   }
-  if (hit) atomicOr(mask + (size_t)d * tiles + i / 256, fk_wave_bits(i));
+  if (hit) atomicOr(mask + (size_t)d * tiles + i / 256, 1u);
 }
 
 // ---- weight repacking (reference layouts -> kernel layouts) --------------------------
@@ -1561,6 +1563,7 @@ struct expecto_beluga {
   bool fc_wide = true;                // f16x3 FC split-K GEMMs on 336-column tiles (EXPECTO_FC_WIDE; same bits)
   int conv_tile = 0;                  // f16x3 conv M tile: 0 = auto (conv_tile_rows), 256 or 384
   bool conv_ea = true;                // f16x3 conv consumers' early next-stage reads (EXPECTO_CONV_EA)
+  bool fk_seq_nt = true;              // FC1 sequences written with streaming stores (EXPECTO_FK_SEQ_NT; same bits)
   int fc1_narrow = -1;                // grouped FC1 tile width: -1 auto (fc1_narrow), 0 336, 1 112 columns
   int conv_narrow = -1;               // conv5 / conv6 tile width: -1 auto (conv_narrow), 0 160, 1 64 columns
   bool narrow_scope = false;          // inside forward_chunk: auto narrow tiles allowed (nothing runs beside)
@@ -2395,7 +2398,10 @@ int fk_sequences(expecto_beluga* h, const float* x, long long blocks, int T, int
   LayerTimer lt(h, 7, st);   // the sequences are timed with the FC1 reduction (slot fc1_reduce)
   const long long nblk = blocks * 7;   // 7 workgroups of 4 residue walks per block
   EXPECTO_REQUIRE(nblk > 0 && nblk < (1LL << 31), "FC1 sequence grid");
-  fk_seq_h2<<<dim3((unsigned)nblk), dim3(320), 0, st>>>(x, T, s, tab, n_ph, gres, out[0], out[1], out[2], h->ovf);
+  if (h->fk_seq_nt)
+    fk_seq_h2<true><<<dim3((unsigned)nblk), dim3(320), 0, st>>>(x, T, s, tab, n_ph, gres, out[0], out[1], out[2], h->ovf);
+  else
+    fk_seq_h2<false><<<dim3((unsigned)nblk), dim3(320), 0, st>>>(x, T, s, tab, n_ph, gres, out[0], out[1], out[2], h->ovf);
   return check_launch("fk_seq_h2");
 }
 
@@ -2631,7 +2637,7 @@ int count_desc_macs(expecto_beluga* h, const unsigned* mask, int tiles, double p
     h->macs_d = reinterpret_cast<double*>(f);
     EXPECTO_HIP_CHECK(hipMemsetAsync(h->macs_d, 0, 2 * kNumLayers * sizeof(double), st));
   }
-  slab_macs<<<dim3(1), dim3(64), 0, st>>>(mask, tiles, per_tile / 8, h->macs_d + h->timer_base + 6, 1);
+  slab_macs<<<dim3(1), dim3(64), 0, st>>>(mask, tiles, per_tile, h->macs_d + h->timer_base + 6);
   return check_launch("slab_macs");
 }
 
@@ -3675,6 +3681,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
     h->fc1_narrow = v;
   }
   if (const char* e = getenv("EXPECTO_CONV_EA")) h->conv_ea = atoi(e) != 0;   // same bits either way
+  if (const char* e = getenv("EXPECTO_FK_SEQ_NT")) h->fk_seq_nt = atoi(e) != 0;   // same bits either way
   if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)
     const int v = atoi(e);
     EXPECTO_REQUIRE(v == 0 || v == 256 || v == 384, "EXPECTO_CONV_TILE must be 0 (auto), 256 or 384");

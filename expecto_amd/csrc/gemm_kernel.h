@@ -1070,13 +1070,10 @@ struct FcwGeo {
   static_assert(2 * STAGE >= 8 * FCW_EWAVE, "epilogue staging inside the stage ring");
 };
 
-// wlive: bit w = wave w (rows 32 w ..) computes; a masked in-place alt launch clears the bits of
-// the waves none of whose rows it must recompute (they skip MFMAs, reads and stores, as waves past M)
 template <int TM, int NB = FCW_NB, int NS = 2>
 __device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_rows, long long a_off, long long lda_kb,
                                             int kb0a, long long M, const char* Bb, int kb_total, int nk, float* cbase,
-                                            long long ldc, int n_store, long long m0, int n0, char* smem,
-                                            unsigned wlive = 0xffu) {
+                                            long long ldc, int n_store, long long m0, int n0, char* smem) {
   using G = FcwGeo<NB>;
   constexpr int ROW_KB = 128;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1187,7 +1184,7 @@ __device__ __forceinline__ void fc_h3w_tile(const float* A, const long long* a_r
   asm volatile("" ::: "memory");
   bf16x8 as[2][3];
   bf16x8 b0[3], b1[3];
-  const bool live = m0 + 32 * wave < M && ((wlive >> wave) & 1u);   // wave-uniform: some rows to compute
+  const bool live = m0 + 32 * wave < M;   // wave-uniform: some of this wave's rows are real
   if (live) {
     for (int s = 0; s < nk; ++s) {
       const char* base = smem + (s % NS) * G::STAGE;
@@ -1373,12 +1370,11 @@ __device__ __forceinline__ void fc_h3k_body(const FcGroup& g, char* smem) {
     mt = r / g.n_tiles;
   }
   const FcDesc& d = g.d[k];
-  const unsigned mw = d.mask ? d.mask[mt] : 0x1ffu;   // bit 0 the tile, bits 1..8 its waves
-  if (!(mw & 1u)) return;
+  if (d.mask && !(d.mask[mt] & 1u)) return;
   const int n0 = nt * 16 * NB;
   constexpr int ROW_KB = 128;
   fc_h3w_tile<TM, NB, NS>(d.A, d.a_rows, d.a_off, 0, 0, d.M, d.Bp + (long long)n0 * g.kb_total * ROW_KB, g.kb_total,
-                          d.nk, d.C, g.ldc, g.n_store, (long long)mt * X6P_BM, n0, smem, (mw >> 1) & 0xffu);
+                          d.nk, d.C, g.ldc, g.n_store, (long long)mt * X6P_BM, n0, smem);
 }
 
 template <int TM = 0>
