@@ -861,7 +861,6 @@ __global__ void fk_weights(const float* __restrict__ w1, long long rows, float* 
 // planes are consumed as stored), the overflow flag as any f16x3 store.  [lo, hi) = [0, T), or
 // with `tab` (segment pairs: the alt blocks seg_alt_blocks filled, n_ph blocks per segment) the
 // rows that alt block holds.  320 threads = 4 rows x 80 eight-channel pieces (16 B of hi + 16 B of lo).
-template <bool NT>
 __global__ __launch_bounds__(320) void fk_seq_h2(const float* __restrict__ x, int T, int s, const int* __restrict__ tab,
                                                  int n_ph, const int* __restrict__ gres, float* __restrict__ d1,
                                                  float* __restrict__ d2, float* __restrict__ dd, int* __restrict__ ovf) {
@@ -918,14 +917,7 @@ __global__ __launch_bounds__(320) void fk_seq_h2(const float* __restrict__ x, in
     for (int w = 0; w < 4; ++w) recv[w] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)send[w], 0x141, 0xf, 0xf, false);
     const u32x4 keep = __builtin_bit_cast(u32x4, low ? h : l);
     char* d = reinterpret_cast<char*>(dst) + blk * s * rb + row * rb + (c8 >> 3) * 256;
-    // NT: streaming stores (the 1.3 GB of sequences are read back by the next FC1 launch, far
-    // beyond L2 / MALL reuse distance)
-    auto st = [](char* p, const u32x4& v) {
-      if constexpr (NT)
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-      else
-        *reinterpret_cast<u32x4*>(p) = v;
-    };
+    auto st = [](char* p, const u32x4& v) { *reinterpret_cast<u32x4*>(p) = v; };
     if (low) {   // hi quarter j of group 2m' (own), hi quarter 3 - j of group 2m'+1 (mirror's)
       st(d + j * 16, keep);
       st(d + 128 + (3 - j) * 16, recv);
@@ -1563,7 +1555,6 @@ struct expecto_beluga {
   bool fc_wide = true;                // f16x3 FC split-K GEMMs on 336-column tiles (EXPECTO_FC_WIDE; same bits)
   int conv_tile = 0;                  // f16x3 conv M tile: 0 = auto (conv_tile_rows), 256 or 384
   bool conv_ea = true;                // f16x3 conv consumers' early next-stage reads (EXPECTO_CONV_EA)
-  bool fk_seq_nt = true;              // FC1 sequences written with streaming stores (EXPECTO_FK_SEQ_NT; same bits)
   int fc1_narrow = -1;                // grouped FC1 tile width: -1 auto (fc1_narrow), 0 336, 1 112 columns
   int conv_narrow = -1;               // conv5 / conv6 tile width: -1 auto (conv_narrow), 0 160, 1 64 columns
   bool narrow_scope = false;          // inside forward_chunk: auto narrow tiles allowed (nothing runs beside)
@@ -2398,10 +2389,7 @@ int fk_sequences(expecto_beluga* h, const float* x, long long blocks, int T, int
   LayerTimer lt(h, 7, st);   // the sequences are timed with the FC1 reduction (slot fc1_reduce)
   const long long nblk = blocks * 7;   // 7 workgroups of 4 residue walks per block
   EXPECTO_REQUIRE(nblk > 0 && nblk < (1LL << 31), "FC1 sequence grid");
-  if (h->fk_seq_nt)
-    fk_seq_h2<true><<<dim3((unsigned)nblk), dim3(320), 0, st>>>(x, T, s, tab, n_ph, gres, out[0], out[1], out[2], h->ovf);
-  else
-    fk_seq_h2<false><<<dim3((unsigned)nblk), dim3(320), 0, st>>>(x, T, s, tab, n_ph, gres, out[0], out[1], out[2], h->ovf);
+  fk_seq_h2<<<dim3((unsigned)nblk), dim3(320), 0, st>>>(x, T, s, tab, n_ph, gres, out[0], out[1], out[2], h->ovf);
   return check_launch("fk_seq_h2");
 }
 
@@ -3681,7 +3669,6 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
     h->fc1_narrow = v;
   }
   if (const char* e = getenv("EXPECTO_CONV_EA")) h->conv_ea = atoi(e) != 0;   // same bits either way
-  if (const char* e = getenv("EXPECTO_FK_SEQ_NT")) h->fk_seq_nt = atoi(e) != 0;   // same bits either way
   if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)
     const int v = atoi(e);
     EXPECTO_REQUIRE(v == 0 || v == 256 || v == 384, "EXPECTO_CONV_TILE must be 0 (auto), 256 or 384");
