@@ -1555,6 +1555,7 @@ struct expecto_beluga {
   bool fc_wide = true;                // f16x3 FC split-K GEMMs on 336-column tiles (EXPECTO_FC_WIDE; same bits)
   int conv_tile = 0;                  // f16x3 conv M tile: 0 = auto (conv_tile_rows), 256 or 384
   bool conv_ea = true;                // f16x3 conv consumers' early next-stage reads (EXPECTO_CONV_EA)
+  bool fc_skinny = true;              // FC1 / FC2 of <= 32 rows on 32 x 32 tiles (EXPECTO_FC_SKINNY; same bits)
   int fc1_narrow = -1;                // grouped FC1 tile width: -1 auto (fc1_narrow), 0 336, 1 112 columns
   int conv_narrow = -1;               // conv5 / conv6 tile width: -1 auto (conv_narrow), 0 160, 1 64 columns
   bool narrow_scope = false;          // inside forward_chunk: auto narrow tiles allowed (nothing runs beside)
@@ -2006,14 +2007,19 @@ int launch_gemm(const GemmArgs& a, int splits, hipStream_t st, int bm = 0) {
       // FC split-K partials: 336-column tiles on 8 MFMA waves when the caller tiled N that way
       // (n_tile_cols, set from fc_wide_tiles), else 160-column producer / consumer tiles (same
       // bits either way)
-      EXPECTO_REQUIRE(a.n_tile_cols == 0 || a.n_tile_cols == FCW_BN || a.n_tile_cols == 112,
-                      "FC tile width: 0 (160), 336 or 112 columns");
+      EXPECTO_REQUIRE(a.n_tile_cols == 0 || a.n_tile_cols == FCW_BN || a.n_tile_cols == 112 ||
+                          a.n_tile_cols == 16 * FCS_NB,
+                      "FC tile width: 0 (160), 336, 112 or 32 columns");
       EXPECTO_REQUIRE((long long)a.n_tiles * (a.n_tile_cols ? a.n_tile_cols : GBN) >= a.n_store,
                       "FC N tiles do not cover the stored columns");
       if (a.n_tile_cols == FCW_BN)
         beluga_fc_h3w<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
       else if (a.n_tile_cols == 112)
         beluga_fc_h3w_narrow<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
+      else if (a.n_tile_cols == 16 * FCS_NB) {   // <= 32 rows: 32 x 32 tiles, 9-stage ring (fc_skinny)
+        EXPECTO_REQUIRE(a.m_tiles == 1 && a.M <= 32 && !a.ks_mask, "skinny FC tiles: one tile of <= 32 rows");
+        beluga_fc_h3s<LAYER, EPI><<<dim3((unsigned)nblk), dim3(64 * 2 * FCS_NB), 0, st>>>(a);
+      }
       else
         beluga_fc_h3p<LAYER, EPI><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
     } else {   // FC layers: producer / consumer waves, both operands through an LDS ring (same bits)
@@ -2158,6 +2164,7 @@ float* h1_rows(expecto_beluga* h, long long rows) { return h->h1 + rows * kHidLd
 bool fc_wide_tiles(const expecto_beluga* h) { return h->fc_wide && g_precision == EXPECTO_PRECISION_F16X3; }
 
 bool fc1_narrow(const expecto_beluga* h, long long mtt);
+bool fc_skinny(const expecto_beluga* h, long long rows);
 
 // FC1 (split-K slabs into `part`) + fc1_reduce (bias, ReLU, activation planes) into h1.
 int run_fc1(expecto_beluga* h, const float* act, const long long* a_rows, int nb, float* h1, hipStream_t st,
@@ -2204,7 +2211,10 @@ int run_fc1(expecto_beluga* h, const float* act, const long long* a_rows, int nb
       a.m_fastest = 0;
       a.linear_order = 0;
       a.n_tile_cols = FCW_BN;
-      if (!ks_mask && fc1_narrow(h, m_tiles * splits)) {   // small per-window batches: 112 columns
+      if (!ks_mask && fc_skinny(h, nb)) {   // <= 32 rows: 48 columns, deep ring
+        a.n_tile_cols = 16 * FCS_NB;
+        a.n_tiles = kHidLd / a.n_tile_cols;
+      } else if (!ks_mask && fc1_narrow(h, m_tiles * splits)) {   // small per-window batches: 112 columns
         a.n_tile_cols = 112;
         a.n_tiles = kHidLd / 112;
       }
@@ -2259,7 +2269,10 @@ int run_fc2(expecto_beluga* h, const float* h1, int nb, float* y, hipStream_t st
     if (wide) {
       a.m_fastest = 0;
       a.n_tile_cols = FCW_BN;
-      if (fc1_narrow(h, m_tiles * h->fc2_splits)) {   // small per-window batches: 112 columns
+      if (fc_skinny(h, nb)) {   // <= 32 rows: 48 columns, deep ring
+        a.n_tile_cols = 16 * FCS_NB;
+        a.n_tiles = (kNFeat + a.n_tile_cols - 1) / a.n_tile_cols;
+      } else if (fc1_narrow(h, m_tiles * h->fc2_splits)) {   // small per-window batches: 112 columns
         a.n_tile_cols = 112;
         a.n_tiles = (kNFeat + 111) / 112;
       }
@@ -2415,7 +2428,7 @@ int fk_reduce(expecto_beluga* h, const float* part, const int* prow, int n, floa
 // fc_h3w_tile NB 7, same bits) fit in one round of the chip's workgroups -- the per-window forwards
 // of small batches (the reference's batch 32 / 200 calls: 9 M tiles, 54 workgroups on 256 CUs;
 // FC1 525 -> ~185 us at batch 32).  EXPECTO_FC1_NARROW=0 / 1 forces the choice (same bits either way).
-constexpr int kFcNarrowNb = 7;   // beluga_fc_h3k_narrow
+constexpr int kFcNarrowNb = 7;   // beluga_fc_h3w_narrow
 static_assert(kHidLd % (16 * kFcNarrowNb) == 0 && kHidLd % FCW_BN == 0, "FC1 N tiles");
 bool fc1_narrow(const expecto_beluga* h, long long mtt) {
   if (h->fc1_narrow >= 0) return h->fc1_narrow != 0;
@@ -2424,6 +2437,16 @@ bool fc1_narrow(const expecto_beluga* h, long long mtt) {
   // wide: no gain measured)
   const long long cus = h->cus > 0 ? h->cus : 256;
   return mtt * (kHidLd / (16 * kFcNarrowNb)) <= cus;
+}
+
+// Batches of <= 32 rows (the reference's per-window batch): FC1 / FC2 on beluga_fc_h3s (32 x 32 tiles,
+// a 9-stage ring; the same bits) where the narrow tiles would run: FC1 at batch 32 160 -> 125 us
+// (32 x 48 tiles on a 7-stage ring: 145 us).  EXPECTO_FC_SKINNY=0 keeps the narrow tiles.
+static_assert(kHidLd % (16 * FCS_NB) == 0 &&
+                  (kNFeat + 16 * FCS_NB - 1) / (16 * FCS_NB) * 16 * FCS_NB <= (kNFeat + GBN - 1) / GBN * GBN,
+              "skinny FC tiles");
+bool fc_skinny(const expecto_beluga* h, long long rows) {
+  return h->fc_skinny && rows <= 32 && (h->fc1_narrow >= 0 ? h->fc1_narrow != 0 : h->narrow_scope);
 }
 
 // One grouped launch of the Karatsuba FC1 over n windows: per product g with cnt[g] groups, its
@@ -3669,6 +3692,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
     h->fc1_narrow = v;
   }
   if (const char* e = getenv("EXPECTO_CONV_EA")) h->conv_ea = atoi(e) != 0;   // same bits either way
+  if (const char* e = getenv("EXPECTO_FC_SKINNY")) h->fc_skinny = atoi(e) != 0;   // same bits either way
   if (const char* e = getenv("EXPECTO_CONV_TILE")) {    // tuning knob: f16x3 conv M tile (same bits)
     const int v = atoi(e);
     EXPECTO_REQUIRE(v == 0 || v == 256 || v == 384, "EXPECTO_CONV_TILE must be 0 (auto), 256 or 384");

@@ -1317,6 +1317,127 @@ __global__ __launch_bounds__(512, 1) void beluga_fc_h3w_narrow(GemmArgs p) {
   gemm_fc_h3w_body<LAYER, EPI, 0, 7, 3>(p, smem);
 }
 
+// The same split-K GEMM for batches of <= 32 rows (the reference's per-window batch of 32): a
+// weight stream with almost no MFMA work per byte, so the time is how many bytes each CU keeps in
+// flight.  The 256-row tiles above stage 32 KB of A planes per K block for 32 live rows and run a
+// 3-stage ring on 144 workgroups (FC1: 160 us, 3.4 TB/s of weights); here a tile is 32 rows x 16 NB
+// columns, a stage (A 32 rows + B 16 NB columns, two planes each) 4 + 2 NB KB and the ring NS
+// stages deep: NB 2, NS 9 = FC1 in 504 workgroups, two per CU, 128 KB of pieces in flight per CU
+// (125 us; NB 3, NS 7: 336 workgroups, 145 us).  The wait for a stage is the memory latency over
+// the ring depth: the weights arrive at ~35 GB/s per CU either way.  2 NB waves, one 16 x 16 output block each (rows 16 (w / NB), columns 16 (w % NB)):
+// the same pieces, swizzle, fragments, products and k order per output as fc_h3w_tile -- the same
+// bits.
+template <int NB>
+struct FcsGeo {
+  static constexpr int APLANE = 32 * 64;                 // 2 KB
+  static constexpr int BPLANE = NB * 1024;
+  static constexpr int STAGE = 2 * APLANE + 2 * BPLANE;
+  static constexpr int WAVES = 2 * NB;
+  static constexpr int PIECES = 4 + 2 * NB;              // 4 A, then 2 NB B pieces per stage
+};
+constexpr int FCS_NB = 2;   // 32 columns: FC1 63 N tiles x 8 slabs = 504 workgroups, two per CU
+constexpr int FCS_NS = 9;   // ring stages (2 x 9 x 8 KB of LDS per CU)
+template <int N>
+__device__ __forceinline__ void wait_vmn() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int LAYER, int EPI, int NB = FCS_NB, int NS = FCS_NS>
+__global__ __launch_bounds__(64 * 2 * NB, 2) void beluga_fc_h3s(GemmArgs p) {
+  static_assert(EPI == EPI_PARTIAL, "split-K partial slabs only");
+  using G = FcsGeo<NB>;
+  static_assert(2 * NS * G::STAGE <= 160 * 1024, "two workgroups per CU");
+  __shared__ __attribute__((aligned(1024))) char smem[NS * G::STAGE];
+  constexpr int ROW_KB = 128;
+  constexpr int LOOK = NS - 1;
+  // N tiles fastest: the tiles of a slab share its A rows
+  const int nt = (int)(blockIdx.x % (unsigned)p.n_tiles), ks = (int)(blockIdx.x / (unsigned)p.n_tiles);
+  const int n0 = nt * 16 * NB;
+  const int kb_total = (int)(p.ldb / GBK), nk = (int)(p.kper / GBK), kb0a = ks * nk;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int mb = wave / NB, nb = wave % NB;
+  auto swz = [](int r) { return (-(r >> 2)) & 3; };
+  // wave w issues pieces w and w + WAVES (if any): piece k < 4 is A piece k (plane k & 1, rows
+  // 16 (k >> 1) ..), piece k >= 4 B piece Q = k - 4 (plane Q / NB, columns 16 (Q % NB) ..)
+  const char* gsrc[2] = {nullptr, nullptr};   // A pieces: global source
+  unsigned boff[2] = {0, 0}, dst[2] = {0, 0};
+  bool isa[2] = {false, false};
+  constexpr int NPW1 = G::PIECES > G::WAVES ? 1 : 0;   // waves with a second piece: w < PIECES - WAVES
+  const int npw = 1 + (wave < G::PIECES - G::WAVES ? 1 : 0);
+#pragma unroll
+  for (int i = 0; i < 1 + NPW1; ++i) {
+    const int k = wave + i * G::WAVES;
+    if (k >= G::PIECES) break;
+    if (k < 4) {
+      const int g = k >> 1, pl = k & 1, r = 16 * g + (lane >> 2);
+      const long long m = min((long long)r, p.M - 1);
+      const long long kb0 = (p.a_rows ? p.a_rows[m] / GBK : m * (p.lda / GBK)) + kb0a;
+      gsrc[i] = (const char*)p.A + kb0 * ROW_KB + pl * 64 + 16 * ((lane & 3) ^ swz(r));
+      dst[i] = (unsigned)(pl * G::APLANE + g * 1024);
+      isa[i] = true;
+    } else {
+      const int Q = k - 4, pl = Q / NB, r = 16 * (Q % NB) + (lane >> 2);
+      boff[i] = (unsigned)((long long)r * kb_total * ROW_KB + pl * 64 + 16 * ((lane & 3) ^ swz(r)));
+      dst[i] = (unsigned)(2 * G::APLANE + Q * 1024);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((const char*)p.Bp + ((long long)n0 * kb_total + kb0a) * ROW_KB), (short)0, 0x7fffffff, 0x00020000);
+  auto issue = [&](int s, char* base) {   // this wave's pieces of stage s (wave-uniform branches)
+#pragma unroll
+    for (int i = 0; i < 1 + NPW1; ++i) {
+      if (i == 1 && npw == 1) break;
+      if (isa[i])
+        glds16(gsrc[i] + (long long)s * ROW_KB, base + dst[i]);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void*)(base + dst[i]), 16, boff[i], (unsigned)(s * ROW_KB),
+                                                 0, 0);
+    }
+  };
+  // at a stage end a wave waits until only its pieces of the LOOK - 1 later stages are in flight
+  auto stage_end_wait = [&]() {
+    if (npw == 2)
+      wait_vmn<2 * (LOOK - 1)>();
+    else
+      wait_vmn<LOOK - 1>();
+  };
+#pragma unroll
+  for (int st = 0; st < LOOK; ++st) issue(min(st, nk - 1), smem + st * G::STAGE);
+  stage_end_wait();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  const bool live = 16 * mb < p.M;   // wave-uniform
+  const int fr = lane & 15, fq = lane >> 4;
+  const int arow = (mb * 16 + fr) * 64 + 16 * (fq ^ swz(fr));
+  const int brow = 2 * G::APLANE + nb * 1024 + fr * 64 + 16 * (fq ^ swz(fr));
+  floatx4v acc = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < nk; ++s) {
+    const char* base = smem + (s % NS) * G::STAGE;
+    issue(min(s + LOOK, nk - 1), smem + ((s + LOOK) % NS) * G::STAGE);   // (the last re-fetch the last block)
+    if (live) {
+      bf16x8 a[3], b[3];
+      a[0] = *(const bf16x8*)(base + arow);
+      a[1] = *(const bf16x8*)(base + arow + G::APLANE);
+      b[0] = *(const bf16x8*)(base + brow);
+      b[1] = *(const bf16x8*)(base + brow + G::BPLANE);
+      acc = planes_mfma<2>(acc, a, b);
+    }
+    stage_end_wait();
+    __builtin_amdgcn_s_barrier();   // everyone's pieces of stage s + 1 landed, stage s fully read
+    asm volatile("" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the re-fetches, before the workgroup's LDS is released
+  if (!live) return;
+  const int n = n0 + nb * 16 + fr;
+  if (n >= p.n_store) return;
+  float* cp = p.C + (long long)ks * p.split_stride + n;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const long long m = mb * 16 + 4 * fq + j;
+    if (m < p.M) cp[m * p.ldc] = acc[j];
+  }
+}
+
 // ---- grouped wide FC GEMM: several split-K partial GEMMs in one launch ----------------------
 // FC1's block Karatsuba (beluga.hip, "FC1 as a block-Karatsuba convolution") runs up to 9
 // products x 2 K slabs + the tail per window group as separate GEMMs with their own A rows,

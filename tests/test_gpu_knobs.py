@@ -68,7 +68,8 @@ def test_conv_early_reads_same_bits_with_fused_conv1(monkeypatch):
 def test_tile_widths_small_batches(monkeypatch):
     """Per-window batches take narrower N tiles where they need fewer rounds of workgroups: the
     grouped FC1, the direct FC1 and FC2 112 instead of 336 columns (beluga.hip fc1_narrow; part-filled
-    M tiles' empty waves skip their MFMAs), conv3 / conv4 128 and conv5 / conv6 64 instead of 160
+    M tiles' empty waves skip their MFMAs), the direct FC1 and FC2 of <= 32 rows 32 x 48 tiles on a
+    7-stage ring (fc_skinny, beluga_fc_h3s), conv3 / conv4 128 and conv5 / conv6 64 instead of 160
     (conv_narrow).  Batch 5 / 32 / 200 / 512 in FC1 roles 0, 3 and the direct FC1: the same bits as
     the wide tiles (EXPECTO_FC1_NARROW=0, EXPECTO_CONV_NARROW=0)."""
     from expecto_amd import beluga
