@@ -112,12 +112,14 @@ def conv2_table_roofline(layers, n):
 
 def kernel_name(layer: str, precision: str, segments: bool = True) -> str:
     """rocprofv3 kernel name of a layer's launch.  On the segment path (the headline, configs[2]
-    and [4]) conv4 runs unpooled (its pool2 is a separate per-phase kernel)."""
+    and [4]) conv4 writes the pool2 phase blocks from its epilogue (f16x3; else it runs unpooled and
+    its pool2 is a separate per-phase kernel)."""
     if layer not in GEMM_LAYER_EPI:
         return {"conv1": "beluga_conv1", "fc1_reduce": "fc1_reduce"}[layer]
     l, e = GEMM_LAYER_EPI[layer]
     if segments and layer == "conv4":
-        e = 0
+        # unpooled, its pool2 a separate pass; f16x3 with the pool2 phases in the epilogue: EPI 4
+        e = 4 if precision == "f16x3" and os.environ.get("EXPECTO_POOL_FUSED", "1") != "0" else 0
     if layer == "conv2" and conv2_table_on(precision):
         return "conv2_kmer_pool"                           # conv1 + conv2 + pool1 gathered from the k-mer table
     if precision == "bf16x6":

@@ -725,8 +725,12 @@ __global__ __launch_bounds__(256) void seg_delta_assemble(const float* __restric
 
 // pool2 of the alt run for each phase: pooled rows [r4p, r4p+6) of block (seg, phase) from the
 // ref's unpooled conv4 rows and the alt conv4 run (exact max, as pool4_phases)
+// (edge != 0: conv4 holds only the ref rows this kernel reads, kSegEdge per segment from the first
+// one, the fused conv4 + pool2 epilogue's layout, gemm_kernel.h epilogue_pool_ph02)
+constexpr int kSegEdge = 32;
+__device__ __forceinline__ int seg_edge_lo(const int* t) { return min(4 * t[5], 2 + 4 * t[6]); }
 __global__ void seg_delta_pool(const float* __restrict__ conv4, int t4, const float* __restrict__ d4, int n_ph,
-                               int4 ph, const int* __restrict__ tab, int fmt, float* __restrict__ out) {
+                               int4 ph, const int* __restrict__ tab, int fmt, float* __restrict__ out, int edge = 0) {
   const int c = threadIdx.x;
   if (c >= 480) return;
   const int gi = blockIdx.x, m = blockIdx.y;
@@ -734,17 +738,61 @@ __global__ void seg_delta_pool(const float* __restrict__ conv4, int t4, const fl
   const int p = i == 0 ? ph.x : i == 1 ? ph.y : i == 2 ? ph.z : ph.w;
   const int r4 = tab[seg * kSegTab + 4];
   const int row0 = p + 4 * (tab[seg * kSegTab + 5 + i] + gi);
+  const int elo = edge ? seg_edge_lo(tab + seg * kSegTab) : 0;
   float mx = 0.f;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int row = row0 + j;
     const bool alt = row >= r4 && row < r4 + kW4u;
     const float* b = alt ? d4 : conv4;
-    const long long r = alt ? (long long)seg * kW4u + row - r4 : (long long)seg * t4 + row;
+    const long long r = alt    ? (long long)seg * kW4u + row - r4
+                        : edge ? (long long)seg * kSegEdge + row - elo
+                               : (long long)seg * t4 + row;
     const float v = load_act_rt(fmt, b, r, 480, c);
     mx = j == 0 ? v : fmaxf(mx, v);
   }
   store_act_rt(fmt, out, (long long)m * kDW[4] + gi, 480, c, mx);
+}
+
+// The phase-2 pooled row whose 4 conv4 rows straddle two 256-row tiles of the fused conv4 + pool2
+// launch (epilogue_pool_ph02 leaves it): from the two tiles' edge rows (seam: 4 rows per tile, its
+// rows 0, 1, 254, 255, plain split), pooled as pool4_phases_h2m does (decode, fmaxf in row order,
+// canonical split).  One workgroup per tile boundary b = 256 k, rows b - 2 .. b + 1.
+__global__ void pool2_tile_seams(const float* __restrict__ seam, long long M, int s_in, int t4, int s5,
+                                 float* __restrict__ out) {
+  const int c8 = threadIdx.x;   // 60 eight-channel pieces
+  if (c8 >= 60) return;
+  const long long k = blockIdx.x + 1, b = 256 * k;
+  if (b + 1 >= M) return;
+  const long long w = (b - 2) / s_in;   // segment blocks of s_in rows (4-aligned), t4 of them valid
+  const int t = (int)(b - 2 - w * s_in), g = (t - 2) >> 2;
+  if (t + 3 >= t4) return;   // the group would leave its segment's valid rows: no such pooled row
+  constexpr long long rb = 480 * 4;
+  const int cofs = (c8 >> 2) * 128 + (c8 & 3) * 16;
+  const char* sb = reinterpret_cast<const char*>(seam);
+  const char* src[4] = {sb + ((k - 1) * 4 + 2) * rb, sb + ((k - 1) * 4 + 3) * rb, sb + (k * 4 + 0) * rb,
+                        sb + (k * 4 + 1) * rb};
+  halfx8 oh, ol;
+  float m[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const halfx8 hv = *reinterpret_cast<const halfx8*>(src[j] + cofs), lv = *reinterpret_cast<const halfx8*>(src[j] + cofs + 64);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = (float)hv[e] + (float)lv[e];
+      m[e] = j == 0 ? v : fmaxf(m[e], v);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    _Float16 h, l;
+    split_h2(m[e], h, l);
+    oh[e] = h;
+    ol[e] = l;
+  }
+  char* dst = reinterpret_cast<char*>(out) + ((2 * w + 1) * s5 + g) * rb + cofs;
+  *reinterpret_cast<halfx8*>(dst) = oh;
+  *reinterpret_cast<halfx8*>(dst + 64) = ol;
 }
 
 // alt conv6 phase blocks: the ref block (t6 rows) with rows [r6, r6+20) from the alt run.  Only
@@ -1562,6 +1610,10 @@ struct expecto_beluga {
   int seg_chunk_windows = 0;          // segment path: windows per chunk cap (0 = none; tuning knob)
   int cus = 0;                        // compute units of the device (workgroups per round)
   bool pool_one_pass = true;          // segment path: pool2 of all phases in one pass (same bits)
+  bool pool_fused = true;             // segment path, phases {0, 2}: pool2 in conv4's epilogue (EXPECTO_POOL_FUSED; same bits)
+  float* seam = nullptr;              //   its tile-seam rows (4 per 256-row tile) and seg_delta_pool's ref rows
+  float* edge = nullptr;
+  size_t seam_cap = 0, edge_cap = 0;
   bool fuse_conv1 = true;             // f16x3 codes input: conv1 inside the conv2 launch (EXPECTO_FUSE_CONV1; same bits)
   bool kmer_on = true;                // f16x3 codes input: conv1 + conv2 + pool1 from the k-mer table (EXPECTO_CONV2_TABLE)
   float* kmer = nullptr;              //   the table (shared by handles with the same conv1 / conv2 weights)
@@ -2148,6 +2200,81 @@ int run_conv(expecto_beluga* h, int l, const float* src, float* dst, long long g
   }
 }
 
+// Segment path, f16x3, pool2 phases {0, 2} (the 200-bp shift sweeps): conv4 with its pool2 in the
+// epilogue (gemm_kernel.h epilogue_pool_ph02) straight into the phase blocks at `dst` (n_ph = 2, s5
+// pooled rows each), then pool2_tile_seams for the phase-2 rows across tile boundaries.  The same
+// bits as conv4 unpooled + pool4_phases_h2m; the unpooled rows themselves are written only where
+// something reads them: the tile seams (h->seam) and, for segment pairs (tab), seg_delta_pool's ref
+// rows (h->edge, kSegEdge per segment).  EXPECTO_POOL_FUSED=0 keeps the separate pool pass.
+bool conv4_pool_fused(const expecto_beluga* h, long long M, int n_ph, const int* ph) {
+  if (!h->pool_fused || act_fmt() != 2 || !h->pool_one_pass || n_ph != 2 || ph[0] != 0 || ph[1] != 2) return false;
+  const int bm = conv_tile_rows(h, 2, false, M, npad_of(480) / GBN);
+  return bm == 256 && !conv_narrow(h, 2, M, bm, npad_of(480) / GBN);
+}
+int run_conv4_pool_fused(expecto_beluga* h, const float* src, float* dst, long long groups, int s_in, int t4, int s5,
+                         const int* tab, hipStream_t st) {
+  const ConvGeo& g = kConv[2];
+  GemmArgs a{};
+  a.A = src;
+  a.lda = g.cin;
+  a.M = groups * s_in;
+  a.B = h->wt[2];
+  a.Bp = h->wh[2];
+  a.col_scale = h->cs[2];
+  a.out_scale = exp2i(h->sx[3]);
+  a.ovf = h->ovf;
+  a.ldb = 8LL * g.cin;
+  a.kper = 8 * g.cin;
+  a.taps = 8;
+  a.n_tiles = npad_of(g.cout) / GBN;
+  a.m_tiles = (a.M + 255) / 256;
+  a.bias = h->bt[2];
+  a.C = dst;
+  a.ldc = g.cout;
+  a.n_store = g.cout;
+  a.s_in = s_in;
+  a.t_valid = t4;
+  a.s_out = s5;
+  EXPECTO_REQUIRE(g_precision == EXPECTO_PRECISION_F16X3 && s_in % 4 == 0 && t4 <= s_in && a.n_tiles == 3,
+                  "fused conv4 + pool2: f16x3 segment blocks at a 4-aligned row stride");
+  const size_t seam_rows = (size_t)a.m_tiles * 4, edge_rows = tab ? (size_t)groups * kSegEdge : 0;
+  auto grow = [&](float*& b, size_t& cap, size_t rows) -> int {   // (grown once per handle and size)
+    if (rows <= cap) return EXPECTO_OK;
+    if (b) EXPECTO_HIP_CHECK(hipFree(b));
+    b = nullptr;
+    h->bytes -= cap * 480 * 4;
+    cap = 0;
+    EXPECTO_HIP_CHECK(hipMalloc(&b, rows * 480 * 4));
+    EXPECTO_HIP_CHECK(hipMemset(b, 0, rows * 480 * 4));
+    cap = rows;
+    h->bytes += rows * 480 * 4;
+    return EXPECTO_OK;
+  };
+  int rc;
+  if ((rc = grow(h->seam, h->seam_cap, seam_rows)) || (rc = grow(h->edge, h->edge_cap, edge_rows))) return rc;
+  a.c_seam = h->seam;
+  a.c_edge = h->edge;
+  a.unp_tab = tab;
+  a.unp_ld = kSegTab;
+  a.unp_dw = kDW[4];
+  const long long nblk = a.m_tiles * a.n_tiles;
+  EXPECTO_REQUIRE(nblk > 0 && nblk < (1LL << 31), "gemm grid out of range");
+  {
+    LayerTimer lt(h, 3, st);
+    if (h->profiling) h->macs[h->timer_base + 3] += (double)a.M * g.cout * a.kper;
+    LaunchTimer lrec(h, 3, a.M, (double)a.M * g.cout * a.kper, st);
+    if (g_conv_ea)
+      beluga_conv_h3p<4, EPI_POOL_PH02, 256 | 64, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
+    else
+      beluga_conv_h3p<4, EPI_POOL_PH02, 256, 4><<<dim3((unsigned)nblk), dim3(512), 0, st>>>(a);
+    if ((rc = check_launch("beluga_conv_h3p pool2"))) return rc;
+  }
+  LayerTimer lt(h, 3, st);   // pool2 is timed with conv4
+  if (a.m_tiles > 1)
+    pool2_tile_seams<<<dim3((unsigned)(a.m_tiles - 1)), dim3(64), 0, st>>>(h->seam, a.M, s_in, t4, s5, dst);
+  return check_launch("pool2_tile_seams");
+}
+
 // FC1 (split-K) + reduce + FC2/sigmoid for nb windows whose conv6 rows are at act
 // (+ a_rows[m] when given, else m*67840).
 // part_rows: row count of the split-K partial slabs (default nb): an alt FC1 that recomputes
@@ -2727,7 +2854,7 @@ SegGeo seg_geo(int L, int n_ph) {
   g.S5 = g.T4 / 4;        // rows of the phase-0 pool2 block (the longest)
   g.T5 = g.S5 - 7;
   g.T6 = g.T5 - 7;
-  const size_t p_conv1 = (size_t)g.S1 * 320, p_conv3 = (size_t)g.T3 * 480, p_pool2 = (size_t)n_ph * g.S5 * 480,
+  const size_t p_conv1 = (size_t)g.S1 * 320, p_conv3 = (size_t)((g.T3 + 3) & ~3) * 480, p_pool2 = (size_t)n_ph * g.S5 * 480,
                p_conv6 = (size_t)n_ph * g.T6 * 640;
   const size_t q_pool1 = (size_t)g.P1 * 320, q_conv4 = (size_t)g.T4 * 480, q_conv5 = (size_t)n_ph * g.T5 * 640;
   g.p_rows_floats = std::max(std::max(p_conv1, p_conv3), std::max(p_pool2, p_conv6));
@@ -3017,12 +3144,32 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
         return rc;
       }
       if (pr && (rc = alt_asm(1, h->Q, g.P1, h->D1, kDW[2], 1, 3, 1, 2, kDA[3], h->pev[3], h->pev[4]))) return rc;
-      if ((rc = run_conv(h, 1, h->Q, h->P, ns, g.P1, g.T3, g.T3, false, st))) return rc;
+      // conv3 rows at a 4-aligned stride per segment (T3p >= T3), so conv4's rows of every segment
+      // start 4-aligned in its M index space: pool2 groups are then lane-local (epilogue_pool_ph02)
+      const int T3p = (g.T3 + 3) & ~3;
+      if ((rc = run_conv(h, 1, h->Q, h->P, ns, g.P1, g.T3, T3p, false, st))) return rc;
       if (pr && ((rc = st_wait(h->pev[4])) || (rc = alt_gemm(1, 1, kDA[3], kDW[3], false, h->D0)))) return rc;
-      if (pr && (rc = alt_asm(2, h->P, g.T3, h->D0, kDW[3], 1, 4, 1, 3, kA4u, h->pev[5], h->pev[6]))) return rc;
-      if ((rc = run_conv(h, 2, h->P, h->Q, ns, g.T3, g.T4, g.T4, false, st))) return rc;
+      if (pr && (rc = alt_asm(2, h->P, T3p, h->D0, kDW[3], 1, 4, 1, 3, kA4u, h->pev[5], h->pev[6]))) return rc;
+      // pool2 fused into conv4 (P -> phase blocks in Q, then P and Q trade roles for the rest of
+      // the chunk: conv5 Q -> P, conv6 P -> Q, ... -- both hold a chunk's conv5 / conv6 rows, see
+      // seg_geo), else conv4 unpooled (P -> Q) and a pool pass (Q -> P)
+      const bool pfused = conv4_pool_fused(h, (long long)ns * T3p, n_ph, ph);
+      struct PQSwap {
+        expecto_beluga* h;
+        bool on;
+        ~PQSwap() {
+          if (on) std::swap(h->P, h->Q);
+        }
+      } pq{h, false};
+      if (pfused) {
+        if ((rc = run_conv4_pool_fused(h, h->P, h->Q, ns, T3p, g.T4, g.S5, pr ? h->seg_tab : nullptr, st))) return rc;
+        std::swap(h->P, h->Q);
+        pq.on = true;
+      } else if ((rc = run_conv(h, 2, h->P, h->Q, ns, T3p, g.T4, g.T4, false, st))) {
+        return rc;
+      }
       if (pr && ((rc = st_wait(h->pev[6])) || (rc = alt_gemm(2, 1, kA4u, kW4u, false, h->D1)))) return rc;
-      {  // pool2 phases (Q -> P)
+      if (!pfused) {  // pool2 phases (Q -> P)
         LayerTimer lt(h, 3, st);
         if (act_fmt() == 2 && h->pool_one_pass) {   // all phases in one pass over the conv4 rows
           dim3 grid((g.S5 + 3) / 4, ns);
@@ -3041,8 +3188,9 @@ int forward_segments(expecto_beluga* h, const uint8_t* codes, int n_seg, int L, 
           EXPECTO_HIP_CHECK(hipEventRecord(h->pev[7], st));
           EXPECTO_HIP_CHECK(hipStreamWaitEvent(sa, h->pev[7], 0));
         }
-        seg_delta_pool<<<dim3(kDW[4], (unsigned)nb), dim3(480), 0, sa>>>(h->Q, g.T4, h->D1, n_ph, ph4, h->seg_tab,
-                                                                         act_fmt(), h->D0);
+        seg_delta_pool<<<dim3(kDW[4], (unsigned)nb), dim3(480), 0, sa>>>(pfused ? h->edge : h->Q, g.T4, h->D1, n_ph,
+                                                                         ph4, h->seg_tab, act_fmt(), h->D0,
+                                                                         pfused ? 1 : 0);
         if ((rc = check_launch("seg_delta_pool"))) return rc;
         if (sa != st) EXPECTO_HIP_CHECK(hipEventRecord(h->pev[8], sa));
         if ((rc = alt_asm(3, h->P, g.S5, h->D0, kDW[4], n_ph, 9, 1, 5, kDA[5], h->pev[9], h->pev[10]))) return rc;
@@ -3669,6 +3817,7 @@ int expecto_beluga_create(int device, const float* const* params, int max_batch,
   if (const char* e = getenv("EXPECTO_FC_WIDE")) h->fc_wide = atoi(e) != 0;                   // same bits
   if (const char* e = getenv("EXPECTO_OVERLAP")) h->overlap = atoi(e) != 0;   // same bits either way
   if (const char* e = getenv("EXPECTO_POOL_ONE_PASS")) h->pool_one_pass = atoi(e) != 0;   // same bits either way
+  if (const char* e = getenv("EXPECTO_POOL_FUSED")) h->pool_fused = atoi(e) != 0;         // same bits either way
   if (const char* e = getenv("EXPECTO_FUSE_CONV1")) h->fuse_conv1 = atoi(e) != 0;         // same bits either way
   if (const char* e = getenv("EXPECTO_CONV2_TABLE")) h->kmer_on = atoi(e) != 0;   // conv2 on the MFMAs (parity, not bits)
   if (const char* e = getenv("EXPECTO_KMER_QUAD")) h->kmer_quad = atoi(e) != 0;    // pair tables only (parity, not bits)
@@ -3743,6 +3892,8 @@ void expecto_beluga_destroy(expecto_beluga_t h) {
   for (float* p : h->fk_aseq)
     if (p) (void)hipFree(p);
   if (h->fk_gres) (void)hipFree(h->fk_gres);
+  if (h->seam) (void)hipFree(h->seam);
+  if (h->edge) (void)hipFree(h->edge);
   for (void* p : h->allocs) (void)hipFree(p);
   for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->pev)

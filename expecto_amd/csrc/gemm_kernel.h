@@ -19,7 +19,7 @@ constexpr int GBN = 160;
 constexpr int GBK = 32;               // K block (one conv (chunk, tap) pair)
 constexpr int GTN = GBN / 32;
 
-enum { EPI_RELU = 0, EPI_RELU_POOL4 = 1, EPI_SIGMOID = 2, EPI_PARTIAL = 3 };
+enum { EPI_RELU = 0, EPI_RELU_POOL4 = 1, EPI_SIGMOID = 2, EPI_PARTIAL = 3, EPI_POOL_PH02 = 4 };
 
 struct GemmArgs {
   const float* A;
@@ -67,6 +67,15 @@ struct GemmArgs {
   const float* c1_b;        // conv1 bias
   float c1_osc;             // conv2 input scale 2^sx[0]
   unsigned long long* stamps;   // diagnostic builds only (TM & H3P_STAMP, tools/ck_bench): per-wave cycle sums
+  // EPI_POOL_PH02 (segment path, conv4 + pool2 phases 0 and 2 in the epilogue): C = the phase blocks
+  // (segment w, phase i at rows (2 w + i) * s_out).  Unpooled rows (plain split) only where others
+  // read them: c_seam gets each 256-row tile's rows 0, 1, 254, 255 (4 rows per tile, pool2_tile_seams),
+  // and with unp_tab c_edge the ref rows seg_delta_pool pools (phase 0 from pooled row tab[5], phase
+  // 2 from tab[6], unp_dw pooled rows each): 32 rows per segment from the first of them
+  float* c_seam;
+  float* c_edge;
+  const int* unp_tab;
+  int unp_ld, unp_dw;
 };
 constexpr int H3P_FUSE_CONV1 = 16384;
 // Diagnostic build of beluga_conv_h3p (tools/ck_bench "stamp"; the library never sets it): s_memtime
@@ -1716,6 +1725,148 @@ __device__ __forceinline__ void epilogue_pool_h2_lds(const GemmArgs& p, const fl
   if (!(vmax < 65504.f)) *p.ovf = 1;   // overflow: the call is recomputed (bf16x6)
 }
 
+// Pool2 of conv4's rows in the epilogue for the segment path's two pool phases 0 and 2 (the 200-bp
+// shift sweeps): the same values as EPI_RELU's plain-split rows pooled by pool4_phases_h2m --
+// x = relu(acc * cs + b) per row; the phase-p row of group rows t..t+3 (t = p mod 4) is the
+// canonical split of max(x), and split_h2(max x) = canon(r(max x)) = canon(max r(x)) with r(x) =
+// hi + lo of the plain split (r is monotone and r(r(x)) = r(x)).  A lane holds rows 4 fq .. 4 fq + 3
+// of each 16-row block, i.e. a phase-0 group; a phase-2 group takes this lane's rows 2, 3 and the
+// next lane group's rows 0, 1 (ds_bpermute by 16 lanes; across a 16-row block the next block's
+// register, across waves an LDS exchange).  The group across the tile's end is left to
+// pool2_tile_seams, which pools it from the two tiles' edge rows written unpooled (c_unp).
+// Pooled rows are staged per wave in LDS (rows 0..15 phase 0, 16..31 phase 2) and stored as 16-B
+// chunks like epilogue_pool_h2_lds.
+template <bool BATCH>
+__device__ __forceinline__ void epilogue_pool_ph02(const GemmArgs& p, floatx4v (&acc)[4][10], long long mw, int n0,
+                                                   int lane, int wave, char* smem) {
+  constexpr int NB = 10, CPR = 40;
+  const int fr = lane & 15, fq = lane >> 4;
+  float csov[NB], bov[NB];
+  epi_factors<BATCH, NB>(p, n0, fr, csov, bov);
+  float vmax = 0.f;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float x = fmaxf(fmaf(acc[mb][nb][j], csov[nb], bov[nb]), 0.f);
+        vmax = fmaxf(vmax, x);
+        acc[mb][nb][j] = x;
+      }
+  const long long w0 = mw / p.s_in;
+  const int t0 = (int)(mw - w0 * p.s_in);
+  const long long ldb = p.ldc >> 5;
+  // unpooled rows others read (plain split, as EPI_RELU stores them)
+  auto put_row = [&](char* base, long long drow, const floatx4v (&a)[NB], int j) {
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      if (n0 + nb * 16 + fr >= p.n_store) continue;
+      _Float16 hi, lo;
+      split_h2p(a[nb][j], hi, lo);
+      char* d = base + drow * ldb * 128 + ((n0 >> 5) + (nb >> 1)) * 128 + ((nb & 1) * 16 + fr) * 2;
+      *(_Float16*)d = hi;
+      *(_Float16*)(d + 64) = lo;
+    }
+  };
+  // the tile's edge rows: wave 0's rows 0, 1 and wave 3's rows 62, 63 (pool2_tile_seams)
+  const long long mt = (mw - wave * 64) >> 8;
+  if (wave == 0 && fq == 0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (mw + j < p.M) put_row((char*)p.c_seam, mt * 4 + j, acc[0], j);
+  } else if (wave == 3 && fq == 3) {
+#pragma unroll
+    for (int j = 2; j < 4; ++j)
+      if (mw + 60 + j < p.M) put_row((char*)p.c_seam, mt * 4 + j, acc[3], j);
+  }
+  // seg_delta_pool's ref rows: only waves whose 64 rows meet a segment's range (wave-uniform test;
+  // the rows span at most two segments)
+  if (p.unp_tab && mw < p.M) {
+    auto range = [&](long long w, int& lo_, int& hi_) {
+      const int* tb = p.unp_tab + w * p.unp_ld;   // phase 0 pooled rows from tb[5], phase 2 from tb[6]
+      lo_ = min(4 * tb[5], 2 + 4 * tb[6]);
+      hi_ = max(4 * (tb[5] + p.unp_dw), 2 + 4 * (tb[6] + p.unp_dw));
+    };
+    long long wl;
+    int tl;
+    row_wt(w0, t0, 63, p.s_in, wl, tl);
+    int lo0, hi0, lo1 = 0, hi1 = 0;
+    range(w0, lo0, hi0);
+    bool hit = t0 < hi0 && (wl == w0 ? tl : p.s_in - 1) >= lo0;
+    if (wl != w0 && wl * p.s_in < p.M) {   // (a segment past the launch's rows has no table entry)
+      range(wl, lo1, hi1);
+      hit = hit || (0 < hi1 && tl >= lo1);
+    }
+    if (hit) {
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int ro = mb * 16 + 4 * fq + j;
+          if (mw + ro >= p.M) continue;
+          long long w;
+          int t;
+          row_wt(w0, t0, ro, p.s_in, w, t);
+          const int ulo = w == w0 ? lo0 : lo1, uhi = w == w0 ? hi0 : hi1;
+          if (t >= ulo && t < uhi && t - ulo < 32) put_row((char*)p.c_edge, w * 32 + (t - ulo), acc[mb], j);
+        }
+    }
+  }
+  // phase-2 partners: h01 = max of a lane's rows 0, 1; rot = the next lane group's h01
+  float* xch = (float*)(smem + 4 * H3E_WAVE);   // [wave][nb][fr]: h01 of block 0, lane group 0
+  if (wave > 0 && fq == 0) {
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) xch[(wave * NB + nb) * 16 + fr] = fmaxf(acc[0][nb][0], acc[0][nb][1]);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();   // (the producers meet it before they end)
+  asm volatile("" ::: "memory");
+  char* const lds = smem + wave * H3E_WAVE;
+  const int src = ((lane + 16) & 63) * 4;
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    float rot[4];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+      rot[mb] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, fmaxf(acc[mb][nb][0], acc[mb][nb][1]))));
+    const float nxt = wave < 3 ? xch[((wave + 1) * NB + nb) * 16 + fr] : 0.f;
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      const float m0v = fmaxf(fmaxf(acc[mb][nb][0], acc[mb][nb][1]), fmaxf(acc[mb][nb][2], acc[mb][nb][3]));
+      const float part = fq < 3 ? rot[mb] : (mb < 3 ? rot[mb + 1] : nxt);
+      const float m2v = fmaxf(fmaxf(acc[mb][nb][2], acc[mb][nb][3]), part);
+      _Float16 hi, lo;
+      split_h2(m0v, hi, lo);
+      char* d = lds + (mb * 4 + fq) * H3E_ROW + (nb >> 1) * 128 + ((nb & 1) * 16 + fr) * 2;
+      *(_Float16*)d = hi;
+      *(_Float16*)(d + 64) = lo;
+      split_h2(m2v, hi, lo);
+      d += 16 * H3E_ROW;
+      *(_Float16*)d = hi;
+      *(_Float16*)(d + 64) = lo;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll 4
+  for (int i = 0; i < (32 * CPR) / 64; ++i) {
+    const int k = i * 64 + lane, row = k / CPR, ch = k - row * CPR;
+    const int ph = row >> 4, g = row & 15;   // phase index (0: phase 0, 1: phase 2), group
+    const int ro = 4 * g + 2 * ph;          // first row of the group in the wave's 64
+    if (ph == 1 && wave == 3 && g == 15) continue;   // across the tile's end: pool2_tile_seams
+    const long long m = mw + ro;
+    if (m + 3 >= p.M) continue;
+    long long w;
+    int t;
+    row_wt(w0, t0, ro, p.s_in, w, t);
+    if (t + 3 >= p.t_valid || n0 + (ch >> 3) * 32 >= p.n_store) continue;   // group past its segment's rows
+    const long long prow = (2 * w + ph) * p.s_out + (t >> 2);
+    char* gp = (char*)p.C + (prow * ldb + (n0 >> 5)) * 128 + ch * 16;
+    *(floatx4v*)gp = *(const floatx4v*)(lds + row * H3E_ROW + ch * 16);
+  }
+  if (!(vmax < 65504.f)) *p.ovf = 1;   // overflow: the call is recomputed (bf16x6)
+}
+
 // NSB: depth of the B ring (3: loads of stage s+2 in flight during stage s; 4: s+3).
 template <int LAYER, int EPI, int TM, int NSB, int MB = 4>
 __device__ __forceinline__ void gemm_conv_h3_body(const GemmArgs& p, char* smem) {
@@ -2239,9 +2390,10 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (EPI == EPI_RELU || EPI == EPI_RELU_POOL4) {
+    if constexpr (EPI == EPI_RELU || EPI == EPI_RELU_POOL4 || EPI == EPI_POOL_PH02) {
       __builtin_amdgcn_s_barrier();                    // consumers' epilogue reuses the LDS
     }
+    if constexpr (EPI == EPI_POOL_PH02) __builtin_amdgcn_s_barrier();   // the epilogue's wave exchange
     return;
   }
 
@@ -2366,7 +2518,11 @@ __device__ __forceinline__ void gemm_conv_h3p_body(const GemmArgs& p, char* smem
     p.C[(m0 + wave * 64 + lane) % p.M] = t;
     return;
   }
-  if constexpr (EPI == EPI_RELU || EPI == EPI_RELU_POOL4) {
+  if constexpr (EPI == EPI_POOL_PH02) {
+    static_assert(NB == 10 && (TM & H3P_FUSE_CONV1) == 0, "pool phases epilogue: wide conv4 tiles");
+    __builtin_amdgcn_s_barrier();                     // producers drained their tail pieces
+    epilogue_pool_ph02<(TM & 8192) == 0>(p, acc, m0 + wave * 64, n0, lane, wave, smem);
+  } else if constexpr (EPI == EPI_RELU || EPI == EPI_RELU_POOL4) {
     __builtin_amdgcn_s_barrier();                     // producers drained their tail pieces
     if constexpr (EPI == EPI_RELU)
       epilogue_relu_h2_lds<4, (TM & 8192) == 0, NB, (TM & 512) != 0>(p, acc, m0 + wave * 64, n0, lane,

@@ -47,7 +47,7 @@ def _run(monkeypatch, env, fa, dg, vs, shifts, max_batch=2048, use_segments=True
                                  {"EXPECTO_FC_WIDE": "0", "EXPECTO_FC1_ORDER": "0", "EXPECTO_FC1_M_ORDER_MB": "0"},
                                  {"EXPECTO_FC_WIDE": "0", "EXPECTO_FC1_M_GROUP": "3"},
                                  {"EXPECTO_FC1K_SLICE": "700"}, {"EXPECTO_FC1_NARROW": "1"},
-                                 {"EXPECTO_CONV_NARROW": "1"}, {"EXPECTO_CONV_EA": "0"}])
+                                 {"EXPECTO_CONV_NARROW": "1"}, {"EXPECTO_CONV_EA": "0"}, {"EXPECTO_POOL_FUSED": "0"}])
 def test_same_bits_knobs(monkeypatch, env):
     fa, dg, vs, shifts = _setup()
     want = _run(monkeypatch, {}, fa, dg, vs, shifts)
