@@ -1733,9 +1733,10 @@ __device__ __forceinline__ void epilogue_pool_h2_lds(const GemmArgs& p, const fl
 // of each 16-row block, i.e. a phase-0 group; a phase-2 group takes this lane's rows 2, 3 and the
 // next lane group's rows 0, 1 (ds_bpermute by 16 lanes; across a 16-row block the next block's
 // register, across waves an LDS exchange).  The group across the tile's end is left to
-// pool2_tile_seams, which pools it from the two tiles' edge rows written unpooled (c_unp).
-// Pooled rows are staged per wave in LDS (rows 0..15 phase 0, 16..31 phase 2) and stored as 16-B
-// chunks like epilogue_pool_h2_lds.
+// pool2_tile_seams, which pools it from the two tiles' edge rows written unpooled (c_seam).  Rows
+// of a segment start 4-aligned in M (the caller's segment stride s_in is a multiple of 4), so t and
+// the tile-local row agree mod 4.  Pooled rows are staged per wave in LDS (rows 0..15 phase 0,
+// 16..31 phase 2) and stored as 16-B chunks like epilogue_pool_h2_lds.
 template <bool BATCH>
 __device__ __forceinline__ void epilogue_pool_ph02(const GemmArgs& p, floatx4v (&acc)[4][10], long long mw, int n0,
                                                    int lane, int wave, char* smem) {
